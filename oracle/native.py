@@ -1,0 +1,98 @@
+"""ctypes loader for oracle/build/libsd_oracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.  The
+C restatement it loads is documented in oracle/sd_oracle.c.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "libsd_oracle.so")
+_lib = None
+
+EXTENT_DTYPE = np.dtype([("size", "<u8"), ("msg_offset", "<u8"), ("msg_len", "<u4"), ("kind", "<u4")])
+
+
+def build() -> None:
+    import subprocess
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P, U64, I = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+        L.sdo_blake3.argtypes = [P, ctypes.c_size_t, P]
+        L.sdo_cas_message_len.argtypes = [U64]
+        L.sdo_cas_message_len.restype = U64
+        L.sdo_synth_fill.argtypes = [U64, ctypes.c_uint32, U64, U64, P]
+        L.sdo_synth_cas_message.argtypes = [U64, ctypes.c_uint32, U64, P]
+        L.sdo_synth_cas_message.restype = U64
+        L.sdo_cas_ids_staged.argtypes = [P, P, U64, P, I]
+        L.sdo_cas_ids_synth.argtypes = [P, P, P, U64, P, I]
+        L.sdo_checksums.argtypes = [P, P, P, U64, P, I]
+        L.sdo_checksums_synth.argtypes = [P, P, P, U64, P, I]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def blake3(data: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    lib().sdo_blake3(buf, len(data), out)
+    return out.raw
+
+
+def synth_bytes(cid: int, twin: int, offset: int, length: int) -> bytes:
+    out = np.empty(length, np.uint8)
+    lib().sdo_synth_fill(cid, twin, offset, length, _p(out))
+    return out.tobytes()
+
+
+def cas_message(cid: int, twin: int, size: int) -> bytes:
+    out = np.empty(8 + min(size, 102400) if size <= 102400 else 57352, np.uint8)
+    n = lib().sdo_synth_cas_message(cid, twin, size, _p(out))
+    return out[:n].tobytes()
+
+
+def cas_ids_synth(sizes, cids, twins=None, nthreads: int = 1) -> np.ndarray:
+    sizes = np.ascontiguousarray(sizes, np.uint64)
+    cids = np.ascontiguousarray(cids, np.uint64)
+    tw = None if twins is None else np.ascontiguousarray(twins, np.uint32)
+    out = np.empty((len(sizes), 8), np.uint8)
+    lib().sdo_cas_ids_synth(_p(sizes), _p(cids), _p(tw), len(sizes), _p(out), nthreads)
+    return out
+
+
+def cas_ids_staged(staged: np.ndarray, extents: np.ndarray, nthreads: int = 1) -> np.ndarray:
+    out = np.empty((len(extents), 8), np.uint8)
+    lib().sdo_cas_ids_staged(_p(staged), _p(extents), len(extents), _p(out), nthreads)
+    return out
+
+
+def checksums(data: np.ndarray, offsets, lens, nthreads: int = 1) -> np.ndarray:
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint64)
+    out = np.empty((len(offsets), 32), np.uint8)
+    lib().sdo_checksums(_p(data), _p(offsets), _p(lens), len(offsets), _p(out), nthreads)
+    return out
+
+
+def checksums_synth(sizes, cids, twins=None, nthreads: int = 1) -> np.ndarray:
+    sizes = np.ascontiguousarray(sizes, np.uint64)
+    cids = np.ascontiguousarray(cids, np.uint64)
+    tw = None if twins is None else np.ascontiguousarray(twins, np.uint32)
+    out = np.empty((len(sizes), 32), np.uint8)
+    lib().sdo_checksums_synth(_p(sizes), _p(cids), _p(tw), len(sizes), _p(out), nthreads)
+    return out
