@@ -1,0 +1,235 @@
+"""bench.py -- cas_id files/s (+ checksum GB/s) on 1..8 MI355X, one process per GPU.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Workload (BASELINE.json configs[4], weak-scaled): a 10 M-file synthetic library with the
+configs[0] mixture (60 % of files <= 100 KiB hashed whole, 40 % sampled), sharded by file
+index: each GPU owns ``--files-per-gpu`` (default 1 250 000 = 10 M / 8) files, so N = 8 is
+the full 10 M-file library.  One step = hash every file of the shard (sampled kernel +
+whole-file kernels) + the dedup exchange (partition by cas_id prefix, all-to-all of the
+records over RCCL, sort + group).  Inputs are resident in HBM before timing (generated on
+device from the counter-based generator; host staging + PCIe is reported separately in
+DESIGN.md, never as `value`).
+
+After the timed steps, rank 0 (N = 1 only) times the CPU baseline (oracle/sd_oracle.c,
+the C restatement of cas.rs + blake3) on a bounded sample of the same files, and every
+rank times configs[3] (full-file checksums of 16 x 4 GiB files) as `checksum`.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+SAMPLED_MSG = 57352
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--files-per-gpu", type=int, default=1_250_000)
+    p.add_argument("--checksum-gib", type=int, default=64, help="configs[3] size per GPU; 0 = skip")
+    p.add_argument("--checksum-steps", type=int, default=5)
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="target seconds per CPU-baseline leg")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_summary.json)."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        d = json.load(open(path))
+        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def cpu_baseline(sizes, cids, twins, seconds: float):
+    """Oracle C restatement on the host: hash-only over pre-staged messages."""
+    from oracle import native
+    from spacedrive_amd.device import stage_plan
+    threads = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share for one GPU
+
+    def rate(nthreads, n0):
+        n = n0
+        while True:
+            s, c, t = sizes[:n], cids[:n], twins[:n]
+            ext, total = stage_plan(s)
+            buf = native.stage_synth(s, c, t, ext["msg_offset"], total)
+            t0 = time.perf_counter()
+            native.cas_ids_staged(buf, ext, nthreads=nthreads)
+            dt = time.perf_counter() - t0
+            if dt >= seconds * 0.5 or n >= len(sizes):
+                return n, dt, float(ext["msg_len"].astype(np.float64).sum())
+            n = min(len(sizes), int(n * max(2.0, seconds / max(dt, 1e-3))))
+
+    n1, dt1, b1 = rate(1, 2000)
+    nT, dtT, bT = rate(threads, 20000)
+    return {
+        "value": nT / dtT, "unit": "files/s", "cores": threads, "kind": "port",
+        "sample": f"first {nT} files of this shard (same mixture), messages pre-staged in host RAM, "
+                  f"hash only, portable scalar C restatement (oracle/sd_oracle.c) on {threads} threads; "
+                  f"{bT / dtT / 1e9:.2f} GB/s of message bytes",
+        "single_thread": {"value": n1 / dt1, "unit": "files/s", "cores": 1, "sample_files": n1,
+                          "GBps": b1 / dt1 / 1e9},
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import spacedrive_amd as sd
+    from spacedrive_amd import dedup, synth
+
+    ctx = sd.Context(local)
+    n = args.files_per_gpu
+    start, n_total = rank * n, world * n
+    t_setup = time.time()
+    sizes, cids, twins = synth.library(start, n, n_total)
+    ext, total = sd.stage_plan(sizes)
+    dev = torch.device("cuda", local)
+    d_staged = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    d_ext = torch.from_numpy(ext.view(np.uint8).copy()).to(dev)
+    ctx.synth_stage_cas(torch.from_numpy(sizes.view(np.int64)).to(dev), torch.from_numpy(cids.view(np.int64)).to(dev),
+                        torch.from_numpy(twins.astype(np.int32)).to(dev), d_ext, n, d_staged)
+    batch = ctx.cas_batch(ext)
+    d_hash = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    d_valid = torch.from_numpy((sizes != 0).astype(np.uint8)).to(dev)  # size 0: no cas_id (mod.rs:80-88)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: {n} files ({batch.n_sampled} sampled), "
+        f"{batch.msg_bytes / 1e9:.2f} GB of messages, {batch.compressions / 1e9:.3f} G compressions")
+
+    stream = torch.cuda.current_stream()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def step(k=None):
+        if k is not None:
+            ev[k][0].record(stream)
+        batch.run_part(1, d_staged, d_hash, stream)  # k_cas_sampled
+        if k is not None:
+            ev[k][1].record(stream)
+        batch.run_part(2, d_staged, d_hash, stream)  # k_whole_leaf + k_whole_tree
+        if k is not None:
+            ev[k][2].record(stream)
+        return dedup.dedup_shard(ctx, d_hash.view(n, 32), d_valid, n, start)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        res = step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    samp_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
+    whole_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
+    recs, rep, n_groups = res
+    files_total = n_total * args.steps
+    value = files_total / elapsed
+
+    # roofline of the dominant kernel (k_cas_sampled): algorithmic bytes = staged message
+    # bytes read + 32 B hash written per sampled file; VALU = 953 compressions x 672 ops
+    samp_bytes = batch.n_sampled * (SAMPLED_MSG + 32)
+    samp_gbps = samp_bytes / (samp_ms * 1e-3) / 1e9 if samp_ms > 0 else 0.0
+    valu_peak = ctx.valu_peak()
+    samp_valu = batch.n_sampled * 953 * 672 / (samp_ms * 1e-3) if samp_ms > 0 else 0.0
+    whole_bytes = (batch.msg_bytes - batch.n_sampled * SAMPLED_MSG) + 32 * batch.n_whole
+    traffic = pmc_traffic("k_cas_sampled")
+
+    out = {
+        "metric": "cas_id files/sec (10M synthetic files) + checksum GB/s at 1/2/4/8 MI355X",
+        "value": value, "unit": "files/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic (device-generated, SURVEY.md 8(d) generator)",
+        "config": {"workload": f"10M-file library mixture (configs[0] mix: 60% <=100KiB whole-content, 40% sampled; "
+                               f"10% dups, 1% sample twins), {n} files per GPU, step = hash shard + "
+                               f"cas_id-prefix all-to-all dedup",
+                   "files_per_gpu": n, "global_files": n_total, "parallelism": f"file-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": samp_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": samp_gbps / HBM_PEAK_GBPS, "traffic": traffic, "kernel": "k_cas_sampled",
+                     "kernel_ms": samp_ms,
+                     "valu": {"achieved_lane_ops_per_s": samp_valu, "measured_peak_lane_ops_per_s": valu_peak,
+                              "frac": samp_valu / valu_peak if valu_peak else None}},
+        "kernels": {"k_cas_sampled_ms": samp_ms, "whole_file_ms": whole_ms,
+                    "whole_file_GBps": whole_bytes / (whole_ms * 1e-3) / 1e9 if whole_ms > 0 else None,
+                    "dedup_and_exchange_ms": elapsed / args.steps * 1e3 - samp_ms - whole_ms},
+        "dedup": {"records_on_rank0": int(recs.shape[0]), "groups_on_rank0": int(n_groups)},
+    }
+    del d_staged, recs, rep
+    torch.cuda.empty_cache()
+
+    # configs[3]: validator checksums, 16 files of (G/16) GiB per GPU
+    if args.checksum_gib > 0:
+        nf = 16
+        flen = (args.checksum_gib << 30) // nf
+        d_data = torch.empty(nf * flen + 128, dtype=torch.uint8, device=dev)
+        offs = [i * flen for i in range(nf)]
+        for i in range(nf):
+            ctx.synth_fill(10_000 + start + i, 0, flen, d_data[offs[i]:])
+        cb = ctx.checksum_batch(offs, [flen] * nf)
+        d_sum = torch.empty(nf * 32, dtype=torch.uint8, device=dev)
+        cb.run(d_data, d_sum, stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(args.checksum_steps):
+            cb.run(d_data, d_sum, stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ck_ms = e0.elapsed_time(e1) / args.checksum_steps
+        gbps = cb.total_bytes / (ck_ms * 1e-3) / 1e9
+        tot = torch.tensor([gbps], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tot)
+        out["checksum"] = {"GBps": float(tot.item()), "unit": "GB/s", "per_gpu_GBps": gbps, "ms_per_run": ck_ms,
+                           "workload": f"configs[3]: {nf} x {flen >> 30} GiB files per GPU, full-file BLAKE3",
+                           "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                        "frac": gbps / HBM_PEAK_GBPS,
+                                        "valu_frac": cb.compressions * 672 / (ck_ms * 1e-3) / valu_peak},
+                           "traffic": pmc_traffic("k_ck_leaf")}
+        del d_data
+        torch.cuda.empty_cache()
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(sizes, cids, twins, args.cpu_seconds)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,190 @@
+/*
+ * sd_cas.h -- C ABI of the MI355X content-addressing library (libsdcas.so).
+ *
+ * Drop-in boundary for Spacedrive's content-addressing hot path:
+ *   generate_cas_id  /root/reference/core/src/object/cas.rs:23
+ *       pub async fn generate_cas_id(path: impl AsRef<Path>, size: u64) -> Result<String, io::Error>
+ *   file_checksum    /root/reference/core/src/object/validation/hash.rs:10
+ *       pub async fn file_checksum(path: impl AsRef<Path>) -> Result<String, io::Error>
+ * The Rust signatures stay as they are; a thin shim crate calls these
+ * entry points inside tokio::task::spawn_blocking, and a batched sibling replaces the
+ * per-file join_all of identifier_job_step (core/src/object/file_identifier/mod.rs:107-134).
+ *
+ * Conventions:
+ *   - plain pointers and sizes only; the caller owns every buffer; nothing is retained
+ *     after a call returns (batches are explicit objects the caller destroys);
+ *   - every entry point is thread-safe and re-entrant: a context hands each call its own
+ *     stream and scratch from an internal pool; no C++ exception crosses the ABI (the
+ *     analogue of the reference FFI's panic::catch_unwind fence,
+ *     apps/mobile/modules/sd-core/ios/crate/src/lib.rs:36-86);
+ *   - return value: SD_OK (0) or a negative sd_rc for the whole call; per-file outcomes go
+ *     to an int32 status array (sd_file_status);
+ *   - `stream` arguments are hipStream_t passed as void* (NULL = the context's stream);
+ *     device-pointer entry points only enqueue work and do not synchronise;
+ *   - the library has no CPU fallback: without a usable gfx950 device every compute entry
+ *     point fails with SD_ERR_DEVICE.
+ */
+#ifndef SD_CAS_H
+#define SD_CAS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SD_CAS_ABI_VERSION 1
+
+/* cas.rs:10-15 */
+#define SD_SAMPLE_COUNT 4u
+#define SD_SAMPLE_SIZE 10240u
+#define SD_HEADER_OR_FOOTER_SIZE 8192u
+#define SD_MINIMUM_FILE_SIZE 102400u
+/* le64 header + head + 4 samples + tail */
+#define SD_SAMPLED_MSG_LEN 57352u
+/* staged messages start on this alignment and are zero-padded up to it */
+#define SD_STAGE_ALIGN 64u
+
+typedef enum sd_rc {
+    SD_OK = 0,
+    SD_ERR_INVALID = -1,  /* bad argument (null pointer, misaligned extent, ...) */
+    SD_ERR_DEVICE = -2,   /* HIP / device error, or no gfx950 device */
+    SD_ERR_NOMEM = -3,    /* device or pinned-host allocation failed */
+    SD_ERR_INTERNAL = -4, /* unexpected exception caught at the boundary */
+    SD_ERR_COMM = -5      /* collective (RCCL) failure */
+} sd_rc;
+
+/* per-file status, mapped back to io::ErrorKind by the Rust shim */
+typedef enum sd_file_status {
+    SD_FILE_OK = 0,
+    SD_FILE_SKIPPED_EMPTY = 1, /* FileMetadata::new skips len 0 (file_identifier/mod.rs:80-88) */
+    SD_FILE_IO_ERROR = 2,      /* open/read failed: errno in the high 16 bits */
+    SD_FILE_SHORT_READ = 3     /* read_exact hit EOF: io::ErrorKind::UnexpectedEof (cas.rs:36,43,56) */
+} sd_file_status;
+
+typedef enum sd_kind {
+    SD_KIND_WHOLE = 1,  /* size <= 102400: le64(size) || whole file          (cas.rs:27-29) */
+    SD_KIND_SAMPLED = 2 /* size  > 102400: le64(size) || head || 4 samples || tail (cas.rs:30-58) */
+} sd_kind;
+
+/* One file of a cas batch: where its hashed message sits in the staged buffer. 24 bytes. */
+typedef struct sd_extent {
+    uint64_t size;       /* file size as passed to generate_cas_id (hashed as le64)  */
+    uint64_t msg_offset; /* byte offset of the message in the staged buffer (64-B aligned) */
+    uint32_t msg_len;    /* 8 + size (WHOLE) or 57352 (SAMPLED)                      */
+    uint32_t kind;       /* sd_kind                                                  */
+} sd_extent;
+
+typedef struct sd_cas_ctx sd_cas_ctx;
+typedef struct sd_cas_batch sd_cas_batch;
+typedef struct sd_checksum_batch sd_checksum_batch;
+
+/* ---------------------------------------------------------------- context */
+int sd_cas_abi_version(void);
+/* last error message of the calling thread ("" if none) */
+const char* sd_cas_last_error(void);
+int sd_cas_ctx_create(int device, sd_cas_ctx** out);
+void sd_cas_ctx_destroy(sd_cas_ctx* ctx);
+/* pinned host staging memory (fastest H2D); free with sd_cas_host_free */
+int sd_cas_host_alloc(sd_cas_ctx* ctx, uint64_t bytes, void** out);
+void sd_cas_host_free(sd_cas_ctx* ctx, void* p);
+
+/* ---------------------------------------------------------------- staging (host) */
+/* Layout of the cas messages of n files (cas.rs:25-58): fills extents_out[n] and the
+ * staged-buffer size.  Pure host arithmetic; no device needed. */
+int sd_cas_stage_plan(const uint64_t* sizes, size_t n, sd_extent* extents_out,
+                      uint64_t* total_bytes_out);
+/* Reads one file into its extent exactly as generate_cas_id does (le64 header, whole
+ * file or head/samples/tail via pread), zero-padding to SD_STAGE_ALIGN.  Sets *status
+ * to an sd_file_status; returns SD_OK unless arguments are invalid. */
+int sd_cas_stage_file(const char* path, const sd_extent* ext, uint8_t* staged, int32_t* status);
+
+/* ---------------------------------------------------------------- cas ids */
+/* Drop-in batch: staged messages in host memory (pinned or pageable) -> n cas_ids as
+ * 16 lowercase hex chars + NUL (cas.rs:61), 17 bytes per file.  status may be NULL;
+ * entries whose status[i] != SD_FILE_OK on input are skipped and left untouched. */
+int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes,
+               const sd_extent* extents, size_t n, char* out_hex17, int32_t* status);
+
+/* Prepared batch for device-resident data: builds the work lists for these extents once
+ * (host arithmetic + one upload).  extents are host pointers. */
+int sd_cas_batch_create(sd_cas_ctx* ctx, const sd_extent* extents, size_t n, sd_cas_batch** out);
+void sd_cas_batch_destroy(sd_cas_batch* batch);
+/* Enqueue the hashing of a prepared batch: d_staged (device, >= staged size) ->
+ * d_hash32 (device, n x 32 bytes: the full BLAKE3 hash; the cas_id is its first 8). */
+int sd_cas_batch_run(sd_cas_ctx* ctx, const sd_cas_batch* batch, const uint8_t* d_staged,
+                     uint8_t* d_hash32, void* stream);
+/* Same, restricted to one part of the batch (bitmask): SD_PART_SAMPLED runs only the
+ * sampled-file kernel, SD_PART_WHOLE only the whole-file kernels (lets a caller time
+ * each kernel with events on `stream`). */
+#define SD_PART_SAMPLED 1
+#define SD_PART_WHOLE 2
+int sd_cas_batch_run_part(sd_cas_ctx* ctx, const sd_cas_batch* batch, int parts, const uint8_t* d_staged,
+                          uint8_t* d_hash32, void* stream);
+/* Statistics of a prepared batch: [0] files, [1] sampled files, [2] whole files,
+ * [3] chunks of whole files, [4] BLAKE3 compressions, [5] message bytes. */
+int sd_cas_batch_stats(const sd_cas_batch* batch, uint64_t out[6]);
+
+/* ---------------------------------------------------------------- checksums */
+/* Full-file BLAKE3 (hash.rs:10-24) of n files that are byte ranges of one device
+ * buffer.  offsets/lens are HOST arrays; each range must start 16-byte aligned and the
+ * buffer must be readable up to the next 64-byte boundary after each range. */
+int sd_checksum_batch_create(sd_cas_ctx* ctx, const uint64_t* offsets, const uint64_t* lens,
+                             size_t n, sd_checksum_batch** out);
+void sd_checksum_batch_destroy(sd_checksum_batch* batch);
+int sd_checksum_batch_run(sd_cas_ctx* ctx, const sd_checksum_batch* batch, const uint8_t* d_data,
+                          uint8_t* d_hash32, void* stream);
+/* [0] files, [1] total bytes, [2] BLAKE3 compressions, [3] 1 MiB leaf blocks */
+int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
+/* Drop-in: checksums of files on disk (path list, NUL-separated, n paths) streamed
+ * through pinned windows -> 65-byte lowercase hex (hash.rs:21-23).  status required. */
+int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65,
+                      int32_t* status);
+
+/* ---------------------------------------------------------------- dedup (post-hash) */
+/* Bucket records (cas_id as big-endian u64 of the first 8 hash bytes, global file
+ * index) by the top bits of the cas_id for an all-to-all over nparts ranks.
+ * d_hash32: n x 32 bytes on device; d_valid: n bytes (0 = skip, e.g. empty files;
+ * may be NULL).  Writes d_counts[nparts] (u64) and d_records[n] (2 x u64 each,
+ * grouped by destination, stable within a destination).  Returns the number of valid
+ * records in *n_valid (host). */
+int sd_dedup_partition(sd_cas_ctx* ctx, const uint8_t* d_hash32, const uint8_t* d_valid,
+                       uint64_t n, uint64_t global_index_base, int nparts, uint64_t* d_counts,
+                       uint64_t* d_records, uint64_t* n_valid, void* stream);
+/* Group received records by cas_id: sorts d_records[m] (in place) by (cas_id, index) and
+ * writes d_rep[m] (u64): for each record, the smallest global index with an equal
+ * cas_id -- the Object-link candidate (file_identifier/mod.rs:168-225 semantics up to
+ * the chunk-of-100 rule).  Returns the number of groups. */
+int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, uint64_t* d_rep,
+                   uint64_t* n_groups, void* stream);
+
+/* ---------------------------------------------------------------- synthetic data */
+/* Device generator of SURVEY.md §8(d) (seed 0x5D5DCA51D, splitmix64 counter stream),
+ * for benchmarks and parity tests: writes the exact cas message of each synthetic file
+ * (content id cids[i], twin tag twins[i]) into its extent.  All arrays device. */
+int sd_synth_stage_cas(sd_cas_ctx* ctx, const uint64_t* d_sizes, const uint64_t* d_cids,
+                       const uint32_t* d_twins, const sd_extent* d_extents, size_t n,
+                       uint8_t* d_staged, void* stream);
+/* bytes [0, len) of synthetic content (cid, twin) -> d_out (device) */
+int sd_synth_fill(sd_cas_ctx* ctx, uint64_t cid, uint32_t twin, uint64_t len, uint8_t* d_out,
+                  void* stream);
+
+/* ---------------------------------------------------------------- device utilities */
+int sd_device_malloc(sd_cas_ctx* ctx, uint64_t bytes, void** out);
+void sd_device_free(sd_cas_ctx* ctx, void* p);
+int sd_memcpy(sd_cas_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream);
+int sd_stream_sync(sd_cas_ctx* ctx, void* stream);
+/* Time `iters` back-to-back runs of a prepared batch with HIP events on `stream`:
+ * *ms_total = elapsed milliseconds (kernel time on that stream, no host sync inside). */
+int sd_cas_batch_time(sd_cas_ctx* ctx, const sd_cas_batch* batch, const uint8_t* d_staged,
+                      uint8_t* d_hash32, int iters, void* stream, float* ms_total);
+int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, const uint8_t* d_data,
+                           uint8_t* d_hash32, int iters, void* stream, float* ms_total);
+/* VALU integer-throughput microbenchmark: returns measured lane-ops/s (BLAKE3 ARX mix). */
+int sd_valu_peak(sd_cas_ctx* ctx, double* lane_ops_per_s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SD_CAS_H */

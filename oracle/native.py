@@ -39,6 +39,7 @@ def lib():
         L.sdo_cas_ids_synth.argtypes = [P, P, P, U64, P, I]
         L.sdo_checksums.argtypes = [P, P, P, U64, P, I]
         L.sdo_checksums_synth.argtypes = [P, P, P, U64, P, I]
+        L.sdo_stage_synth.argtypes = [P, P, P, P, U64, P]
         _lib = L
     return _lib
 
@@ -96,3 +97,14 @@ def checksums_synth(sizes, cids, twins=None, nthreads: int = 1) -> np.ndarray:
     out = np.empty((len(sizes), 32), np.uint8)
     lib().sdo_checksums_synth(_p(sizes), _p(cids), _p(tw), len(sizes), _p(out), nthreads)
     return out
+
+
+def stage_synth(sizes, cids, twins, offsets, total: int) -> np.ndarray:
+    """Host buffer holding the exact cas messages of synthetic files at `offsets`."""
+    sizes = np.ascontiguousarray(sizes, np.uint64)
+    cids = np.ascontiguousarray(cids, np.uint64)
+    tw = None if twins is None else np.ascontiguousarray(twins, np.uint32)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    buf = np.zeros(total + 64, np.uint8)
+    lib().sdo_stage_synth(_p(sizes), _p(cids), _p(tw), _p(offsets), len(sizes), _p(buf))
+    return buf

@@ -320,3 +320,10 @@ void sdo_checksums_synth(const uint64_t* sizes, const uint64_t* cids, const uint
     j.out = out32; j.out_stride = 32;
     run_job(&j, nthreads);
 }
+
+/* stage the exact cas messages of synthetic files at the given offsets (host buffer) */
+void sdo_stage_synth(const uint64_t* sizes, const uint64_t* cids, const uint32_t* twins,
+                     const uint64_t* offsets, uint64_t n, uint8_t* buf) {
+    for (uint64_t i = 0; i < n; i++)
+        sdo_synth_cas_message(cids[i], twins ? twins[i] : 0, sizes[i], buf + offsets[i]);
+}

@@ -1,0 +1,17 @@
+"""spacedrive_amd -- MI355X-native content addressing for Spacedrive.
+
+The hot path of the reference (cavellblood/spacedrive):
+  * ``generate_cas_id``  core/src/object/cas.rs:23-62      (sampled BLAKE3 cas_id)
+  * ``file_checksum``    core/src/object/validation/hash.rs:10-24 (full-file BLAKE3)
+  * the post-hash cas_id -> Object grouping, sharded over GPUs by cas_id prefix
+re-implemented as hand-written gfx950 HIP kernels behind the C ABI in include/sd_cas.h
+(``libsdcas.so``).  See DESIGN.md.
+"""
+from ._native import SdCasError, lib  # noqa: F401  (raises ImportError if libsdcas.so is missing)
+from .cas import (FileMetadata, UnexpectedEofError, file_checksum, file_checksums,  # noqa: F401
+                  generate_cas_id, generate_cas_ids)
+from .device import CasBatch, ChecksumBatch, Context, default_context, stage_plan  # noqa: F401
+
+__all__ = ["generate_cas_id", "generate_cas_ids", "file_checksum", "file_checksums", "FileMetadata",
+           "UnexpectedEofError", "Context", "CasBatch", "ChecksumBatch", "default_context", "stage_plan",
+           "SdCasError"]

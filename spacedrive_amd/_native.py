@@ -1,0 +1,106 @@
+"""Loader for the in-tree HIP library ``spacedrive_amd/libsdcas.so`` (C ABI: include/sd_cas.h).
+
+There is no CPU fallback: importing the product path without the built library raises,
+and every compute entry point of the library fails with SD_ERR_DEVICE when no gfx950
+device is present.
+
+torch is imported first on purpose: the torch wheel ships its own ``libamdhip64.so.7``
+and the library's ``NEEDED libamdhip64.so.7`` must bind to that same copy, so that one
+HIP runtime serves torch's allocations, streams and RCCL and our kernels alike.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  -- must precede the CDLL load (one HIP runtime per process)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsdcas.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "sd_cas.h")
+
+SD_OK = 0
+RC_NAMES = {0: "SD_OK", -1: "SD_ERR_INVALID", -2: "SD_ERR_DEVICE", -3: "SD_ERR_NOMEM",
+            -4: "SD_ERR_INTERNAL", -5: "SD_ERR_COMM"}
+SD_FILE_OK, SD_FILE_SKIPPED_EMPTY, SD_FILE_IO_ERROR, SD_FILE_SHORT_READ = 0, 1, 2, 3
+SD_KIND_WHOLE, SD_KIND_SAMPLED = 1, 2
+SAMPLED_MSG_LEN = 57352
+STAGE_ALIGN = 64
+
+
+class SdCasError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__(f"{RC_NAMES.get(rc, rc)}: {msg}")
+        self.rc = rc
+
+
+class Extent(ctypes.Structure):
+    _fields_ = [("size", ctypes.c_uint64), ("msg_offset", ctypes.c_uint64),
+                ("msg_len", ctypes.c_uint32), ("kind", ctypes.c_uint32)]
+
+
+_lib = None
+
+P = ctypes.c_void_p
+U64 = ctypes.c_uint64
+U32 = ctypes.c_uint32
+I32 = ctypes.c_int
+SZ = ctypes.c_size_t
+PU64 = ctypes.POINTER(ctypes.c_uint64)
+
+# (name, restype, argtypes) -- exactly the exports of include/sd_cas.h
+SIGNATURES = [
+    ("sd_cas_abi_version", I32, []),
+    ("sd_cas_last_error", ctypes.c_char_p, []),
+    ("sd_cas_ctx_create", I32, [I32, ctypes.POINTER(P)]),
+    ("sd_cas_ctx_destroy", None, [P]),
+    ("sd_cas_host_alloc", I32, [P, U64, ctypes.POINTER(P)]),
+    ("sd_cas_host_free", None, [P, P]),
+    ("sd_cas_stage_plan", I32, [P, SZ, P, PU64]),
+    ("sd_cas_stage_file", I32, [ctypes.c_char_p, P, P, ctypes.POINTER(ctypes.c_int32)]),
+    ("sd_cas_ids", I32, [P, P, U64, P, SZ, P, P]),
+    ("sd_cas_batch_create", I32, [P, P, SZ, ctypes.POINTER(P)]),
+    ("sd_cas_batch_destroy", None, [P]),
+    ("sd_cas_batch_run", I32, [P, P, P, P, P]),
+    ("sd_cas_batch_run_part", I32, [P, P, I32, P, P, P]),
+    ("sd_cas_batch_stats", I32, [P, P]),
+    ("sd_checksum_batch_create", I32, [P, P, P, SZ, ctypes.POINTER(P)]),
+    ("sd_checksum_batch_destroy", None, [P]),
+    ("sd_checksum_batch_run", I32, [P, P, P, P, P]),
+    ("sd_checksum_batch_stats", I32, [P, P]),
+    ("sd_file_checksums", I32, [P, P, SZ, P, P]),
+    ("sd_dedup_partition", I32, [P, P, P, U64, U64, I32, P, P, PU64, P]),
+    ("sd_dedup_group", I32, [P, P, U64, P, PU64, P]),
+    ("sd_synth_stage_cas", I32, [P, P, P, P, P, SZ, P, P]),
+    ("sd_synth_fill", I32, [P, U64, U32, U64, P, P]),
+    ("sd_device_malloc", I32, [P, U64, ctypes.POINTER(P)]),
+    ("sd_device_free", None, [P, P]),
+    ("sd_memcpy", I32, [P, P, P, U64, P]),
+    ("sd_stream_sync", I32, [P, P]),
+    ("sd_cas_batch_time", I32, [P, P, P, P, I32, P, ctypes.POINTER(ctypes.c_float)]),
+    ("sd_checksum_batch_time", I32, [P, P, P, P, I32, P, ctypes.POINTER(ctypes.c_float)]),
+    ("sd_valu_peak", I32, [P, ctypes.POINTER(ctypes.c_double)]),
+]
+
+
+def lib():
+    """The loaded library; raises ImportError (no fallback) if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950). spacedrive_amd has no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != SD_OK:
+        msg = lib().sd_cas_last_error()
+        raise SdCasError(rc, msg.decode() if msg else "")

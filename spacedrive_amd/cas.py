@@ -1,0 +1,171 @@
+"""Host-side mirror of the reference's content-addressing interface.
+
+Same names, argument meaning and error behaviour as the Rust functions they replace:
+
+* ``generate_cas_id(path, size) -> str``  -- core/src/object/cas.rs:23-62
+  (16 lowercase hex chars; the ``size`` argument is hashed as le64 exactly as given,
+  and selects whole-file (``size <= 102400``) or sampled hashing).
+* ``file_checksum(path) -> str``          -- core/src/object/validation/hash.rs:10-24
+  (64 lowercase hex chars).
+* ``FileMetadata.new(path)``              -- core/src/object/file_identifier/mod.rs:59-97
+  (``cas_id`` is ``None`` for an empty file; directories are rejected).
+
+I/O errors surface as ``OSError`` (the reference's ``io::Error``); a file shorter than
+the ``size`` it was planned with raises ``UnexpectedEofError`` (``read_exact``'s
+``io::ErrorKind::UnexpectedEof``, cas.rs:36,43,56).  The batched variants return one
+result or exception per input, which lets callers keep the reference's per-caller
+policy (identifier: log and drop, file_identifier/mod.rs:127-128; validator: abort the
+step, validator_job.rs:147-149).
+
+Hashing always runs in libsdcas.so on the GPU; there is no CPU path here.
+"""
+from __future__ import annotations
+
+import ctypes
+import errno as _errno
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Union
+
+import numpy as np
+
+from ._native import (SD_FILE_IO_ERROR, SD_FILE_OK, SD_FILE_SHORT_READ, check, lib)
+from .device import _ptr, default_context, stage_plan
+
+MINIMUM_FILE_SIZE = 1024 * 100  # cas.rs:15
+
+
+class UnexpectedEofError(OSError):
+    """io::ErrorKind::UnexpectedEof from read_exact (cas.rs:36,43,56)."""
+
+
+def _status_error(st: int, path: str) -> OSError:
+    code = st & 0xFFFF
+    if code == SD_FILE_SHORT_READ:
+        return UnexpectedEofError(_errno.EIO, "failed to fill whole buffer", path)
+    if code == SD_FILE_IO_ERROR:
+        err = (st >> 16) & 0xFFFF
+        return OSError(err, os.strerror(err), path)
+    return OSError(_errno.EIO, f"sd_cas status {st}", path)
+
+
+class _PinnedHost:
+    """Pinned host staging buffer from sd_cas_host_alloc, viewed as numpy."""
+
+    def __init__(self, ctx, nbytes: int):
+        self.ctx = ctx
+        p = ctypes.c_void_p()
+        check(lib().sd_cas_host_alloc(ctx.handle, max(nbytes, 16), ctypes.byref(p)))
+        self.ptr = p
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(nbytes, 16)).from_address(p.value))
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().sd_cas_host_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+
+def generate_cas_ids(paths: Sequence[Union[str, os.PathLike]], sizes: Sequence[int],
+                     device: Optional[int] = None) -> List[Union[str, OSError]]:
+    """Batched generate_cas_id: one cas_id string or OSError per (path, size)."""
+    n = len(paths)
+    if n != len(sizes):
+        raise ValueError("paths and sizes differ in length")
+    if n == 0:
+        return []
+    ctx = default_context(device)
+    ext, total = stage_plan(sizes)
+    staged = _PinnedHost(ctx, total)
+    try:
+        status = np.zeros(n, np.int32)
+        L = lib()
+        for i, p in enumerate(paths):  # pread of header/samples/tail or the whole file
+            st = ctypes.c_int32(0)
+            check(L.sd_cas_stage_file(os.fsencode(p), ctypes.c_void_p(ext.ctypes.data + 24 * i),
+                                      staged.ptr, ctypes.byref(st)))
+            status[i] = st.value
+        out = ctypes.create_string_buffer(17 * n)
+        check(L.sd_cas_ids(ctx.handle, staged.ptr, total, _ptr(ext), n, out, _ptr(status)))
+    finally:
+        staged.free()
+    raw = out.raw
+    res: List[Union[str, OSError]] = []
+    for i in range(n):
+        if status[i] == SD_FILE_OK:
+            res.append(raw[17 * i:17 * i + 16].decode())
+        else:
+            res.append(_status_error(int(status[i]), os.fsdecode(paths[i])))
+    return res
+
+
+def generate_cas_id(path: Union[str, os.PathLike], size: int, device: Optional[int] = None) -> str:
+    """cas.rs:23 ``generate_cas_id(path, size) -> Result<String, io::Error>``."""
+    r = generate_cas_ids([path], [size], device)[0]
+    if isinstance(r, OSError):
+        raise r
+    return r
+
+
+def file_checksums(paths: Sequence[Union[str, os.PathLike]],
+                   device: Optional[int] = None) -> List[Union[str, OSError]]:
+    """Batched file_checksum: one 64-hex string or OSError per path."""
+    n = len(paths)
+    if n == 0:
+        return []
+    ctx = default_context(device)
+    enc = [os.fsencode(p) for p in paths]
+    arr = (ctypes.c_char_p * n)(*enc)
+    out = ctypes.create_string_buffer(65 * n)
+    status = np.zeros(n, np.int32)
+    check(lib().sd_file_checksums(ctx.handle, arr, n, out, _ptr(status)))
+    raw = out.raw
+    return [raw[65 * i:65 * i + 64].decode() if status[i] == SD_FILE_OK
+            else _status_error(int(status[i]), os.fsdecode(paths[i])) for i in range(n)]
+
+
+def file_checksum(path: Union[str, os.PathLike], device: Optional[int] = None) -> str:
+    """hash.rs:10 ``file_checksum(path) -> Result<String, io::Error>``."""
+    r = file_checksums([path], device)[0]
+    if isinstance(r, OSError):
+        raise r
+    return r
+
+
+@dataclass
+class FileMetadata:
+    """file_identifier/mod.rs:50-55 (kind detection is out of scope: SURVEY.md §2)."""
+
+    cas_id: Optional[str]
+    size: int
+
+    @staticmethod
+    def new(path: Union[str, os.PathLike], device: Optional[int] = None) -> "FileMetadata":
+        r = FileMetadata.batch([path], device)[0]
+        if isinstance(r, OSError):
+            raise r
+        return r
+
+    @staticmethod
+    def batch(paths: Sequence[Union[str, os.PathLike]],
+              device: Optional[int] = None) -> List[Union["FileMetadata", OSError]]:
+        """mod.rs:59-97 for a whole identifier step: stat, skip empty files, hash the rest."""
+        out: List[Union[FileMetadata, OSError, None]] = [None] * len(paths)
+        todo, sizes = [], []
+        for i, p in enumerate(paths):
+            try:
+                st = os.stat(p)
+            except OSError as e:  # mod.rs:65-67
+                out[i] = e
+                continue
+            if os.path.isdir(p):  # mod.rs:69-72
+                raise AssertionError("We can't generate cas_id for directories")
+            if st.st_size == 0:  # mod.rs:80-88
+                out[i] = FileMetadata(None, 0)
+            else:
+                todo.append(i)
+                sizes.append(st.st_size)
+        if todo:
+            ids = generate_cas_ids([paths[i] for i in todo], sizes, device)
+            for i, s, r in zip(todo, sizes, ids):
+                out[i] = r if isinstance(r, OSError) else FileMetadata(r, s)
+        return out  # type: ignore[return-value]

@@ -1,0 +1,318 @@
+// cas_kernels.hip -- gfx950 kernels for Spacedrive's content-addressing hot path.
+//
+//   k_cas_sampled   generate_cas_id, size > 102400 (cas.rs:30-58): every message is the
+//                   same 57 352 B = 56 full chunks + one 8-byte chunk, so a workgroup of
+//                   7 waves hashes 8 files with one lane per full chunk and merges the
+//                   8 x 57 chaining values level-wise in LDS.  No work lists.
+//   k_whole_leaf    generate_cas_id, size <= 102400 (cas.rs:27-29): one lane per chunk of
+//   k_whole_tree    a host-sorted (msg_len descending) file list; single-chunk files end
+//                   in the leaf kernel (ROOT on their last block), multi-chunk files are
+//                   merged by one lane each, in place, in the chaining-value buffer.
+//   k_ck_leaf       file_checksum (hash.rs:10-24): one 256-lane workgroup per 1 MiB of a
+//   k_ck_reduce     file, 4 consecutive chunks per lane merged in-lane, 256 lane CVs
+//                   merged in LDS; then 256-way LDS reductions over the block CVs.
+//
+// Tree shape: every merge is the level-wise pairwise merge with the odd node carried up
+// unchanged, over power-of-two aligned groups.  It is the BLAKE3 tree (left subtree =
+// largest power of two); tests/test_oracle.py checks the equivalence for 1..600 chunks.
+#include <hip/hip_runtime.h>
+
+#include "blake3_device.h"
+#include "sd_internal.h"
+
+using namespace sdb3;
+
+namespace {
+
+__device__ __forceinline__ void store_cv(uint32_t* dst, const uint32_t (&cv)[8]) {
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    d[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
+    d[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
+}
+__device__ __forceinline__ void load_cv(uint32_t (&cv)[8], const uint32_t* src) {
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4 a = s[0], b = s[1];
+    cv[0] = a.x; cv[1] = a.y; cv[2] = a.z; cv[3] = a.w;
+    cv[4] = b.x; cv[5] = b.y; cv[6] = b.z; cv[7] = b.w;
+}
+
+// Level-wise merge of n (1..blockDim) CVs held in lds[0..n) -> lds[0].  ROOT goes on the
+// final parent when `root`.  Every thread of the workgroup must call it.
+__device__ void lds_reduce(uint32_t (*lds)[8], uint32_t n, bool root) {
+    const uint32_t t = threadIdx.x;
+    while (n > 1) {
+        const uint32_t P = n >> 1;
+        const bool carry = n & 1u;
+        uint32_t res[8];
+        bool have = false;
+        if (t < P) {
+            uint32_t l[8], r[8];
+            load_cv(l, lds[2 * t]);
+            load_cv(r, lds[2 * t + 1]);
+            parent(res, l, r, (root && n == 2) ? ROOT : 0u);
+            have = true;
+        } else if (carry && t == P) {
+            load_cv(res, lds[n - 1]);
+            have = true;
+        }
+        __syncthreads();
+        if (have) store_cv(lds[t], res);
+        __syncthreads();
+        n = P + (carry ? 1u : 0u);
+    }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------ sampled cas
+constexpr int S_FILES = 8;       // files per workgroup
+constexpr int S_FULL = 56;       // full chunks per sampled message (57344 bytes)
+constexpr int S_NODES = 57;      // + the 8-byte tail chunk
+constexpr int S_THREADS = S_FILES * S_FULL;  // 448 = 7 waves
+
+__global__ __launch_bounds__(S_THREADS) void k_cas_sampled(const uint8_t* __restrict__ staged,
+                                                           const sd_extent* __restrict__ ext,
+                                                           const uint32_t* __restrict__ idx,
+                                                           uint32_t n, uint32_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t cvs[S_FILES][S_NODES][8];
+    const uint32_t t = threadIdx.x;
+    const uint32_t f = t / S_FULL, c = t % S_FULL;
+    const uint32_t g = blockIdx.x * S_FILES + f;
+    if (g < n) {
+        const uint8_t* msg = staged + ext[idx[g]].msg_offset;
+        uint32_t cv[8];
+        full_chunk_cv(cv, msg + (size_t)c * CHUNK_LEN, c);
+        store_cv(cvs[f][c], cv);
+    }
+    if (t < S_FILES) {  // the 8-byte tail chunk (chunk 56: message bytes 57344..57351)
+        const uint32_t gt = blockIdx.x * S_FILES + t;
+        if (gt < n) {
+            const uint8_t* msg = staged + ext[idx[gt]].msg_offset;
+            uint32_t cv[8];
+            chunk_cv(cv, msg + (size_t)S_FULL * CHUNK_LEN, SD_SAMPLED_MSG_LEN - S_FULL * CHUNK_LEN, S_FULL,
+                     false);
+            store_cv(cvs[t][S_FULL], cv);
+        }
+    }
+    __syncthreads();
+    // 57 -> 29 -> 15 -> 8 -> 4 -> 2 -> 1, 8 files side by side
+    uint32_t nodes = S_NODES;
+#pragma unroll 1
+    while (nodes > 1) {
+        const uint32_t P = nodes >> 1;
+        const bool carry = nodes & 1u;
+        uint32_t res[8];
+        bool have = false;
+        uint32_t ff = 0, p = 0;
+        if (t < S_FILES * P) {
+            ff = t / P; p = t % P;
+            uint32_t l[8], r[8];
+            load_cv(l, cvs[ff][2 * p]);
+            load_cv(r, cvs[ff][2 * p + 1]);
+            parent(res, l, r, nodes == 2 ? ROOT : 0u);
+            have = true;
+        } else if (carry && t >= 256 && t < 256 + S_FILES) {  // a wave with no parent work
+            ff = t - 256; p = P;
+            load_cv(res, cvs[ff][nodes - 1]);
+            have = true;
+        }
+        __syncthreads();
+        if (have) store_cv(cvs[ff][p], res);
+        __syncthreads();
+        nodes = P + (carry ? 1u : 0u);
+    }
+    if (t < S_FILES * 8) {
+        const uint32_t ff = t >> 3, w = t & 7;
+        const uint32_t gg = blockIdx.x * S_FILES + ff;
+        if (gg < n) out[(size_t)idx[gg] * 8 + w] = cvs[ff][0][w];
+    }
+}
+
+// ------------------------------------------------------------------ whole-file cas
+// chunk_prefix[k]: first global chunk of sorted file k (k = 0..nw, prefix[nw] = total).
+// hint[w]: sorted file holding chunk 64*w.
+__global__ __launch_bounds__(256) void k_whole_leaf(const uint8_t* __restrict__ staged,
+                                                    const sd_extent* __restrict__ ext,
+                                                    const uint32_t* __restrict__ order,
+                                                    const uint32_t* __restrict__ chunk_prefix,
+                                                    const uint32_t* __restrict__ hint, uint32_t nw,
+                                                    uint32_t total_chunks, uint32_t* __restrict__ cvbuf,
+                                                    uint32_t* __restrict__ out) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total_chunks) return;
+    const uint32_t w = g >> 6;
+    uint32_t lo = hint[w], hi = hint[w + 1];
+    if (hi > nw - 1) hi = nw - 1;
+    while (lo < hi) {  // largest k in [lo, hi] with chunk_prefix[k] <= g
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (chunk_prefix[mid] <= g) lo = mid; else hi = mid - 1;
+    }
+    const uint32_t k = lo;
+    const uint32_t file = order[k];
+    const uint32_t c = g - chunk_prefix[k];
+    const uint32_t C = chunk_prefix[k + 1] - chunk_prefix[k];
+    const sd_extent e = ext[file];
+    const uint32_t rem = e.msg_len - c * CHUNK_LEN;
+    const uint32_t len = rem < CHUNK_LEN ? rem : CHUNK_LEN;
+    uint32_t cv[8];
+    chunk_cv(cv, staged + e.msg_offset + (size_t)c * CHUNK_LEN, len, c, C == 1);
+    if (C == 1) store_cv(out + (size_t)file * 8, cv);
+    else store_cv(cvbuf + (size_t)g * 8, cv);
+}
+
+// one lane per multi-chunk file (sorted files 0..n_multi-1 all have C >= 2)
+__global__ __launch_bounds__(256) void k_whole_tree(const uint32_t* __restrict__ order,
+                                                    const uint32_t* __restrict__ chunk_prefix, uint32_t n_multi,
+                                                    uint32_t* __restrict__ cvbuf, uint32_t* __restrict__ out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_multi) return;
+    uint32_t* base = cvbuf + (size_t)chunk_prefix[k] * 8;
+    uint32_t n = chunk_prefix[k + 1] - chunk_prefix[k];
+    uint32_t res[8];
+    while (n > 1) {  // in place: parent p is written after nodes 2p, 2p+1 were read
+        const uint32_t P = n >> 1;
+        for (uint32_t p = 0; p < P; p++) {
+            uint32_t l[8], r[8];
+            load_cv(l, base + (size_t)(2 * p) * 8);
+            load_cv(r, base + (size_t)(2 * p + 1) * 8);
+            parent(res, l, r, n == 2 ? ROOT : 0u);
+            if (n != 2) store_cv(base + (size_t)p * 8, res);
+        }
+        if (n & 1u) {
+            uint32_t cv[8];
+            load_cv(cv, base + (size_t)(n - 1) * 8);
+            store_cv(base + (size_t)P * 8, cv);
+        }
+        n = P + (n & 1u);
+    }
+    store_cv(out + (size_t)order[k] * 8, res);
+}
+
+// ------------------------------------------------------------------------ checksums
+// Leaf: workgroup (256 lanes) = 1 MiB block = 1024 chunks of one file; lane l hashes
+// chunks [4l, 4l+4) and merges them in-lane; then the lane CVs merge in LDS.
+constexpr uint32_t CK_LANE_CHUNKS = 4;
+constexpr uint32_t CK_BLOCK_CHUNKS = 1024;
+
+__global__ __launch_bounds__(256) void k_ck_leaf(const uint8_t* __restrict__ data, uint64_t shift,
+                                                 const ck_file* __restrict__ files,
+                                                 const uint2* __restrict__ wg_map,
+                                                 uint32_t* __restrict__ cvbuf, uint32_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[256][8];
+    const uint2 wm = wg_map[blockIdx.x];  // (file, block)
+    const ck_file fi = files[wm.x];
+    const uint64_t nchunks = fi.len == 0 ? 1 : (fi.len + CHUNK_LEN - 1) / CHUNK_LEN;
+    const uint64_t blk0 = (uint64_t)wm.y * CK_BLOCK_CHUNKS;
+    const uint64_t blk_chunks64 = nchunks - blk0 < CK_BLOCK_CHUNKS ? nchunks - blk0 : CK_BLOCK_CHUNKS;
+    const uint32_t blk_chunks = (uint32_t)blk_chunks64;
+    const uint32_t t = threadIdx.x;
+    const uint32_t c0 = t * CK_LANE_CHUNKS;
+    const bool file_is_lane = nchunks <= CK_LANE_CHUNKS;  // whole file inside lane 0
+    if (c0 < blk_chunks) {
+        const uint32_t nch = blk_chunks - c0 < CK_LANE_CHUNKS ? blk_chunks - c0 : CK_LANE_CHUNKS;
+        const uint8_t* p = data + (fi.offset - shift);  // shift: window start when streaming
+        uint32_t acc[8], cv[8], tmp[8];
+        for (uint32_t j = 0; j < nch; j++) {
+            const uint64_t ci = blk0 + c0 + j;
+            const uint64_t rem = fi.len - ci * CHUNK_LEN;
+            const uint32_t len = fi.len == 0 ? 0u : (rem < CHUNK_LEN ? (uint32_t)rem : CHUNK_LEN);
+            if (len == CHUNK_LEN && !(file_is_lane && nchunks == 1)) full_chunk_cv(cv, p + ci * CHUNK_LEN, ci);
+            else chunk_cv(cv, p + ci * CHUNK_LEN, len, ci, nchunks == 1);
+            // level-wise in-lane merge of up to 4 chunks: ((0,1),(2,3)) or ((0,1),2)
+            if (j == 0) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) acc[i] = cv[i];
+            } else if (j == 1) {
+                const bool root = file_is_lane && nch == 2;
+                parent(tmp, acc, cv, root ? ROOT : 0u);
+#pragma unroll
+                for (int i = 0; i < 8; i++) acc[i] = tmp[i];
+            } else if (j == 2) {
+                if (nch == 3) {
+                    parent(tmp, acc, cv, file_is_lane ? ROOT : 0u);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) acc[i] = tmp[i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) tmp[i] = cv[i];  // hold chunk 2
+                }
+            } else {
+                uint32_t p23[8];
+                parent(p23, tmp, cv, 0u);
+                parent(tmp, acc, p23, file_is_lane ? ROOT : 0u);
+#pragma unroll
+                for (int i = 0; i < 8; i++) acc[i] = tmp[i];
+            }
+        }
+        store_cv(lds[t], acc);
+    }
+    __syncthreads();
+    const uint32_t lanes = (blk_chunks + CK_LANE_CHUNKS - 1) / CK_LANE_CHUNKS;
+    const bool file_is_block = nchunks <= CK_BLOCK_CHUNKS;
+    lds_reduce(lds, lanes, file_is_block && !file_is_lane);
+    if (t < 8) {
+        if (file_is_block) out[(size_t)wm.x * 8 + t] = lds[0][t];
+        else cvbuf[(fi.cv_base + wm.y) * 8 + t] = lds[0][t];
+    }
+}
+
+// Reduce: workgroup = up to 256 consecutive CVs of one file's level; writes one CV to the
+// next level, or the root hash when the level fits one group.
+__global__ __launch_bounds__(256) void k_ck_reduce(const uint32_t* __restrict__ src,
+                                                   uint32_t* __restrict__ dst,
+                                                   const ck_reduce_wg* __restrict__ wgs,
+                                                   uint32_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[256][8];
+    const ck_reduce_wg w = wgs[blockIdx.x];
+    const uint32_t t = threadIdx.x;
+    if (t < w.count) {
+        uint32_t cv[8];
+        load_cv(cv, src + (w.src_base + t) * 8);
+        store_cv(lds[t], cv);
+    }
+    __syncthreads();
+    lds_reduce(lds, w.count, w.is_root != 0);
+    if (t < 8) {
+        if (w.is_root) out[(size_t)w.file * 8 + t] = lds[0][t];
+        else dst[w.dst_index * 8 + t] = lds[0][t];
+    }
+}
+
+// --------------------------------------------------------------------- launchers
+namespace sdk {
+
+hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const uint32_t* idx, uint32_t n,
+                              uint32_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t grid = (n + S_FILES - 1) / S_FILES;
+    hipLaunchKernelGGL(k_cas_sampled, dim3(grid), dim3(S_THREADS), 0, s, staged, ext, idx, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_whole(const uint8_t* staged, const sd_extent* ext, const uint32_t* order,
+                        const uint32_t* chunk_prefix, const uint32_t* hint, uint32_t nw, uint32_t total_chunks,
+                        uint32_t n_multi, uint32_t* cvbuf, uint32_t* out, hipStream_t s) {
+    if (nw == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_whole_leaf, dim3((total_chunks + 255) / 256), dim3(256), 0, s, staged, ext, order,
+                       chunk_prefix, hint, nw, total_chunks, cvbuf, out);
+    if (n_multi)
+        hipLaunchKernelGGL(k_whole_tree, dim3((n_multi + 255) / 256), dim3(256), 0, s, order, chunk_prefix,
+                           n_multi, cvbuf, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_ck_leaf(const uint8_t* data, uint64_t shift, const ck_file* files, const uint2* wg_map,
+                          uint32_t n_wg, uint32_t* cvbuf, uint32_t* out, hipStream_t s) {
+    if (n_wg == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ck_leaf, dim3(n_wg), dim3(256), 0, s, data, shift, files, wg_map, cvbuf, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_ck_reduce(const uint32_t* src, uint32_t* dst, const ck_reduce_wg* wgs, uint32_t n_wg,
+                            uint32_t* out, hipStream_t s) {
+    if (n_wg == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ck_reduce, dim3(n_wg), dim3(256), 0, s, src, dst, wgs, out);
+    return hipGetLastError();
+}
+
+}  // namespace sdk

@@ -1,0 +1,891 @@
+// sd_cas_api.cpp -- host side of the C ABI declared in include/sd_cas.h.
+//
+// Replaces, behind `extern "C"`, the per-file calls
+//   generate_cas_id   /root/reference/core/src/object/cas.rs:23-62
+//   file_checksum     /root/reference/core/src/object/validation/hash.rs:10-24
+// with batched calls that stage messages on the host and hash them with the gfx950
+// kernels of cas_kernels.hip.  Thread-safety: a context owns a mutex-protected pool of
+// streams; prepared batches own their scratch (one run of a batch at a time).  Every
+// entry point catches all C++ exceptions (the reference FFI fences panics with
+// catch_unwind, apps/mobile/modules/sd-core/ios/crate/src/lib.rs:41,60).
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "sd_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+struct sd_failure : std::runtime_error {
+    int rc;
+    sd_failure(int r, const std::string& m) : std::runtime_error(m), rc(r) {}
+};
+
+#define HIP_CHECK(expr)                                                                              \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess)                                                                        \
+            throw sd_failure(e_ == hipErrorOutOfMemory ? SD_ERR_NOMEM : SD_ERR_DEVICE,              \
+                             std::string(#expr) + ": " + hipGetErrorString(e_));                    \
+    } while (0)
+
+#define SD_GUARD_BEGIN try {
+#define SD_GUARD_END                                   \
+    }                                                  \
+    catch (const sd_failure& f) {                      \
+        set_err("%s", f.what());                       \
+        return f.rc;                                   \
+    }                                                  \
+    catch (const std::bad_alloc&) {                    \
+        set_err("host allocation failed");             \
+        return SD_ERR_NOMEM;                           \
+    }                                                  \
+    catch (const std::exception& ex) {                 \
+        set_err("internal error: %s", ex.what());      \
+        return SD_ERR_INTERNAL;                        \
+    }                                                  \
+    catch (...) {                                      \
+        set_err("internal error");                     \
+        return SD_ERR_INTERNAL;                        \
+    }
+
+inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+// RAII device buffer
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void alloc(size_t n) {
+        reset();
+        if (n == 0) n = 16;
+        HIP_CHECK(hipMalloc(&p, n));
+        bytes = n;
+    }
+    void ensure(size_t n) {
+        if (n > bytes) alloc(n);
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+    template <class T>
+    void upload(const std::vector<T>& v) {
+        alloc(v.size() * sizeof(T));
+        if (!v.empty()) HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    }
+};
+
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~PinnedBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void ensure(size_t n) {
+        if (n <= bytes) return;
+        reset();
+        HIP_CHECK(hipHostMalloc(&p, n, hipHostMallocDefault));
+        bytes = n;
+    }
+};
+
+// per-call working set of the host drop-in entry points
+struct Slot {
+    hipStream_t stream = nullptr;
+    DevBuf staged, hashes;
+    PinnedBuf host_hashes, window;
+};
+
+}  // namespace
+
+struct sd_cas_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::vector<std::unique_ptr<Slot>> free_slots;
+
+    std::unique_ptr<Slot> acquire() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!free_slots.empty()) {
+                auto s = std::move(free_slots.back());
+                free_slots.pop_back();
+                return s;
+            }
+        }
+        auto s = std::make_unique<Slot>();
+        HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        return s;
+    }
+    void release(std::unique_ptr<Slot> s) {
+        std::lock_guard<std::mutex> g(mu);
+        free_slots.push_back(std::move(s));
+    }
+    void bind() { HIP_CHECK(hipSetDevice(device)); }
+    hipStream_t pick(void* s) const { return s ? reinterpret_cast<hipStream_t>(s) : stream; }
+};
+
+struct sd_cas_batch {
+    size_t n = 0;
+    uint32_t n_sampled = 0, n_whole = 0, n_multi = 0;
+    uint32_t total_chunks = 0;
+    uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0;
+    DevBuf ext, sidx, order, prefix, hint, cvbuf;
+};
+
+struct ck_pass {
+    DevBuf wgs;
+    uint32_t n_wg = 0;
+    int src = 0, dst = 1;  // which CV level buffer
+};
+
+struct sd_checksum_batch {
+    size_t n = 0;
+    uint64_t total_bytes = 0, compressions = 0, blocks = 0;
+    std::vector<ck_file> files_h;
+    std::vector<uint2> wg_map_h;
+    DevBuf files, wg_map;
+    DevBuf lvl[2];
+    std::vector<std::unique_ptr<ck_pass>> passes;
+};
+
+namespace {
+
+// ----------------------------------------------------------------- cas batch planning
+uint32_t msg_chunks(uint32_t msg_len) { return msg_len == 0 ? 1u : (msg_len + 1023u) / 1024u; }
+
+uint64_t msg_compressions(uint64_t msg_len) {  // blocks in all chunks + parents
+    const uint64_t C = msg_len == 0 ? 1 : (msg_len + 1023) / 1024;
+    uint64_t blocks = 0;
+    for (uint64_t c = 0; c < C; c++) {
+        const uint64_t len = std::min<uint64_t>(1024, msg_len - c * 1024);
+        blocks += len == 0 ? 1 : (len + 63) / 64;
+    }
+    return blocks + (C - 1);
+}
+
+uint64_t file_compressions(uint64_t len) {  // same, closed form for large inputs
+    const uint64_t C = len == 0 ? 1 : (len + 1023) / 1024;
+    const uint64_t last = len - (C - 1) * 1024;
+    return (C - 1) * 16 + (last == 0 ? 1 : (last + 63) / 64) + (C - 1);
+}
+
+void validate_extent(const sd_extent& e, size_t i) {
+    const bool whole = e.size <= SD_MINIMUM_FILE_SIZE;
+    const uint64_t want = whole ? 8 + e.size : SD_SAMPLED_MSG_LEN;
+    if (e.kind != (whole ? SD_KIND_WHOLE : SD_KIND_SAMPLED) || e.msg_len != want)
+        throw sd_failure(SD_ERR_INVALID, "extent " + std::to_string(i) + ": kind/msg_len do not match size");
+    if (e.msg_offset % 16)
+        throw sd_failure(SD_ERR_INVALID, "extent " + std::to_string(i) + ": msg_offset not 16-byte aligned");
+}
+
+sd_cas_batch* build_cas_batch(const sd_extent* ext, size_t n) {
+    if (n >= (1ull << 31)) throw sd_failure(SD_ERR_INVALID, "batch too large");
+    auto b = std::make_unique<sd_cas_batch>();
+    b->n = n;
+    std::vector<uint32_t> sidx;
+    std::vector<uint32_t> count(SD_MINIMUM_FILE_SIZE + 9 + 1, 0);
+    uint64_t end = 0;
+    for (size_t i = 0; i < n; i++) {
+        validate_extent(ext[i], i);
+        end = std::max<uint64_t>(end, align_up(ext[i].msg_offset + ext[i].msg_len, SD_STAGE_ALIGN));
+        b->msg_bytes += ext[i].msg_len;
+        if (ext[i].kind == SD_KIND_SAMPLED) {
+            sidx.push_back((uint32_t)i);
+            b->compressions += 953;  // 56 x 16 + 1 blocks, 56 parents
+        } else {
+            count[ext[i].msg_len]++;
+            b->compressions += msg_compressions(ext[i].msg_len);
+        }
+    }
+    b->staged_bytes = end;
+    b->n_sampled = (uint32_t)sidx.size();
+    b->n_whole = (uint32_t)(n - sidx.size());
+    // counting sort of whole files by msg_len, descending (uniform lanes in both kernels)
+    std::vector<uint32_t> start(count.size() + 1, 0);
+    for (size_t L = count.size(); L-- > 0;) start[L] = start[L + 1] + count[L];
+    std::vector<uint32_t> order(b->n_whole);
+    for (size_t i = 0; i < n; i++)
+        if (ext[i].kind == SD_KIND_WHOLE) order[start[ext[i].msg_len + 1]++] = (uint32_t)i;
+    std::vector<uint32_t> prefix(b->n_whole + 1, 0);
+    uint64_t total = 0;
+    for (uint32_t k = 0; k < b->n_whole; k++) {
+        prefix[k] = (uint32_t)total;
+        const uint32_t C = msg_chunks(ext[order[k]].msg_len);
+        total += C;
+        if (C >= 2) b->n_multi = k + 1;
+    }
+    if (total >= (1ull << 32)) throw sd_failure(SD_ERR_INVALID, "too many chunks in one batch");
+    prefix[b->n_whole] = (uint32_t)total;
+    b->total_chunks = (uint32_t)total;
+    const uint32_t W = (b->total_chunks + 63) / 64;
+    std::vector<uint32_t> hint(W + 1, 0);
+    {
+        uint32_t k = 0;
+        for (uint32_t w = 0; w <= W; w++) {
+            const uint64_t c = std::min<uint64_t>((uint64_t)w * 64, total ? total - 1 : 0);
+            while (k + 1 < b->n_whole && prefix[k + 1] <= c) k++;
+            hint[w] = k;
+        }
+    }
+    b->ext.alloc(n * sizeof(sd_extent));
+    if (n) HIP_CHECK(hipMemcpy(b->ext.p, ext, n * sizeof(sd_extent), hipMemcpyHostToDevice));
+    b->sidx.upload(sidx);
+    b->order.upload(order);
+    b->prefix.upload(prefix);
+    b->hint.upload(hint);
+    b->cvbuf.alloc((size_t)b->total_chunks * 32);
+    return b.release();
+}
+
+void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_hash32, hipStream_t s,
+                   int parts = SD_PART_SAMPLED | SD_PART_WHOLE) {
+    uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
+    if (parts & SD_PART_SAMPLED)
+        HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled, out,
+                                          s));
+    if (parts & SD_PART_WHOLE)
+        HIP_CHECK(sdk::launch_whole(d_staged, b->ext.as<sd_extent>(), b->order.as<uint32_t>(), b->prefix.as<uint32_t>(),
+                                b->hint.as<uint32_t>(), b->n_whole, b->total_chunks, b->n_multi,
+                                b->cvbuf.as<uint32_t>(), out, s));
+}
+
+// -------------------------------------------------------------- checksum planning
+constexpr uint64_t CK_BLOCK_BYTES = 1024ull * 1024ull;  // 1024 chunks per leaf workgroup
+
+sd_checksum_batch* build_checksum_batch(const uint64_t* offsets, const uint64_t* lens, size_t n) {
+    if (n >= (1ull << 31)) throw sd_failure(SD_ERR_INVALID, "batch too large");
+    auto b = std::make_unique<sd_checksum_batch>();
+    b->n = n;
+    b->files_h.resize(n);
+    std::vector<uint64_t> level_n;  // current level size per file
+    level_n.resize(n);
+    uint64_t cv0 = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (offsets[i] % 16) throw sd_failure(SD_ERR_INVALID, "checksum range " + std::to_string(i) + " not 16-byte aligned");
+        const uint64_t nb = lens[i] == 0 ? 1 : (lens[i] + CK_BLOCK_BYTES - 1) / CK_BLOCK_BYTES;
+        b->files_h[i] = ck_file{offsets[i], lens[i], nb > 1 ? cv0 : 0};
+        for (uint64_t k = 0; k < nb; k++) {
+            if (k >= (1ull << 32)) throw sd_failure(SD_ERR_INVALID, "file too large");
+            b->wg_map_h.push_back(make_uint2((uint32_t)i, (uint32_t)k));
+        }
+        if (nb > 1) cv0 += nb;
+        level_n[i] = nb;
+        b->total_bytes += lens[i];
+        b->compressions += file_compressions(lens[i]);
+        b->blocks += nb;
+    }
+    b->files.upload(b->files_h);
+    b->wg_map.upload(b->wg_map_h);
+    // reduce passes: groups of 256 CVs per workgroup until every file has its root
+    std::vector<uint64_t> base(n, 0);
+    for (size_t i = 0; i < n; i++) base[i] = b->files_h[i].cv_base;
+    size_t lvl_cap[2] = {cv0, 0};
+    int src = 0;
+    for (;;) {
+        std::vector<ck_reduce_wg> wgs;
+        uint64_t dst_total = 0;
+        std::vector<uint64_t> nbase(n, 0);
+        for (size_t i = 0; i < n; i++) {
+            const uint64_t cnt = level_n[i];
+            if (cnt <= 1) continue;
+            const uint64_t groups = (cnt + 255) / 256;
+            nbase[i] = dst_total;
+            for (uint64_t g = 0; g < groups; g++) {
+                ck_reduce_wg w{};
+                w.src_base = base[i] + g * 256;
+                w.dst_index = dst_total + g;
+                w.count = (uint32_t)std::min<uint64_t>(256, cnt - g * 256);
+                w.file = (uint32_t)i;
+                w.is_root = groups == 1;
+                wgs.push_back(w);
+            }
+            dst_total += groups == 1 ? 0 : groups;
+            level_n[i] = groups == 1 ? 1 : groups;
+        }
+        if (wgs.empty()) break;
+        auto p = std::make_unique<ck_pass>();
+        p->wgs.upload(wgs);
+        p->n_wg = (uint32_t)wgs.size();
+        p->src = src;
+        p->dst = 1 - src;
+        lvl_cap[1 - src] = std::max<size_t>(lvl_cap[1 - src], dst_total);
+        b->passes.push_back(std::move(p));
+        base = nbase;
+        src = 1 - src;
+    }
+    b->lvl[0].alloc(lvl_cap[0] * 32);
+    b->lvl[1].alloc(lvl_cap[1] * 32);
+    return b.release();
+}
+
+void run_checksum_leaf(const sd_checksum_batch* b, const uint8_t* d_data, uint64_t shift, uint32_t wg0, uint32_t wg1,
+                       uint32_t* out, hipStream_t s);
+
+void run_checksum_reduce(const sd_checksum_batch* b, uint32_t* out, hipStream_t s) {
+    for (const auto& p : b->passes)
+        HIP_CHECK(sdk::launch_ck_reduce(b->lvl[p->src].as<uint32_t>(), b->lvl[p->dst].as<uint32_t>(),
+                                        p->wgs.as<ck_reduce_wg>(), p->n_wg, out, s));
+}
+
+void run_checksum_batch(const sd_checksum_batch* b, const uint8_t* d_data, uint8_t* d_hash32, hipStream_t s) {
+    uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
+    run_checksum_leaf(b, d_data, 0, 0, (uint32_t)b->wg_map_h.size(), out, s);
+    run_checksum_reduce(b, out, s);
+}
+
+const char HEX[] = "0123456789abcdef";
+void to_hex(const uint8_t* h, int nbytes, char* out) {
+    for (int i = 0; i < nbytes; i++) {
+        out[2 * i] = HEX[h[i] >> 4];
+        out[2 * i + 1] = HEX[h[i] & 15];
+    }
+    out[2 * nbytes] = 0;
+}
+
+int32_t io_status(int err) { return (int32_t)(SD_FILE_IO_ERROR | ((uint32_t)(err & 0xFFFF) << 16)); }
+
+// read exactly n bytes at off; returns 0, or an sd_file_status code
+int32_t pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
+    while (n) {
+        const ssize_t r = pread(fd, dst, n, (off_t)off);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return io_status(errno);
+        }
+        if (r == 0) return SD_FILE_SHORT_READ;
+        dst += r;
+        n -= (uint64_t)r;
+        off += (uint64_t)r;
+    }
+    return SD_FILE_OK;
+}
+
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" {
+
+int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }
+
+const char* sd_cas_last_error(void) { return g_err.c_str(); }
+
+int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
+    SD_GUARD_BEGIN
+    if (!out) throw sd_failure(SD_ERR_INVALID, "out is null");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        throw sd_failure(SD_ERR_DEVICE, "no HIP device available (libsdcas has no CPU fallback)");
+    if (device < 0 || device >= count) throw sd_failure(SD_ERR_INVALID, "device index out of range");
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        throw sd_failure(SD_ERR_DEVICE, std::string("libsdcas is built for gfx950, device is ") + prop.gcnArchName);
+    auto c = std::make_unique<sd_cas_ctx>();
+    c->device = device;
+    c->bind();
+    HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    *out = c.release();
+    return SD_OK;
+    SD_GUARD_END
+}
+
+void sd_cas_ctx_destroy(sd_cas_ctx* ctx) {
+    if (!ctx) return;
+    try {
+        ctx->bind();
+        (void)hipDeviceSynchronize();
+        for (auto& s : ctx->free_slots)
+            if (s->stream) (void)hipStreamDestroy(s->stream);
+        ctx->free_slots.clear();
+        if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    } catch (...) {
+    }
+    delete ctx;
+}
+
+int sd_cas_host_alloc(sd_cas_ctx* ctx, uint64_t bytes, void** out) {
+    SD_GUARD_BEGIN
+    if (!ctx || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    HIP_CHECK(hipHostMalloc(out, bytes ? bytes : 16, hipHostMallocDefault));
+    return SD_OK;
+    SD_GUARD_END
+}
+
+void sd_cas_host_free(sd_cas_ctx* ctx, void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int sd_cas_stage_plan(const uint64_t* sizes, size_t n, sd_extent* extents_out, uint64_t* total_bytes_out) {
+    SD_GUARD_BEGIN
+    if ((!sizes || !extents_out) && n) throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (!total_bytes_out) throw sd_failure(SD_ERR_INVALID, "total_bytes_out is null");
+    uint64_t off = 0;
+    for (size_t i = 0; i < n; i++) {
+        sd_extent& e = extents_out[i];
+        e.size = sizes[i];
+        const bool whole = sizes[i] <= SD_MINIMUM_FILE_SIZE;  // cas.rs:27 (<=)
+        e.kind = whole ? SD_KIND_WHOLE : SD_KIND_SAMPLED;
+        e.msg_len = whole ? (uint32_t)(8 + sizes[i]) : SD_SAMPLED_MSG_LEN;
+        e.msg_offset = off;
+        off = align_up(off + e.msg_len, SD_STAGE_ALIGN);
+    }
+    *total_bytes_out = off;
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cas_stage_file(const char* path, const sd_extent* ext, uint8_t* staged, int32_t* status) {
+    SD_GUARD_BEGIN
+    if (!path || !ext || !staged || !status) throw sd_failure(SD_ERR_INVALID, "null argument");
+    validate_extent(*ext, 0);
+    uint8_t* dst = staged + ext->msg_offset;
+    const uint64_t size = ext->size;
+    for (int i = 0; i < 8; i++) dst[i] = (uint8_t)(size >> (8 * i));  // cas.rs:25
+    const uint64_t padded = align_up(ext->msg_len, SD_STAGE_ALIGN);
+    memset(dst + ext->msg_len, 0, padded - ext->msg_len);
+    const int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+        *status = io_status(errno);
+        return SD_OK;
+    }
+    int32_t st = SD_FILE_OK;
+    if (ext->kind == SD_KIND_WHOLE) {  // cas.rs:29 fs::read -- requires len == size
+        st = pread_exact(fd, dst + 8, size, 0);
+        if (st == SD_FILE_OK) {
+            uint8_t extra;
+            if (pread(fd, &extra, 1, (off_t)size) == 1) st = SD_FILE_SHORT_READ;  // file grew since stat
+        }
+    } else {  // cas.rs:31-58: header, 4 samples at 8192 + k*seek_jump, footer
+        const uint64_t H = SD_HEADER_OR_FOOTER_SIZE, S = SD_SAMPLE_SIZE;
+        const uint64_t jump = (size - 2 * H) / SD_SAMPLE_COUNT;
+        uint8_t* p = dst + 8;
+        st = pread_exact(fd, p, H, 0);
+        p += H;
+        uint64_t current_pos = H;
+        while (st == SD_FILE_OK) {
+            st = pread_exact(fd, p, S, current_pos);
+            p += S;
+            if (current_pos >= H + jump * (SD_SAMPLE_COUNT - 1)) break;
+            current_pos += jump;
+        }
+        if (st == SD_FILE_OK) st = pread_exact(fd, p, H, size - H);
+    }
+    close(fd);
+    *status = st;
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cas_batch_create(sd_cas_ctx* ctx, const sd_extent* extents, size_t n, sd_cas_batch** out) {
+    SD_GUARD_BEGIN
+    if (!ctx || !out || (!extents && n)) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    *out = build_cas_batch(extents, n);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+void sd_cas_batch_destroy(sd_cas_batch* batch) {
+    try {
+        delete batch;
+    } catch (...) {
+    }
+}
+
+int sd_cas_batch_run(sd_cas_ctx* ctx, const sd_cas_batch* batch, const uint8_t* d_staged, uint8_t* d_hash32,
+                     void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || !batch || (batch->n && (!d_staged || !d_hash32))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    run_cas_batch(batch, d_staged, d_hash32, ctx->pick(stream));
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cas_batch_run_part(sd_cas_ctx* ctx, const sd_cas_batch* batch, int parts, const uint8_t* d_staged,
+                          uint8_t* d_hash32, void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || !batch || (batch->n && (!d_staged || !d_hash32))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    run_cas_batch(batch, d_staged, d_hash32, ctx->pick(stream), parts);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cas_batch_stats(const sd_cas_batch* b, uint64_t out[6]) {
+    SD_GUARD_BEGIN
+    if (!b || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    out[0] = b->n; out[1] = b->n_sampled; out[2] = b->n_whole; out[3] = b->total_chunks;
+    out[4] = b->compressions; out[5] = b->msg_bytes;
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, const sd_extent* extents, size_t n,
+               char* out_hex17, int32_t* status) {
+    SD_GUARD_BEGIN
+    if (!ctx || (n && (!staged || !extents || !out_hex17))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    // files whose staging failed keep their status and are not hashed
+    std::vector<size_t> live;
+    live.reserve(n);
+    for (size_t i = 0; i < n; i++)
+        if (!status || status[i] == SD_FILE_OK) live.push_back(i);
+    auto slot = ctx->acquire();
+    struct Rel {
+        sd_cas_ctx* c;
+        std::unique_ptr<Slot>* s;
+        ~Rel() { c->release(std::move(*s)); }
+    } rel{ctx, &slot};
+    // groups of files whose staged span fits the device window, in index order
+    const uint64_t WINDOW = 4ull << 30;
+    size_t gi = 0;
+    while (gi < live.size()) {
+        uint64_t lo = UINT64_MAX, hi = 0;
+        size_t gj = gi;
+        std::vector<sd_extent> ext;
+        while (gj < live.size()) {
+            const sd_extent& e = extents[live[gj]];
+            const uint64_t nlo = std::min(lo, e.msg_offset);
+            const uint64_t nhi = std::max(hi, align_up(e.msg_offset + e.msg_len, SD_STAGE_ALIGN));
+            if (gj > gi && nhi - nlo > WINDOW) break;
+            lo = nlo;
+            hi = nhi;
+            gj++;
+        }
+        if (hi > staged_bytes) throw sd_failure(SD_ERR_INVALID, "extent beyond staged_bytes");
+        for (size_t k = gi; k < gj; k++) {
+            sd_extent e = extents[live[k]];
+            e.msg_offset -= lo;
+            ext.push_back(e);
+        }
+        std::unique_ptr<sd_cas_batch> b(build_cas_batch(ext.data(), ext.size()));
+        slot->staged.ensure(hi - lo);
+        slot->hashes.ensure(ext.size() * 32);
+        slot->host_hashes.ensure(ext.size() * 32);
+        HIP_CHECK(hipMemcpyAsync(slot->staged.p, staged + lo, hi - lo, hipMemcpyHostToDevice, slot->stream));
+        run_cas_batch(b.get(), slot->staged.as<uint8_t>(), slot->hashes.as<uint8_t>(), slot->stream);
+        HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, slot->hashes.p, ext.size() * 32, hipMemcpyDeviceToHost,
+                                 slot->stream));
+        HIP_CHECK(hipStreamSynchronize(slot->stream));
+        const uint8_t* h = reinterpret_cast<const uint8_t*>(slot->host_hashes.p);
+        for (size_t k = gi; k < gj; k++) {
+            to_hex(h + (k - gi) * 32, 8, out_hex17 + live[k] * 17);  // cas.rs:61 to_hex()[..16]
+            if (status) status[live[k]] = SD_FILE_OK;
+        }
+        gi = gj;
+    }
+    return SD_OK;
+    SD_GUARD_END
+}
+
+// ---------------------------------------------------------------------- checksums
+int sd_checksum_batch_create(sd_cas_ctx* ctx, const uint64_t* offsets, const uint64_t* lens, size_t n,
+                             sd_checksum_batch** out) {
+    SD_GUARD_BEGIN
+    if (!ctx || !out || (n && (!offsets || !lens))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    *out = build_checksum_batch(offsets, lens, n);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+void sd_checksum_batch_destroy(sd_checksum_batch* b) {
+    try {
+        delete b;
+    } catch (...) {
+    }
+}
+
+int sd_checksum_batch_run(sd_cas_ctx* ctx, const sd_checksum_batch* b, const uint8_t* d_data, uint8_t* d_hash32,
+                          void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || !b || (b->n && (!d_data || !d_hash32))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    run_checksum_batch(b, d_data, d_hash32, ctx->pick(stream));
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_checksum_batch_stats(const sd_checksum_batch* b, uint64_t out[4]) {
+    SD_GUARD_BEGIN
+    if (!b || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    out[0] = b->n; out[1] = b->total_bytes; out[2] = b->compressions; out[3] = b->blocks;
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65, int32_t* status) {
+    SD_GUARD_BEGIN
+    if (!ctx || (n && (!paths || !out_hex65 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    auto slot = ctx->acquire();
+    struct Rel {
+        sd_cas_ctx* c;
+        std::unique_ptr<Slot>* s;
+        ~Rel() { c->release(std::move(*s)); }
+    } rel{ctx, &slot};
+    const uint64_t W = 256ull << 20;  // pinned window; a multiple of the 1 MiB leaf block
+    slot->window.ensure(W + 64);
+    slot->staged.ensure(W + 64);
+    slot->hashes.ensure(32);
+    slot->host_hashes.ensure(32);
+    uint8_t* win = reinterpret_cast<uint8_t*>(slot->window.p);
+    for (size_t i = 0; i < n; i++) {
+        status[i] = SD_FILE_OK;
+        const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+        if (fd < 0) {
+            status[i] = io_status(errno);
+            continue;
+        }
+        struct stat stt;
+        if (fstat(fd, &stt) != 0) {
+            status[i] = io_status(errno);
+            close(fd);
+            continue;
+        }
+        // hash.rs:14-20 reads until a short read; the length is fixed at fstat here
+        const uint64_t len = (uint64_t)stt.st_size;
+        const uint64_t off0 = 0;
+        std::unique_ptr<sd_checksum_batch> b(build_checksum_batch(&off0, &len, 1));
+        uint32_t* out = slot->hashes.as<uint32_t>();
+        const uint64_t blocks_per_window = W / CK_BLOCK_BYTES;
+        for (uint64_t pos = 0; pos < std::max<uint64_t>(len, 1); pos += W) {
+            const uint64_t n_here = std::min<uint64_t>(W, len - pos);
+            if (n_here) {
+                HIP_CHECK(hipStreamSynchronize(slot->stream));  // window reuse
+                const int32_t st = pread_exact(fd, win, n_here, pos);
+                if (st != SD_FILE_OK) {
+                    status[i] = st;
+                    break;
+                }
+            }
+            memset(win + n_here, 0, 64);
+            HIP_CHECK(hipMemcpyAsync(slot->staged.p, win, align_up(n_here, 64) + (n_here ? 0 : 64),
+                                     hipMemcpyHostToDevice, slot->stream));
+            const uint32_t wg0 = (uint32_t)(pos / CK_BLOCK_BYTES);
+            const uint32_t wg1 = (uint32_t)std::min<uint64_t>(b->wg_map_h.size(), wg0 + blocks_per_window);
+            run_checksum_leaf(b.get(), slot->staged.as<uint8_t>(), pos, wg0, wg1, out, slot->stream);
+            if (len == 0) break;
+        }
+        close(fd);
+        if (status[i] != SD_FILE_OK) continue;
+        run_checksum_reduce(b.get(), out, slot->stream);
+        HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, out, 32, hipMemcpyDeviceToHost, slot->stream));
+        HIP_CHECK(hipStreamSynchronize(slot->stream));
+        to_hex(reinterpret_cast<const uint8_t*>(slot->host_hashes.p), 32, out_hex65 + i * 65);  // hash.rs:21-23
+    }
+    return SD_OK;
+    SD_GUARD_END
+}
+
+// -------------------------------------------------------------------------- dedup
+int sd_dedup_partition(sd_cas_ctx* ctx, const uint8_t* d_hash32, const uint8_t* d_valid, uint64_t n,
+                       uint64_t global_index_base, int nparts, uint64_t* d_counts, uint64_t* d_records,
+                       uint64_t* n_valid, void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || !d_counts || !n_valid || (n && (!d_hash32 || !d_records)))
+        throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (nparts < 1 || nparts > 64) throw sd_failure(SD_ERR_INVALID, "nparts must be in [1, 64]");
+    ctx->bind();
+    hipStream_t s = ctx->pick(stream);
+    DevBuf cursor;
+    cursor.alloc((nparts + 1) * sizeof(uint64_t));
+    HIP_CHECK(sdk::dedup_partition(d_hash32, d_valid, n, global_index_base, nparts, d_counts, d_records,
+                                   cursor.as<uint64_t>(), s));
+    uint64_t tot = 0;
+    HIP_CHECK(hipMemcpyAsync(&tot, cursor.as<uint64_t>() + nparts, sizeof tot, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    *n_valid = tot;
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, uint64_t* d_rep, uint64_t* n_groups,
+                   void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || !n_groups || (m && (!d_records || !d_rep))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    hipStream_t s = ctx->pick(stream);
+    size_t need = 0;
+    HIP_CHECK(sdk::dedup_group(d_records, m, d_rep, nullptr, nullptr, &need, s));
+    DevBuf scratch, ng;
+    scratch.alloc(need);
+    ng.alloc(sizeof(uint64_t));
+    HIP_CHECK(sdk::dedup_group(d_records, m, d_rep, ng.as<uint64_t>(), scratch.p, &need, s));
+    uint64_t g = 0;
+    HIP_CHECK(hipMemcpyAsync(&g, ng.p, sizeof g, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    *n_groups = g;
+    return SD_OK;
+    SD_GUARD_END
+}
+
+// ----------------------------------------------------------------- synthetic data
+int sd_synth_stage_cas(sd_cas_ctx* ctx, const uint64_t* d_sizes, const uint64_t* d_cids, const uint32_t* d_twins,
+                       const sd_extent* d_extents, size_t n, uint8_t* d_staged, void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || (n && (!d_sizes || !d_cids || !d_extents || !d_staged))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (n >= (1ull << 31)) throw sd_failure(SD_ERR_INVALID, "too many files");
+    ctx->bind();
+    HIP_CHECK(sdk::launch_synth_stage_cas(d_sizes, d_cids, d_twins, d_extents, (uint32_t)n, d_staged, ctx->pick(stream)));
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_synth_fill(sd_cas_ctx* ctx, uint64_t cid, uint32_t twin, uint64_t len, uint8_t* d_out, void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || (len && !d_out)) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    HIP_CHECK(sdk::launch_synth_fill(cid, twin, len, d_out, ctx->pick(stream)));
+    return SD_OK;
+    SD_GUARD_END
+}
+
+// -------------------------------------------------------------- device utilities
+int sd_device_malloc(sd_cas_ctx* ctx, uint64_t bytes, void** out) {
+    SD_GUARD_BEGIN
+    if (!ctx || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    HIP_CHECK(hipMalloc(out, bytes ? bytes : 16));
+    return SD_OK;
+    SD_GUARD_END
+}
+
+void sd_device_free(sd_cas_ctx* ctx, void* p) {
+    if (p) (void)hipFree(p);
+}
+
+int sd_memcpy(sd_cas_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || (bytes && (!dst || !src))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    hipStream_t s = ctx->pick(stream);
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_stream_sync(sd_cas_ctx* ctx, void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    HIP_CHECK(hipStreamSynchronize(ctx->pick(stream)));
+    return SD_OK;
+    SD_GUARD_END
+}
+
+static int time_loop(sd_cas_ctx* ctx, void* stream, int iters, float* ms, const std::function<void(hipStream_t)>& fn);
+
+int sd_cas_batch_time(sd_cas_ctx* ctx, const sd_cas_batch* batch, const uint8_t* d_staged, uint8_t* d_hash32,
+                      int iters, void* stream, float* ms_total) {
+    return time_loop(ctx, stream, iters, ms_total,
+                     [&](hipStream_t s) { run_cas_batch(batch, d_staged, d_hash32, s); });
+}
+
+int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, const uint8_t* d_data, uint8_t* d_hash32,
+                           int iters, void* stream, float* ms_total) {
+    return time_loop(ctx, stream, iters, ms_total,
+                     [&](hipStream_t s) { run_checksum_batch(batch, d_data, d_hash32, s); });
+}
+
+int sd_valu_peak(sd_cas_ctx* ctx, double* lane_ops_per_s) {
+    SD_GUARD_BEGIN
+    if (!ctx || !lane_ops_per_s) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, ctx->device));
+    const uint32_t grid = (uint32_t)prop.multiProcessorCount * 8;  // 8 x 256 threads per CU
+    const uint32_t iters = 512;
+    DevBuf sink;
+    sink.alloc((size_t)grid * 256 * 4);
+    hipStream_t s = ctx->stream;
+    HIP_CHECK(sdk::launch_valu_peak(sink.as<uint32_t>(), iters, grid, s));  // warm-up
+    hipEvent_t a, b;
+    HIP_CHECK(hipEventCreate(&a));
+    HIP_CHECK(hipEventCreate(&b));
+    HIP_CHECK(hipEventRecord(a, s));
+    const int reps = 3;
+    for (int r = 0; r < reps; r++) HIP_CHECK(sdk::launch_valu_peak(sink.as<uint32_t>(), iters, grid, s));
+    HIP_CHECK(hipEventRecord(b, s));
+    HIP_CHECK(hipEventSynchronize(b));
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    const double ops = (double)reps * grid * 256.0 * iters * 96.0;  // 8 G-mixes x 12 ops per iteration
+    *lane_ops_per_s = ops / (ms * 1e-3);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+}  // extern "C"
+
+// ----------------------------------------------------------------- internal helpers
+namespace {
+void run_checksum_leaf(const sd_checksum_batch* b, const uint8_t* d_data, uint64_t shift, uint32_t wg0, uint32_t wg1,
+                       uint32_t* out, hipStream_t s) {
+    if (wg1 <= wg0) return;
+    HIP_CHECK(sdk::launch_ck_leaf(d_data, shift, b->files.as<ck_file>(), b->wg_map.as<uint2>() + wg0, wg1 - wg0,
+                                  b->lvl[0].as<uint32_t>(), out, s));
+}
+}  // namespace
+
+static int time_loop(sd_cas_ctx* ctx, void* stream, int iters, float* ms,
+                     const std::function<void(hipStream_t)>& fn) {
+    SD_GUARD_BEGIN
+    if (!ctx || !ms || iters < 1) throw sd_failure(SD_ERR_INVALID, "bad argument");
+    ctx->bind();
+    hipStream_t s = ctx->pick(stream);
+    hipEvent_t a, b;
+    HIP_CHECK(hipEventCreate(&a));
+    HIP_CHECK(hipEventCreate(&b));
+    HIP_CHECK(hipEventRecord(a, s));
+    for (int i = 0; i < iters; i++) fn(s);
+    HIP_CHECK(hipEventRecord(b, s));
+    HIP_CHECK(hipEventSynchronize(b));
+    HIP_CHECK(hipEventElapsedTime(ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return SD_OK;
+    SD_GUARD_END
+}

@@ -1,0 +1,44 @@
+// sd_internal.h -- types shared between the host-side C ABI and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sd_cas.h"
+
+// one file of a checksum batch (device table)
+struct ck_file {
+    uint64_t offset;   // byte offset in the data buffer
+    uint64_t len;      // file length
+    uint64_t cv_base;  // first slot of this file's 1 MiB block CVs in the level-0 CV buffer
+};
+
+// one workgroup of a checksum reduce pass
+struct ck_reduce_wg {
+    uint64_t src_base;   // first CV (index into the source level) of this group
+    uint64_t dst_index;  // CV slot in the destination level
+    uint32_t count;      // CVs in this group (1..256)
+    uint32_t file;       // file index (for the root output)
+    uint32_t is_root;    // the group is the file's whole level: ROOT on the final parent
+    uint32_t pad;
+};
+
+namespace sdk {
+hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const uint32_t* idx, uint32_t n,
+                              uint32_t* out, hipStream_t s);
+hipError_t launch_whole(const uint8_t* staged, const sd_extent* ext, const uint32_t* order,
+                        const uint32_t* chunk_prefix, const uint32_t* hint, uint32_t nw, uint32_t total_chunks,
+                        uint32_t n_multi, uint32_t* cvbuf, uint32_t* out, hipStream_t s);
+hipError_t launch_ck_leaf(const uint8_t* data, uint64_t shift, const ck_file* files, const uint2* wg_map,
+                          uint32_t n_wg, uint32_t* cvbuf, uint32_t* out, hipStream_t s);
+hipError_t launch_ck_reduce(const uint32_t* src, uint32_t* dst, const ck_reduce_wg* wgs, uint32_t n_wg,
+                            uint32_t* out, hipStream_t s);
+hipError_t launch_synth_stage_cas(const uint64_t* sizes, const uint64_t* cids, const uint32_t* twins,
+                                  const sd_extent* ext, uint32_t n, uint8_t* staged, hipStream_t s);
+hipError_t launch_synth_fill(uint64_t cid, uint32_t twin, uint64_t len, uint8_t* out, hipStream_t s);
+hipError_t launch_valu_peak(uint32_t* sink, uint32_t iters, uint32_t grid, hipStream_t s);
+// dedup
+hipError_t dedup_partition(const uint8_t* hash32, const uint8_t* valid, uint64_t n, uint64_t base, int nparts,
+                           uint64_t* counts, uint64_t* records, uint64_t* cursor_scratch, hipStream_t s);
+hipError_t dedup_group(uint64_t* records, uint64_t m, uint64_t* rep, uint64_t* n_groups_dev, void* scratch,
+                       size_t* scratch_bytes, hipStream_t s);
+}  // namespace sdk

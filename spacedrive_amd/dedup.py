@@ -1,0 +1,103 @@
+"""Post-hash duplicate grouping across GPUs.
+
+Reference semantics (core/src/object/file_identifier/mod.rs:136-333): after hashing a
+step's files, each file_path is linked to an Object that already owns an equal cas_id,
+otherwise a new Object is created; size-0 files (cas_id None, mod.rs:80-88) never
+dedup.  The partition of files into equal-cas_id groups is what this module computes,
+bit-exactly; which member becomes the Object is a policy of the caller (the reference's
+choice depends on 100-row chunking and HashMap order, §8(e)), here the smallest global
+file index of the group (the "Object-link candidate").
+
+Multi-GPU: files are sharded by index; each rank buckets its records
+``(cas_id as big-endian u64, global index)`` by cas_id prefix (device kernel
+``sd_dedup_partition``), one ``all_to_all_single`` of the per-destination counts and one
+of the 16-byte records move every record to the rank owning its prefix (backend "nccl"
+= RCCL over xGMI on MI355X; "gloo" on CPU for tests), and each rank sorts and groups
+its bucket (``sd_dedup_group``).  No other collective exists on the data path.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def dest_of(keys: np.ndarray, nparts: int) -> np.ndarray:
+    """Destination rank of a cas_id key: its top 16 bits scaled to nparts (contiguous ranges)."""
+    return (((keys >> np.uint64(48)) * np.uint64(nparts)) >> np.uint64(16)).astype(np.int64)
+
+
+def keys_from_hashes(h32: np.ndarray) -> np.ndarray:
+    """First 8 hash bytes as a big-endian u64 (== the hex cas_id's lexicographic order)."""
+    return h32[:, :8].copy().view(">u8").reshape(-1).astype(np.uint64)
+
+
+def exchange(send_records: torch.Tensor, send_counts: torch.Tensor,
+             group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """All-to-all of records grouped by destination.
+
+    send_records: int64 [m, 2] (key, global index) ordered by destination rank;
+    send_counts:  int64 [world] records per destination.  Returns the received records.
+    Works for any backend whose tensors live on the device of ``send_records``.
+    """
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return send_records
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    rc = recv_counts.cpu().tolist()
+    sc = send_counts.cpu().tolist()
+    out = torch.empty((int(sum(rc)), 2), dtype=send_records.dtype, device=send_records.device)
+    dist.all_to_all_single(out, send_records, output_split_sizes=rc, input_split_sizes=sc, group=group)
+    return out
+
+
+def group_device(ctx, records: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, int]:
+    """Sort received records by (cas_id, index) and map each to its group's smallest index."""
+    m = records.shape[0]
+    rep = torch.empty(max(m, 1), dtype=torch.int64, device=records.device)
+    ng = ctx.dedup_group(records, m, rep)
+    return records, rep[:m], ng
+
+
+def dedup_shard(ctx, d_hash32: torch.Tensor, d_valid: Optional[torch.Tensor], n_local: int, global_base: int,
+                group: Optional[dist.ProcessGroup] = None):
+    """Full distributed step on one rank: partition -> exchange -> group.
+
+    Returns (records int64 [m, 2] sorted by (key, index), rep int64 [m], n_groups) for
+    the cas_id prefix range this rank owns.
+    """
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    dev = d_hash32.device
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    recs = torch.empty((max(n_local, 1), 2), dtype=torch.int64, device=dev)
+    nv = ctx.dedup_partition(d_hash32, d_valid, n_local, global_base, world, counts, recs)
+    recv = exchange(recs[:nv], counts, group)
+    return group_device(ctx, recv)
+
+
+# ------------------------------------------------------------------ host reference
+def partition_host(keys: np.ndarray, idx: np.ndarray, nparts: int):
+    """Host mirror of sd_dedup_partition's grouping (order within a destination unspecified)."""
+    d = dest_of(keys, nparts)
+    order = np.argsort(d, kind="stable")
+    counts = np.bincount(d, minlength=nparts).astype(np.int64)
+    recs = np.stack([keys[order].view(np.int64), idx[order].astype(np.int64)], axis=1)
+    return recs, counts
+
+
+def group_host(records: np.ndarray):
+    """Host mirror of sd_dedup_group: sort by (key, index); rep = min index of the group."""
+    if len(records) == 0:
+        return records, np.zeros(0, np.int64), 0
+    k = records[:, 0].view(np.uint64)
+    i = records[:, 1]
+    order = np.lexsort((i, k))
+    r = records[order]
+    ks = r[:, 0].view(np.uint64)
+    head = np.ones(len(r), bool)
+    head[1:] = ks[1:] != ks[:-1]
+    head_pos = np.maximum.accumulate(np.where(head, np.arange(len(r)), 0))
+    return r, r[head_pos, 1], int(head.sum())

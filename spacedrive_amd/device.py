@@ -1,0 +1,193 @@
+"""Device-level interface over libsdcas.so: contexts, prepared batches, device buffers.
+
+Device memory and streams are torch tensors / torch streams (plumbing only); every byte
+of hashing runs in the gfx950 kernels of ``csrc/cas_kernels.hip``.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ._native import Extent, check, lib
+
+EXTENT_DTYPE = np.dtype([("size", "<u8"), ("msg_offset", "<u8"), ("msg_len", "<u4"), ("kind", "<u4")])
+assert EXTENT_DTYPE.itemsize == ctypes.sizeof(Extent) == 24
+
+
+def _ptr(x) -> Optional[int]:
+    if x is None:
+        return None
+    if isinstance(x, torch.Tensor):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    return int(x)
+
+
+def _stream(stream) -> Optional[int]:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, torch.cuda.Stream):
+        return stream.cuda_stream
+    return int(stream)
+
+
+def stage_plan(sizes) -> tuple:
+    """cas.rs:25-58 message layout for files of these sizes -> (extents, staged_bytes)."""
+    sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+    ext = np.zeros(len(sizes), dtype=EXTENT_DTYPE)
+    total = ctypes.c_uint64(0)
+    check(lib().sd_cas_stage_plan(_ptr(sizes), len(sizes), _ptr(ext), ctypes.byref(total)))
+    return ext, int(total.value)
+
+
+class Context:
+    """One per device and process; thread-safe (sd_cas_ctx)."""
+
+    def __init__(self, device: Optional[int] = None):
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib().sd_cas_ctx_create(device, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self) -> None:
+        if self.handle:
+            lib().sd_cas_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------- batches
+    def cas_batch(self, extents: np.ndarray) -> "CasBatch":
+        return CasBatch(self, extents)
+
+    def checksum_batch(self, offsets, lens) -> "ChecksumBatch":
+        return ChecksumBatch(self, offsets, lens)
+
+    # -------------------------------------------------------------- synthetic data
+    def synth_stage_cas(self, d_sizes, d_cids, d_twins, d_extents, n, d_staged, stream=None) -> None:
+        check(lib().sd_synth_stage_cas(self.handle, _ptr(d_sizes), _ptr(d_cids), _ptr(d_twins),
+                                       _ptr(d_extents), n, _ptr(d_staged), _stream(stream)))
+
+    def synth_fill(self, cid: int, twin: int, length: int, d_out, stream=None) -> None:
+        check(lib().sd_synth_fill(self.handle, cid, twin, length, _ptr(d_out), _stream(stream)))
+
+    def valu_peak(self) -> float:
+        v = ctypes.c_double(0)
+        check(lib().sd_valu_peak(self.handle, ctypes.byref(v)))
+        return float(v.value)
+
+    # -------------------------------------------------------------- dedup
+    def dedup_partition(self, d_hash32, d_valid, n: int, base: int, nparts: int, d_counts, d_records,
+                        stream=None) -> int:
+        nv = ctypes.c_uint64(0)
+        check(lib().sd_dedup_partition(self.handle, _ptr(d_hash32), _ptr(d_valid), n, base, nparts,
+                                       _ptr(d_counts), _ptr(d_records), ctypes.byref(nv), _stream(stream)))
+        return int(nv.value)
+
+    def dedup_group(self, d_records, m: int, d_rep, stream=None) -> int:
+        ng = ctypes.c_uint64(0)
+        check(lib().sd_dedup_group(self.handle, _ptr(d_records), m, _ptr(d_rep), ctypes.byref(ng),
+                                   _stream(stream)))
+        return int(ng.value)
+
+
+class CasBatch:
+    """Prepared cas_id batch (sd_cas_batch): run over device-resident staged messages."""
+
+    def __init__(self, ctx: Context, extents: np.ndarray):
+        self.ctx = ctx
+        self.extents = np.ascontiguousarray(extents, dtype=EXTENT_DTYPE)
+        h = ctypes.c_void_p()
+        check(lib().sd_cas_batch_create(ctx.handle, _ptr(self.extents), len(self.extents), ctypes.byref(h)))
+        self.handle = h
+        st = np.zeros(6, np.uint64)
+        check(lib().sd_cas_batch_stats(h, _ptr(st)))
+        (self.n, self.n_sampled, self.n_whole, self.whole_chunks, self.compressions,
+         self.msg_bytes) = (int(v) for v in st)
+
+    def run(self, d_staged: torch.Tensor, d_hash32: torch.Tensor, stream=None) -> None:
+        assert d_hash32.numel() >= 32 * self.n and d_staged.is_cuda and d_hash32.is_cuda
+        check(lib().sd_cas_batch_run(self.ctx.handle, self.handle, _ptr(d_staged), _ptr(d_hash32),
+                                     _stream(stream)))
+
+    def run_part(self, parts: int, d_staged: torch.Tensor, d_hash32: torch.Tensor, stream=None) -> None:
+        """parts: 1 = sampled-file kernel only, 2 = whole-file kernels only."""
+        check(lib().sd_cas_batch_run_part(self.ctx.handle, self.handle, parts, _ptr(d_staged), _ptr(d_hash32),
+                                          _stream(stream)))
+
+    def time(self, d_staged, d_hash32, iters: int, stream=None) -> float:
+        ms = ctypes.c_float(0)
+        check(lib().sd_cas_batch_time(self.ctx.handle, self.handle, _ptr(d_staged), _ptr(d_hash32), iters,
+                                      _stream(stream), ctypes.byref(ms)))
+        return float(ms.value)
+
+    def close(self) -> None:
+        if self.handle:
+            lib().sd_cas_batch_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ChecksumBatch:
+    """Prepared full-file checksum batch (sd_checksum_batch) over byte ranges of one buffer."""
+
+    def __init__(self, ctx: Context, offsets, lens):
+        self.ctx = ctx
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        h = ctypes.c_void_p()
+        check(lib().sd_checksum_batch_create(ctx.handle, _ptr(self.offsets), _ptr(self.lens), len(self.lens),
+                                             ctypes.byref(h)))
+        self.handle = h
+        st = np.zeros(4, np.uint64)
+        check(lib().sd_checksum_batch_stats(h, _ptr(st)))
+        self.n, self.total_bytes, self.compressions, self.blocks = (int(v) for v in st)
+
+    def run(self, d_data: torch.Tensor, d_hash32: torch.Tensor, stream=None) -> None:
+        assert d_hash32.numel() >= 32 * self.n
+        check(lib().sd_checksum_batch_run(self.ctx.handle, self.handle, _ptr(d_data), _ptr(d_hash32),
+                                          _stream(stream)))
+
+    def time(self, d_data, d_hash32, iters: int, stream=None) -> float:
+        ms = ctypes.c_float(0)
+        check(lib().sd_checksum_batch_time(self.ctx.handle, self.handle, _ptr(d_data), _ptr(d_hash32), iters,
+                                           _stream(stream), ctypes.byref(ms)))
+        return float(ms.value)
+
+    def close(self) -> None:
+        if self.handle:
+            lib().sd_checksum_batch_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_default: dict = {}
+
+
+def default_context(device: Optional[int] = None) -> Context:
+    if device is None:
+        device = torch.cuda.current_device()
+    ctx = _default.get(device)
+    if ctx is None:
+        ctx = _default[device] = Context(device)
+    return ctx

@@ -1,0 +1,112 @@
+"""The C ABI boundary on a machine without a GPU: the library loads, exports exactly what
+include/sd_cas.h declares, its host-only planning works, and compute entry points fail
+loudly (no CPU fallback)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from spacedrive_amd import _native
+from spacedrive_amd._native import SdCasError, check, lib
+
+
+def declared_functions():
+    src = open(_native.HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sd_[a-z0-9_]+)\s*\(", src)))
+
+
+def exported_symbols():
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
+
+
+def test_header_declares_abi():
+    fns = declared_functions()
+    for must in ("sd_cas_ctx_create", "sd_cas_ids", "sd_cas_batch_run", "sd_checksum_batch_run",
+                 "sd_file_checksums", "sd_dedup_partition", "sd_dedup_group", "sd_cas_stage_plan"):
+        assert must in fns
+
+
+def test_library_exports_every_declared_symbol():
+    exp = exported_symbols()
+    missing = [f for f in declared_functions() if f not in exp]
+    assert not missing, missing
+    # and the Python binding covers the whole header
+    assert sorted(n for n, _, _ in _native.SIGNATURES) == declared_functions()
+
+
+def test_library_loads_and_binds():
+    L = lib()
+    assert L.sd_cas_abi_version() == 1
+    for name, _, _ in _native.SIGNATURES:
+        assert getattr(L, name) is not None
+
+
+def test_stage_plan_layout():
+    # cas.rs:25-58: 8 + size (<= 102400) or 57352; 64-byte aligned offsets
+    sizes = np.array([0, 1, 102400, 102401, 5 << 30, 1000], np.uint64)
+    from spacedrive_amd.device import stage_plan
+    ext, total = stage_plan(sizes)
+    assert list(ext["msg_len"]) == [8, 9, 102408, 57352, 57352, 1008]
+    assert list(ext["kind"]) == [1, 1, 1, 2, 2, 1]
+    assert all(int(o) % 64 == 0 for o in ext["msg_offset"])
+    ends = ext["msg_offset"] + ext["msg_len"]
+    assert np.all(ext["msg_offset"][1:] >= ends[:-1])
+    assert total % 64 == 0 and total >= int(ends[-1])
+
+
+def test_stage_file_host_only(tmp_path):
+    # staging needs no device: pread of header / samples / tail into the extent
+    from oracle import cas_spec as cs
+    from spacedrive_amd.device import stage_plan
+    sizes = [100, 102400, 300000]
+    paths = []
+    for i, s in enumerate(sizes):
+        p = tmp_path / f"f{i}"
+        p.write_bytes(cs.synth_bytes(40 + i, 0, 0, s))
+        paths.append(p)
+    ext, total = stage_plan(np.array(sizes, np.uint64))
+    staged = np.full(total, 0xAB, np.uint8)
+    for i, p in enumerate(paths):
+        st = ctypes.c_int32(-1)
+        check(lib().sd_cas_stage_file(os.fsencode(p), ctypes.c_void_p(ext.ctypes.data + 24 * i),
+                                      ctypes.c_void_p(staged.ctypes.data), ctypes.byref(st)))
+        assert st.value == 0
+        msg = cs.cas_message(cs.synth_reader(40 + i), sizes[i])
+        o = int(ext["msg_offset"][i])
+        assert staged[o:o + len(msg)].tobytes() == msg
+        pad_end = (o + len(msg) + 63) // 64 * 64
+        assert not staged[o + len(msg):pad_end].any()  # zero padding
+
+
+def test_stage_file_errors(tmp_path):
+    from spacedrive_amd.device import stage_plan
+    ext, total = stage_plan(np.array([200000], np.uint64))
+    staged = np.zeros(total, np.uint8)
+    st = ctypes.c_int32(-1)
+    check(lib().sd_cas_stage_file(b"/nonexistent/x", ctypes.c_void_p(ext.ctypes.data),
+                                  ctypes.c_void_p(staged.ctypes.data), ctypes.byref(st)))
+    assert st.value & 0xFFFF == _native.SD_FILE_IO_ERROR and (st.value >> 16) == 2  # ENOENT
+    short = tmp_path / "short"
+    short.write_bytes(b"x" * 150000)  # shorter than the planned 200000: read_exact EOF
+    check(lib().sd_cas_stage_file(os.fsencode(short), ctypes.c_void_p(ext.ctypes.data),
+                                  ctypes.c_void_p(staged.ctypes.data), ctypes.byref(st)))
+    assert st.value == _native.SD_FILE_SHORT_READ
+
+
+def test_invalid_arguments_do_not_cross_boundary():
+    rc = lib().sd_cas_stage_plan(None, 3, None, None)
+    assert rc == -1 and b"null" in lib().sd_cas_last_error()
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="GPU present")
+def test_no_cpu_fallback_without_gpu():
+    h = ctypes.c_void_p()
+    with pytest.raises(SdCasError) as e:
+        check(lib().sd_cas_ctx_create(0, ctypes.byref(h)))
+    assert e.value.rc == -2

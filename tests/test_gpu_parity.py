@@ -1,0 +1,260 @@
+"""Parity of the HIP path (through the C ABI) with the oracle -- run on an MI355X: -m gpu.
+
+Bit-exact on every byte: the full 32-byte BLAKE3 of every staged message, the 16-hex
+cas_id, the 64-hex checksum, and the dedup grouping.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import cas_spec as cs  # noqa: E402
+from spacedrive_amd import synth  # noqa: E402
+from spacedrive_amd.dedup import group_host, keys_from_hashes, partition_host  # noqa: E402
+
+NT = 8  # oracle threads on the GPU box's host
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import spacedrive_amd
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    c = spacedrive_amd.default_context(0)
+    # the product library must be the in-tree HIP build
+    maps = open("/proc/self/maps").read()
+    assert "spacedrive_amd/libsdcas.so" in maps
+    return c
+
+
+def stage_synth(ctx, sizes, cids, twins):
+    from spacedrive_amd.device import stage_plan
+    n = len(sizes)
+    ext, total = stage_plan(sizes)
+    d_staged = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    d_ext = torch.from_numpy(ext.view(np.uint8).copy()).cuda()
+    ctx.synth_stage_cas(torch.from_numpy(sizes.astype(np.uint64).view(np.int64)).cuda(),
+                        torch.from_numpy(cids.astype(np.uint64).view(np.int64)).cuda(),
+                        torch.from_numpy(twins.astype(np.int32)).cuda(), d_ext, n, d_staged)
+    return ext, total, d_staged
+
+
+def gpu_cas(ctx, sizes, cids, twins, return_staged=False):
+    ext, total, d_staged = stage_synth(ctx, sizes, cids, twins)
+    b = ctx.cas_batch(ext)
+    out = torch.zeros(max(len(sizes), 1) * 32, dtype=torch.uint8, device="cuda")
+    b.run(d_staged, out)
+    torch.cuda.synchronize()
+    h = out.cpu().numpy()[:len(sizes) * 32].reshape(-1, 32)
+    if return_staged:
+        return h, ext, d_staged.cpu().numpy()
+    return h
+
+
+def test_synth_stage_matches_oracle_messages(ctx, oracle_native):
+    sizes = np.array([0, 1, 7, 8, 9, 1015, 1016, 1017, 102400, 102401, 555555, (1 << 32) + 1], np.uint64)
+    cids = np.arange(100, 100 + len(sizes), dtype=np.uint64)
+    twins = np.zeros(len(sizes), np.uint32)
+    twins[-2] = 9
+    _, ext, staged = gpu_cas(ctx, sizes, cids, twins, return_staged=True)
+    for i in range(len(sizes)):
+        o, L = int(ext["msg_offset"][i]), int(ext["msg_len"][i])
+        want = oracle_native.cas_message(int(cids[i]), int(twins[i]), int(sizes[i]))
+        assert staged[o:o + L].tobytes() == want, i
+        pad = (o + L + 63) // 64 * 64
+        assert not staged[o + L:pad].any()
+
+
+def test_cas_goldens(ctx, golden):
+    files = golden["cas_synth"]["files"]
+    sizes = np.array([f["size"] for f in files], np.uint64)
+    cids = np.array([f["content_id"] for f in files], np.uint64)
+    twins = np.array([f["twin"] for f in files], np.uint32)
+    h = gpu_cas(ctx, sizes, cids, twins)
+    for f, row in zip(files, h):
+        assert row[:8].tobytes().hex() == f["cas_id"], f
+
+
+def test_cas_pattern_goldens_host_staged(ctx, golden):
+    # host-staged pattern content through the drop-in sd_cas_ids entry point
+    import ctypes
+    from spacedrive_amd._native import check, lib
+    from spacedrive_amd.device import stage_plan
+    cp = golden["cas_pattern"]["cas_id"]
+    sizes = np.array([int(s) for s in cp], np.uint64)
+    ext, total = stage_plan(sizes)
+    staged = np.zeros(total, np.uint8)
+    reader = lambda o, n: bytes((o + k) % 251 for k in range(n))  # noqa: E731
+    for i, s in enumerate(sizes):
+        msg = cs.cas_message(reader, int(s))
+        o = int(ext["msg_offset"][i])
+        staged[o:o + len(msg)] = np.frombuffer(msg, np.uint8)
+    out = ctypes.create_string_buffer(17 * len(sizes))
+    check(lib().sd_cas_ids(ctx.handle, staged.ctypes.data, total, ext.ctypes.data, len(sizes), out, None))
+    for i, s in enumerate(cp):
+        assert out.raw[17 * i:17 * i + 16].decode() == cp[s], s
+
+
+def test_cas_exhaustive_small_sizes(ctx, oracle_native):
+    # every message length across the first three chunks and the whole-file threshold
+    sizes = np.concatenate([np.arange(0, 3200), np.arange(101000, 102500)]).astype(np.uint64)
+    cids = np.arange(len(sizes), dtype=np.uint64) + 7
+    twins = np.zeros(len(sizes), np.uint32)
+    h, ext, staged = gpu_cas(ctx, sizes, cids, twins, return_staged=True)
+    full = oracle_native.checksums(staged, ext["msg_offset"], ext["msg_len"].astype(np.uint64), nthreads=NT)
+    mism = np.nonzero((h != full).any(axis=1))[0]
+    assert len(mism) == 0, [(int(sizes[i])) for i in mism[:10]]
+
+
+def test_cas_mixture_full_hash_vs_oracle(ctx, oracle_native):
+    # configs[0]-style mixture incl. dups, twins and every edge size; full 32-byte hashes
+    n = 30000
+    sizes, cids, twins = synth.library(0, n, n)
+    h, ext, staged = gpu_cas(ctx, sizes, cids, twins, return_staged=True)
+    full = oracle_native.checksums(staged, ext["msg_offset"], ext["msg_len"].astype(np.uint64), nthreads=NT)
+    assert np.array_equal(h, full)
+    # and the message bytes are the reference's (oracle builds them from the generator)
+    ids = oracle_native.cas_ids_synth(sizes, cids, twins, nthreads=NT)
+    assert np.array_equal(h[:, :8], ids)
+
+
+def test_cas_configs0_full_size_and_idempotent(ctx, oracle_native):
+    # configs[0]: 100k mixed files -- full size, bit-exact vs the oracle, twice
+    n = 100_000
+    sizes, cids, twins = synth.library(0, n, n)
+    h1 = gpu_cas(ctx, sizes, cids, twins)
+    h2 = gpu_cas(ctx, sizes, cids, twins)
+    assert np.array_equal(h1, h2)
+    ids = oracle_native.cas_ids_synth(sizes, cids, twins, nthreads=NT)
+    assert np.array_equal(h1[:, :8], ids)
+
+
+def test_cas_all_sampled_batch_shapes(ctx, oracle_native):
+    # 1..17 sampled files: partial last workgroup of 8 files
+    for n in (1, 7, 8, 9, 17):
+        sizes = np.full(n, 200001, np.uint64) + np.arange(n, dtype=np.uint64) * 4099
+        cids = np.arange(n, dtype=np.uint64)
+        h = gpu_cas(ctx, sizes, cids, np.zeros(n, np.uint32))
+        assert np.array_equal(h[:, :8], oracle_native.cas_ids_synth(sizes, cids)), n
+
+
+def test_sample_twins_and_duplicates(ctx):
+    sizes = np.array([5 << 20, 5 << 20, 5 << 20, 3000, 3000], np.uint64)
+    cids = np.array([1, 1, 1, 2, 2], np.uint64)
+    twins = np.array([0, 0, 4, 0, 0], np.uint32)
+    h = gpu_cas(ctx, sizes, cids, twins)
+    assert h[0, :8].tobytes() == h[1, :8].tobytes() == h[2, :8].tobytes()  # twin: same cas_id
+    assert h[3].tobytes() == h[4].tobytes()
+
+
+# ------------------------------------------------------------------------ checksums
+def gpu_checksums(ctx, lens, cids, twins):
+    offs, off = [], 0
+    for L in lens:
+        offs.append(off)
+        off = (off + int(L) + 64 + 63) // 64 * 64
+    d = torch.zeros(off + 64, dtype=torch.uint8, device="cuda")
+    for L, o, c, t in zip(lens, offs, cids, twins):
+        if L:
+            ctx.synth_fill(int(c), int(t), int(L), d[o:])
+    b = ctx.checksum_batch(offs, lens)
+    out = torch.zeros(max(len(lens), 1) * 32, dtype=torch.uint8, device="cuda")
+    b.run(d, out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()[:len(lens) * 32].reshape(-1, 32)
+
+
+def test_checksum_goldens(ctx, golden):
+    files = golden["checksum_synth"]["files"]
+    lens = [f["size"] for f in files]
+    h = gpu_checksums(ctx, lens, [f["content_id"] for f in files], [f["twin"] for f in files])
+    for f, row in zip(files, h):
+        assert row.tobytes().hex() == f["checksum"], f
+
+
+def test_checksum_sizes_vs_oracle(ctx, oracle_native):
+    MiB = 1 << 20
+    lens = [0, 1, 1024, 1025, 4096, 4097, 5 * 1024, MiB - 1, MiB, MiB + 1, 4 * MiB + 3, 7 * MiB,
+            256 * MiB, 256 * MiB + 1, 300 * MiB + 17, 3 * 1024 + 1, 1020 * 1024 + 5]
+    cids = list(range(500, 500 + len(lens)))
+    twins = [i % 3 for i in range(len(lens))]
+    h = gpu_checksums(ctx, lens, cids, twins)
+    want = oracle_native.checksums_synth(np.array(lens, np.uint64), np.array(cids, np.uint64),
+                                         np.array(twins, np.uint32), nthreads=NT)
+    bad = [lens[i] for i in range(len(lens)) if h[i].tobytes() != want[i].tobytes()]
+    assert not bad, bad
+
+
+def test_file_api_on_disk(ctx, tmp_path, golden):
+    import spacedrive_amd as sd
+    sizes = [0, 1, 1017, 102400, 102401, 2 << 20, 300 * (1 << 20) + 5]
+    paths = []
+    for i, s in enumerate(sizes):
+        p = tmp_path / f"f{i}.bin"
+        with open(p, "wb") as f:
+            pos = 0
+            while pos < s:
+                n = min(64 << 20, s - pos)
+                f.write(cs.synth_bytes(60 + i, 0, pos, n))
+                pos += n
+        paths.append(str(p))
+    ids = sd.generate_cas_ids(paths, sizes)
+    for i, s in enumerate(sizes):
+        assert ids[i] == cs.generate_cas_id(cs.synth_reader(60 + i), s), s
+    sums = sd.file_checksums(paths)
+    from oracle import native
+    want = native.checksums_synth(np.array(sizes, np.uint64), np.arange(60, 60 + len(sizes), dtype=np.uint64),
+                                  nthreads=NT)
+    for i in range(len(sizes)):
+        assert sums[i] == want[i].tobytes().hex(), sizes[i]
+    assert sd.file_checksum(paths[2]) == sums[2]
+    assert sd.generate_cas_id(paths[4], sizes[4]) == ids[4]
+    # FileMetadata: empty file -> cas_id None (file_identifier/mod.rs:80-88)
+    md = sd.FileMetadata.batch(paths[:3])
+    assert md[0].cas_id is None and md[1].cas_id == ids[1]
+    # errors: missing file, and a file shorter than the size it was planned with
+    r = sd.generate_cas_ids([str(tmp_path / "missing"), paths[5]], [10, (2 << 20) + 100])
+    assert isinstance(r[0], FileNotFoundError) or (isinstance(r[0], OSError) and r[0].errno == 2)
+    assert isinstance(r[1], sd.UnexpectedEofError)
+    with pytest.raises(OSError):
+        sd.file_checksum(str(tmp_path / "missing"))
+
+
+# ---------------------------------------------------------------------------- dedup
+def test_dedup_group_matches_host(ctx):
+    n = 50000
+    sizes, cids, twins = synth.library(0, n, n, dup_frac=0.3)
+    h = gpu_cas(ctx, sizes, cids, twins)
+    d_hash = torch.from_numpy(h.copy()).cuda()
+    valid = (sizes != 0).astype(np.uint8)
+    d_valid = torch.from_numpy(valid).cuda()
+    keys = keys_from_hashes(h)
+    idx = np.arange(n, dtype=np.int64)
+    for nparts in (1, 2, 8):
+        counts = torch.zeros(nparts, dtype=torch.int64, device="cuda")
+        recs = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+        nv = ctx.dedup_partition(d_hash, d_valid, n, 0, nparts, counts, recs)
+        assert nv == int(valid.sum())
+        hrecs, hcounts = partition_host(keys[valid == 1], idx[valid == 1], nparts)
+        assert counts.cpu().numpy().tolist() == hcounts.tolist()
+        r = recs[:nv].cpu().numpy()
+        start = 0
+        for d in range(nparts):  # each destination holds exactly the host's set
+            seg = r[start:start + hcounts[d]]
+            hseg = hrecs[start:start + hcounts[d]]
+            assert sorted(map(tuple, seg.tolist())) == sorted(map(tuple, hseg.tolist()))
+            start += hcounts[d]
+            sub = torch.from_numpy(seg.copy()).cuda()
+            rep = torch.zeros(max(len(seg), 1), dtype=torch.int64, device="cuda")
+            ng = ctx.dedup_group(sub, len(seg), rep)
+            gr, grep, gng = group_host(seg)
+            assert ng == gng
+            assert np.array_equal(sub.cpu().numpy(), gr)
+            assert np.array_equal(rep.cpu().numpy()[:len(seg)], grep)
+
+
+def test_valu_peak_plausible(ctx):
+    v = ctx.valu_peak()
+    assert 5e12 < v < 2e14, v
