@@ -19,8 +19,9 @@
  *     apps/mobile/modules/sd-core/ios/crate/src/lib.rs:36-86);
  *   - return value: SD_OK (0) or a negative sd_rc for the whole call; per-file outcomes go
  *     to an int32 status array (sd_file_status);
- *   - `stream` arguments are hipStream_t passed as void* (NULL = the context's stream);
- *     device-pointer entry points only enqueue work and do not synchronise;
+ *   - `stream` arguments are hipStream_t passed as void*; NULL is HIP's null (default)
+ *     stream, as everywhere in HIP.  Device-pointer entry points only enqueue work on it
+ *     and do not synchronise (the dedup calls return host counts and so do sync it);
  *   - the library has no CPU fallback: without a usable gfx950 device every compute entry
  *     point fails with SD_ERR_DEVICE.
  */

@@ -157,7 +157,7 @@ struct sd_cas_ctx {
         free_slots.push_back(std::move(s));
     }
     void bind() { HIP_CHECK(hipSetDevice(device)); }
-    hipStream_t pick(void* s) const { return s ? reinterpret_cast<hipStream_t>(s) : stream; }
+    static hipStream_t pick(void* s) { return reinterpret_cast<hipStream_t>(s); }  // NULL = null stream
 };
 
 struct sd_cas_batch {
@@ -727,14 +727,19 @@ int sd_dedup_partition(sd_cas_ctx* ctx, const uint8_t* d_hash32, const uint8_t* 
     if (nparts < 1 || nparts > 64) throw sd_failure(SD_ERR_INVALID, "nparts must be in [1, 64]");
     ctx->bind();
     hipStream_t s = ctx->pick(stream);
-    DevBuf cursor;
-    cursor.alloc((nparts + 1) * sizeof(uint64_t));
-    HIP_CHECK(sdk::dedup_partition(d_hash32, d_valid, n, global_index_base, nparts, d_counts, d_records,
-                                   cursor.as<uint64_t>(), s));
-    uint64_t tot = 0;
-    HIP_CHECK(hipMemcpyAsync(&tot, cursor.as<uint64_t>() + nparts, sizeof tot, hipMemcpyDeviceToHost, s));
+    auto slot = ctx->acquire();  // scratch reused across calls; released after the sync below
+    struct Rel {
+        sd_cas_ctx* c;
+        std::unique_ptr<Slot>* s;
+        ~Rel() { c->release(std::move(*s)); }
+    } rel{ctx, &slot};
+    slot->hashes.ensure((nparts + 1) * sizeof(uint64_t));
+    slot->host_hashes.ensure(sizeof(uint64_t));
+    uint64_t* cursor = slot->hashes.as<uint64_t>();
+    HIP_CHECK(sdk::dedup_partition(d_hash32, d_valid, n, global_index_base, nparts, d_counts, d_records, cursor, s));
+    HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, cursor + nparts, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    *n_valid = tot;
+    *n_valid = *reinterpret_cast<uint64_t*>(slot->host_hashes.p);
     return SD_OK;
     SD_GUARD_END
 }
@@ -747,14 +752,20 @@ int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, uint64_t* d
     hipStream_t s = ctx->pick(stream);
     size_t need = 0;
     HIP_CHECK(sdk::dedup_group(d_records, m, d_rep, nullptr, nullptr, &need, s));
-    DevBuf scratch, ng;
-    scratch.alloc(need);
-    ng.alloc(sizeof(uint64_t));
-    HIP_CHECK(sdk::dedup_group(d_records, m, d_rep, ng.as<uint64_t>(), scratch.p, &need, s));
-    uint64_t g = 0;
-    HIP_CHECK(hipMemcpyAsync(&g, ng.p, sizeof g, hipMemcpyDeviceToHost, s));
+    auto slot = ctx->acquire();
+    struct Rel {
+        sd_cas_ctx* c;
+        std::unique_ptr<Slot>* s;
+        ~Rel() { c->release(std::move(*s)); }
+    } rel{ctx, &slot};
+    slot->staged.ensure(need);
+    slot->hashes.ensure(sizeof(uint64_t));
+    slot->host_hashes.ensure(sizeof(uint64_t));
+    size_t have = slot->staged.bytes;
+    HIP_CHECK(sdk::dedup_group(d_records, m, d_rep, slot->hashes.as<uint64_t>(), slot->staged.p, &have, s));
+    HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, slot->hashes.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    *n_groups = g;
+    *n_groups = *reinterpret_cast<uint64_t*>(slot->host_hashes.p);
     return SD_OK;
     SD_GUARD_END
 }
