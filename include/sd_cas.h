@@ -182,6 +182,10 @@ int sd_cas_batch_time(sd_cas_ctx* ctx, const sd_cas_batch* batch, const uint8_t*
                       uint8_t* d_hash32, int iters, void* stream, float* ms_total);
 int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, const uint8_t* d_data,
                            uint8_t* d_hash32, int iters, void* stream, float* ms_total);
+/* Process-wide kernel-variant knobs for A/B measurement (results are identical for
+ * every value): "sampled_variant" = 10*U + prefetch with U in {1,2,4} chunks per lane
+ * (default 41), "whole_variant", "checksum_variant" (default 0). */
+int sd_cas_set_tuning(const char* key, int value);
 /* VALU integer-throughput microbenchmark: returns measured lane-ops/s (BLAKE3 ARX mix). */
 int sd_valu_peak(sd_cas_ctx* ctx, double* lane_ops_per_s);
 

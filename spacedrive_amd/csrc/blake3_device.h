@@ -155,4 +155,60 @@ __device__ __forceinline__ void full_chunk_cv(uint32_t (&cv)[8], const uint8_t* 
     compress(cv, m, clo, chi, BLOCK_LEN, CHUNK_END);
 }
 
+// Merge of U consecutive, full, non-root chunks c0..c0+U-1 (an aligned group, U = 1, 2, 4):
+// the chunk CVs merged level-wise in-lane -> `out`.  The message streams through two
+// register buffers: block k+1 is loaded while block k is compressed (PF = true), so a
+// lane always has one 64-byte load in flight behind its compression.
+template <int U, bool PF>
+__device__ __forceinline__ void full_chunks_cv(uint32_t (&out)[8], const uint8_t* __restrict__ p, uint64_t c0) {
+    static_assert(U == 1 || U == 2 || U == 4, "U");
+    uint32_t held[2][8];  // level-wise merge stack: at most two pending nodes for U <= 4
+    uint32_t ma[16], mb[16];
+    if (PF) load_block(ma, p);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        uint32_t cv[8];
+        set_iv(cv);
+        const uint64_t ctr = c0 + u;
+        const uint32_t clo = (uint32_t)ctr, chi = (uint32_t)(ctr >> 32);
+        const uint8_t* q = p + (size_t)u * CHUNK_LEN;
+#pragma unroll 1
+        for (uint32_t b = 0; b < 16; b += 2) {
+            const uint32_t f0 = b == 0 ? CHUNK_START : 0u;
+            const uint32_t f1 = b + 1 == 15 ? CHUNK_END : 0u;
+            if (PF) {
+                load_block(mb, q + 64u * (b + 1));
+                compress(cv, ma, clo, chi, BLOCK_LEN, f0);
+                // next block: b + 2 of this chunk, or block 0 of the next chunk (the last
+                // lane block re-reads itself rather than run past the group)
+                const uint32_t nb = (uint32_t)u * 16 + b + 2;
+                load_block(ma, p + 64u * (nb < 16u * U ? nb : 16u * U - 1));
+                compress(cv, mb, clo, chi, BLOCK_LEN, f1);
+            } else {
+                load_block(ma, q + 64u * b);
+                compress(cv, ma, clo, chi, BLOCK_LEN, f0);
+                load_block(ma, q + 64u * (b + 1));
+                compress(cv, ma, clo, chi, BLOCK_LEN, f1);
+            }
+        }
+        if (U == 1) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) out[i] = cv[i];
+        } else if (u == 0 || u == 2) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) held[u >> 1][i] = cv[i];
+        } else if (u == 1) {
+            parent(out, held[0], cv, 0u);
+            if (U == 4) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) held[0][i] = out[i];
+            }
+        } else {  // u == 3
+            uint32_t p23[8];
+            parent(p23, held[1], cv, 0u);
+            parent(out, held[0], p23, 0u);
+        }
+    }
+}
+
 }  // namespace sdb3

@@ -65,65 +65,75 @@ __device__ void lds_reduce(uint32_t (*lds)[8], uint32_t n, bool root) {
 }  // namespace
 
 // ------------------------------------------------------------------------ sampled cas
-constexpr int S_FILES = 8;       // files per workgroup
+// 448 lanes = 7 waves.  Each lane hashes U consecutive full chunks of one file (an
+// aligned group) and merges them in-lane, so a workgroup covers 8U files.  Per file the
+// 56/U lane CVs plus the 8-byte tail chunk (node 56/U, message bytes 57344..57351) are
+// merged level-wise in LDS; the tail is hashed during the first level by lanes that have
+// no parent to compute (the first level always has 224 parents, and an odd node count,
+// so the tail is the carried node).
 constexpr int S_FULL = 56;       // full chunks per sampled message (57344 bytes)
-constexpr int S_NODES = 57;      // + the 8-byte tail chunk
-constexpr int S_THREADS = S_FILES * S_FULL;  // 448 = 7 waves
+constexpr int S_THREADS = 448;
 
+template <int U, bool PF>
 __global__ __launch_bounds__(S_THREADS) void k_cas_sampled(const uint8_t* __restrict__ staged,
                                                            const sd_extent* __restrict__ ext,
                                                            const uint32_t* __restrict__ idx,
                                                            uint32_t n, uint32_t* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint32_t cvs[S_FILES][S_NODES][8];
+    constexpr int LANES = S_FULL / U;     // lanes per file
+    constexpr int F = S_THREADS / LANES;  // files per workgroup = 8U
+    constexpr int N0 = LANES + 1;         // nodes per file entering the tree
+    __shared__ __attribute__((aligned(16))) uint32_t cvs[F][N0][8];
     const uint32_t t = threadIdx.x;
-    const uint32_t f = t / S_FULL, c = t % S_FULL;
-    const uint32_t g = blockIdx.x * S_FILES + f;
-    if (g < n) {
-        const uint8_t* msg = staged + ext[idx[g]].msg_offset;
-        uint32_t cv[8];
-        full_chunk_cv(cv, msg + (size_t)c * CHUNK_LEN, c);
-        store_cv(cvs[f][c], cv);
-    }
-    if (t < S_FILES) {  // the 8-byte tail chunk (chunk 56: message bytes 57344..57351)
-        const uint32_t gt = blockIdx.x * S_FILES + t;
-        if (gt < n) {
-            const uint8_t* msg = staged + ext[idx[gt]].msg_offset;
+    {
+        const uint32_t f = t / LANES, j = t % LANES;
+        const uint32_t g = blockIdx.x * F + f;
+        if (g < n) {
+            const uint8_t* msg = staged + ext[idx[g]].msg_offset;
             uint32_t cv[8];
-            chunk_cv(cv, msg + (size_t)S_FULL * CHUNK_LEN, SD_SAMPLED_MSG_LEN - S_FULL * CHUNK_LEN, S_FULL,
-                     false);
-            store_cv(cvs[t][S_FULL], cv);
+            full_chunks_cv<U, PF>(cv, msg + (size_t)j * U * CHUNK_LEN, (uint64_t)j * U);
+            store_cv(cvs[f][j], cv);
         }
     }
     __syncthreads();
-    // 57 -> 29 -> 15 -> 8 -> 4 -> 2 -> 1, 8 files side by side
-    uint32_t nodes = S_NODES;
+    uint32_t nodes = N0;
 #pragma unroll 1
-    while (nodes > 1) {
+    for (int level = 0; nodes > 1; level++) {
         const uint32_t P = nodes >> 1;
         const bool carry = nodes & 1u;
         uint32_t res[8];
         bool have = false;
         uint32_t ff = 0, p = 0;
-        if (t < S_FILES * P) {
+        if (t < F * P) {
             ff = t / P; p = t % P;
             uint32_t l[8], r[8];
             load_cv(l, cvs[ff][2 * p]);
             load_cv(r, cvs[ff][2 * p + 1]);
             parent(res, l, r, nodes == 2 ? ROOT : 0u);
             have = true;
-        } else if (carry && t >= 256 && t < 256 + S_FILES) {  // a wave with no parent work
-            ff = t - 256; p = P;
-            load_cv(res, cvs[ff][nodes - 1]);
-            have = true;
+        } else if (carry) {
+            if (level == 0) {  // lanes [224, 224 + F): the tail chunk (8 bytes, chunk index 56)
+                const uint32_t gt = blockIdx.x * F + (t - F * P);
+                if (t < F * P + F && gt < n) {
+                    ff = t - F * P; p = P;
+                    const uint8_t* msg = staged + ext[idx[gt]].msg_offset;
+                    chunk_cv(res, msg + (size_t)S_FULL * CHUNK_LEN, SD_SAMPLED_MSG_LEN - S_FULL * CHUNK_LEN, S_FULL,
+                             false);
+                    have = true;
+                }
+            } else if (t >= 256 && t < 256 + F) {  // a wave with no parent work carries the odd node
+                ff = t - 256; p = P;
+                load_cv(res, cvs[ff][nodes - 1]);
+                have = true;
+            }
         }
         __syncthreads();
         if (have) store_cv(cvs[ff][p], res);
         __syncthreads();
         nodes = P + (carry ? 1u : 0u);
     }
-    if (t < S_FILES * 8) {
+    if (t < F * 8) {
         const uint32_t ff = t >> 3, w = t & 7;
-        const uint32_t gg = blockIdx.x * S_FILES + ff;
+        const uint32_t gg = blockIdx.x * F + ff;
         if (gg < n) out[(size_t)idx[gg] * 8 + w] = cvs[ff][0][w];
     }
 }
@@ -284,8 +294,19 @@ namespace sdk {
 hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const uint32_t* idx, uint32_t n,
                               uint32_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const uint32_t grid = (n + S_FILES - 1) / S_FILES;
-    hipLaunchKernelGGL(k_cas_sampled, dim3(grid), dim3(S_THREADS), 0, s, staged, ext, idx, n, out);
+    const int v = tuning_get(SD_TUNE_SAMPLED_VARIANT);
+#define SD_LAUNCH_SAMPLED(U, PF)                                                                        \
+    hipLaunchKernelGGL((k_cas_sampled<U, PF>), dim3((n + 8 * U - 1) / (8 * U)), dim3(S_THREADS), 0, s, staged, \
+                       ext, idx, n, out)
+    switch (v) {
+        case 10: SD_LAUNCH_SAMPLED(1, false); break;
+        case 11: SD_LAUNCH_SAMPLED(1, true); break;
+        case 20: SD_LAUNCH_SAMPLED(2, false); break;
+        case 21: SD_LAUNCH_SAMPLED(2, true); break;
+        case 40: SD_LAUNCH_SAMPLED(4, false); break;
+        default: SD_LAUNCH_SAMPLED(4, true); break;
+    }
+#undef SD_LAUNCH_SAMPLED
     return hipGetLastError();
 }
 

@@ -28,39 +28,129 @@ __device__ __forceinline__ uint32_t dest_of(uint64_t key, int nparts) {
     return (uint32_t)(((key >> 48) * (uint64_t)nparts) >> 16);  // top 16 bits scaled: contiguous ranges
 }
 
+// Deterministic, contention-free partition in two passes over a fixed grid of PART_BLOCKS
+// workgroups, each owning one contiguous slice of the input:
+//   count:   per (destination, block) histogram, wave-aggregated into LDS;
+//   scan:    one workgroup turns the histogram into destination-major offsets;
+//   scatter: each block walks its slice again in order; a record's position is its
+//            block's offset for its destination + its rank among earlier records of the
+//            same destination (ballot/popcount inside a wave, LDS counts across waves).
+// Output is stable: grouped by destination, in input order within a destination.
+constexpr uint32_t PART_BLOCKS = 1024;
+constexpr uint32_t PART_MAXD = 64;
+
+struct slice_t { uint64_t lo, hi; };
+__device__ __forceinline__ slice_t slice_of(uint64_t n, uint32_t b) {
+    const uint64_t per = (n + PART_BLOCKS - 1) / PART_BLOCKS;
+    uint64_t lo = (uint64_t)b * per, hi = lo + per;
+    if (lo > n) lo = n;
+    if (hi > n) hi = n;
+    return {lo, hi};
+}
+
+// rank of this lane among active lanes with the same destination, and that group's size
+__device__ __forceinline__ void wave_match(bool active, uint32_t d, uint32_t& rank, uint32_t& size, bool& leader) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t remaining = __ballot(active);
+    rank = 0; size = 0; leader = false;
+    while (remaining) {
+        const uint32_t first = __builtin_ctzll(remaining);
+        const uint32_t dl = __shfl(d, first);
+        const uint64_t m = __ballot(active && d == dl);
+        if (active && d == dl) {
+            rank = __popcll(m & ((1ull << lane) - 1));
+            size = __popcll(m);
+            leader = lane == first;
+        }
+        remaining &= ~m;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_part_count(const uint8_t* __restrict__ hash32,
                                                     const uint8_t* __restrict__ valid, uint64_t n, int nparts,
-                                                    unsigned long long* __restrict__ counts) {
-    __shared__ unsigned long long local[64];
-    if (threadIdx.x < 64) local[threadIdx.x] = 0;
+                                                    uint32_t* __restrict__ hist) {
+    __shared__ uint32_t local[PART_MAXD];
+    if (threadIdx.x < PART_MAXD) local[threadIdx.x] = 0;
     __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        if (valid && !valid[i]) continue;
-        atomicAdd(&local[dest_of(cas_key(hash32 + i * 32), nparts)], 1ull);
+    const slice_t sl = slice_of(n, blockIdx.x);
+    for (uint64_t base = sl.lo; base < sl.hi; base += blockDim.x) {
+        const uint64_t i = base + threadIdx.x;
+        const bool act = i < sl.hi && (!valid || valid[i]);
+        const uint32_t d = act ? dest_of(cas_key(hash32 + i * 32), nparts) : 0;
+        uint32_t rank, size;
+        bool leader;
+        wave_match(act, d, rank, size, leader);
+        if (leader) atomicAdd(&local[d], size);
     }
     __syncthreads();
-    if (threadIdx.x < (unsigned)nparts && local[threadIdx.x]) atomicAdd(&counts[threadIdx.x], local[threadIdx.x]);
+    if (threadIdx.x < (unsigned)nparts) hist[threadIdx.x * PART_BLOCKS + blockIdx.x] = local[threadIdx.x];
 }
 
-// cursor[d] starts at the exclusive prefix of counts; records land grouped by destination
+// exclusive scan of hist[nparts * PART_BLOCKS] (destination-major) -> offs; counts[d]
+__global__ __launch_bounds__(1024) void k_part_scan(const uint32_t* __restrict__ hist, int nparts,
+                                                    uint64_t* __restrict__ offs,
+                                                    unsigned long long* __restrict__ counts,
+                                                    unsigned long long* __restrict__ total) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int d = 0; d < nparts; d++) {
+        const uint64_t v = hist[d * PART_BLOCKS + threadIdx.x];
+        uint64_t x = v;  // inclusive wave scan
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(x, o);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        uint64_t before = carry;
+        for (uint32_t k = 0; k < w; k++) before += wsum[k];
+        offs[d * PART_BLOCKS + threadIdx.x] = before + x - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) {
+            counts[d] = before + x - carry;
+            carry = before + x;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
 __global__ __launch_bounds__(256) void k_part_scatter(const uint8_t* __restrict__ hash32,
-                                                      const uint8_t* __restrict__ valid, uint64_t n, uint64_t base,
-                                                      int nparts, unsigned long long* __restrict__ cursor,
+                                                      const uint8_t* __restrict__ valid, uint64_t n, uint64_t base_idx,
+                                                      int nparts, const uint64_t* __restrict__ offs,
                                                       uint64_t* __restrict__ records) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        if (valid && !valid[i]) continue;
-        const uint64_t key = cas_key(hash32 + i * 32);
-        const unsigned long long pos = atomicAdd(&cursor[dest_of(key, nparts)], 1ull);
-        records[2 * pos] = key;
-        records[2 * pos + 1] = base + i;
-    }
-}
-
-__global__ void k_prefix_small(const unsigned long long* counts, int nparts, unsigned long long* cursor) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        unsigned long long acc = 0;
-        for (int d = 0; d < nparts; d++) { cursor[d] = acc; acc += counts[d]; }
-        cursor[nparts] = acc;
+    __shared__ uint64_t run[PART_MAXD];
+    __shared__ uint32_t wcnt[4][PART_MAXD];
+    const uint32_t w = threadIdx.x >> 6;
+    if (threadIdx.x < (unsigned)nparts) run[threadIdx.x] = offs[threadIdx.x * PART_BLOCKS + blockIdx.x];
+    for (uint32_t k = threadIdx.x; k < 4 * PART_MAXD; k += blockDim.x) (&wcnt[0][0])[k] = 0;
+    __syncthreads();
+    const slice_t sl = slice_of(n, blockIdx.x);
+    for (uint64_t base = sl.lo; base < sl.hi; base += blockDim.x) {
+        const uint64_t i = base + threadIdx.x;
+        const bool act = i < sl.hi && (!valid || valid[i]);
+        const uint64_t key = act ? cas_key(hash32 + i * 32) : 0;
+        const uint32_t d = act ? dest_of(key, nparts) : 0;
+        uint32_t rank, size;
+        bool leader;
+        wave_match(act, d, rank, size, leader);
+        if (leader) wcnt[w][d] = size;
+        __syncthreads();
+        if (act) {
+            uint64_t pos = run[d] + rank;
+            for (uint32_t k = 0; k < w; k++) pos += wcnt[k][d];
+            records[2 * pos] = key;
+            records[2 * pos + 1] = base_idx + i;
+        }
+        __syncthreads();
+        if (threadIdx.x < (unsigned)nparts)
+            run[threadIdx.x] += wcnt[0][threadIdx.x] + wcnt[1][threadIdx.x] + wcnt[2][threadIdx.x] + wcnt[3][threadIdx.x];
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < 4 * PART_MAXD; k += blockDim.x) (&wcnt[0][0])[k] = 0;
+        __syncthreads();
     }
 }
 
@@ -111,16 +201,21 @@ uint32_t grid_for(uint64_t n) {
 namespace sdk {
 
 hipError_t dedup_partition(const uint8_t* hash32, const uint8_t* valid, uint64_t n, uint64_t base, int nparts,
-                           uint64_t* counts, uint64_t* records, uint64_t* cursor_scratch, hipStream_t s) {
-    auto* c = reinterpret_cast<unsigned long long*>(counts);
-    auto* cur = reinterpret_cast<unsigned long long*>(cursor_scratch);
-    hipError_t e = hipMemsetAsync(c, 0, sizeof(uint64_t) * nparts, s);
-    if (e != hipSuccess) return e;
-    if (n) hipLaunchKernelGGL(k_part_count, dim3(grid_for(n)), dim3(256), 0, s, hash32, valid, n, nparts, c);
-    hipLaunchKernelGGL(k_prefix_small, dim3(1), dim3(64), 0, s, c, nparts, cur);
-    if (n) hipLaunchKernelGGL(k_part_scatter, dim3(grid_for(n)), dim3(256), 0, s, hash32, valid, n, base, nparts, cur,
-                              records);
+                           uint64_t* counts, uint64_t* records, uint64_t* scratch, hipStream_t s) {
+    // scratch: hist (u32 nparts x PART_BLOCKS), offs (u64 nparts x PART_BLOCKS), total (u64)
+    uint32_t* hist = reinterpret_cast<uint32_t*>(scratch);
+    uint64_t* offs = scratch + (size_t)nparts * PART_BLOCKS / 2 + 1;
+    auto* total = reinterpret_cast<unsigned long long*>(offs + (size_t)nparts * PART_BLOCKS);
+    hipLaunchKernelGGL(k_part_count, dim3(PART_BLOCKS), dim3(256), 0, s, hash32, valid, n, nparts, hist);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, hist, nparts, offs,
+                       reinterpret_cast<unsigned long long*>(counts), total);
+    hipLaunchKernelGGL(k_part_scatter, dim3(PART_BLOCKS), dim3(256), 0, s, hash32, valid, n, base, nparts, offs,
+                       records);
     return hipGetLastError();
+}
+
+size_t dedup_partition_scratch(int nparts) {
+    return ((size_t)nparts * PART_BLOCKS / 2 + 1 + (size_t)nparts * PART_BLOCKS + 1) * sizeof(uint64_t);
 }
 
 // scratch layout: keys[m], idx[m], keys2[m], idx2[m], heads[m], then rocprim temp storage

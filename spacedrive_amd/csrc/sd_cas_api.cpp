@@ -398,8 +398,26 @@ int32_t pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
 
 }  // namespace
 
+// ------------------------------------------------------------------ tuning knobs
+#include <atomic>
+static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{41}, {0}, {0}};
+int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
+
 // ============================================================================ C ABI
 extern "C" {
+
+int sd_cas_set_tuning(const char* key, int value) {
+    SD_GUARD_BEGIN
+    if (!key) throw sd_failure(SD_ERR_INVALID, "null key");
+    static const char* names[SD_TUNE_NKEYS] = {"sampled_variant", "whole_variant", "checksum_variant"};
+    for (int k = 0; k < SD_TUNE_NKEYS; k++)
+        if (strcmp(key, names[k]) == 0) {
+            g_tune[k].store(value, std::memory_order_relaxed);
+            return SD_OK;
+        }
+    throw sd_failure(SD_ERR_INVALID, std::string("unknown tuning key ") + key);
+    SD_GUARD_END
+}
 
 int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }
 
@@ -733,11 +751,13 @@ int sd_dedup_partition(sd_cas_ctx* ctx, const uint8_t* d_hash32, const uint8_t* 
         std::unique_ptr<Slot>* s;
         ~Rel() { c->release(std::move(*s)); }
     } rel{ctx, &slot};
-    slot->hashes.ensure((nparts + 1) * sizeof(uint64_t));
+    const size_t sb = sdk::dedup_partition_scratch(nparts);
+    slot->hashes.ensure(sb);
     slot->host_hashes.ensure(sizeof(uint64_t));
-    uint64_t* cursor = slot->hashes.as<uint64_t>();
-    HIP_CHECK(sdk::dedup_partition(d_hash32, d_valid, n, global_index_base, nparts, d_counts, d_records, cursor, s));
-    HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, cursor + nparts, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    uint64_t* scratch = slot->hashes.as<uint64_t>();
+    HIP_CHECK(sdk::dedup_partition(d_hash32, d_valid, n, global_index_base, nparts, d_counts, d_records, scratch, s));
+    HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, scratch + sb / sizeof(uint64_t) - 1, sizeof(uint64_t),
+                             hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     *n_valid = *reinterpret_cast<uint64_t*>(slot->host_hashes.p);
     return SD_OK;

@@ -22,6 +22,10 @@ struct ck_reduce_wg {
     uint32_t pad;
 };
 
+// process-wide tuning knobs (sd_cas_set_tuning); read at launch time
+enum sd_tune_key { SD_TUNE_SAMPLED_VARIANT = 0, SD_TUNE_WHOLE_VARIANT = 1, SD_TUNE_CK_VARIANT = 2, SD_TUNE_NKEYS = 3 };
+int tuning_get(int key);
+
 namespace sdk {
 hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const uint32_t* idx, uint32_t n,
                               uint32_t* out, hipStream_t s);
@@ -38,7 +42,9 @@ hipError_t launch_synth_fill(uint64_t cid, uint32_t twin, uint64_t len, uint8_t*
 hipError_t launch_valu_peak(uint32_t* sink, uint32_t iters, uint32_t grid, hipStream_t s);
 // dedup
 hipError_t dedup_partition(const uint8_t* hash32, const uint8_t* valid, uint64_t n, uint64_t base, int nparts,
-                           uint64_t* counts, uint64_t* records, uint64_t* cursor_scratch, hipStream_t s);
+                           uint64_t* counts, uint64_t* records, uint64_t* scratch, hipStream_t s);
+// device scratch bytes dedup_partition needs; the valid-record total is its last u64
+size_t dedup_partition_scratch(int nparts);
 hipError_t dedup_group(uint64_t* records, uint64_t m, uint64_t* rep, uint64_t* n_groups_dev, void* scratch,
                        size_t* scratch_bytes, hipStream_t s);
 }  // namespace sdk
