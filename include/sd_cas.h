@@ -186,6 +186,11 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * every value): "sampled_variant" = 10*U + prefetch with U in {1,2,4} chunks per lane
  * (default 41), "whole_variant", "checksum_variant" (default 0). */
 int sd_cas_set_tuning(const char* key, int value);
+/* Read-only probe over d_buf[0, bytes) (bytes a multiple of 4096) for calibrating the
+ * PMC byte counters on this kernel family's access patterns: pattern 0 = coalesced
+ * 16 B/lane streaming, pattern 1 = one lane per 1 KiB chunk reading 4 x 16 B per 64-byte
+ * block (the hashing kernels' pattern), pattern 2 = pattern 1 with 2 chunks per lane. */
+int sd_read_probe(sd_cas_ctx* ctx, const uint8_t* d_buf, uint64_t bytes, int pattern, void* stream);
 /* VALU integer-throughput microbenchmark: returns measured lane-ops/s (BLAKE3 ARX mix). */
 int sd_valu_peak(sd_cas_ctx* ctx, double* lane_ops_per_s);
 

@@ -11,10 +11,13 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
     > gpurun_out/prof_bench_$TAG.json 2> gpurun_out/prof_bench_$TAG.err
 rc=$?; echo "trace rc=$rc"; if fatal $rc; then exit $rc; fi
 [ "${PMC:-1}" = "1" ] || exit 0
-for C in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib_$TAG -o calib \
+    -- python3 scripts/pmc_calib.py > gpurun_out/calib_$TAG.log 2>&1
+rc=$?; echo "calib rc=$rc"; if fatal $rc; then exit $rc; fi
+for C in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE"; do
   N=$(echo $C | cut -d' ' -f1)
   timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_${TAG}_$N -o pmc \
-      -- python3 bench.py --steps 1 --warmup 0 --checksum-gib 8 --checksum-steps 1 --no-cpu-baseline \
+      -- python3 bench.py --steps 1 --warmup 0 --checksum-steps 1 --no-cpu-baseline \
       > gpurun_out/pmc_${TAG}_$N.json 2> gpurun_out/pmc_${TAG}_$N.err
   rc=$?; echo "pmc $N rc=$rc"; if fatal $rc; then exit $rc; fi
 done

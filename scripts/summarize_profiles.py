@@ -1,0 +1,92 @@
+"""gpurun_out/ rocprofv3 output -> committed summaries under profiles/.
+
+    python scripts/summarize_profiles.py TAG
+
+Writes profiles/TAG_kernel_stats.csv (rocprofv3 --stats, verbatim), profiles/TAG_summary.md
+(top kernels) and, if PMC passes exist, profiles/pmc_summary.json: per kernel and launch
+FETCH_SIZE / WRITE_SIZE (KB), the read-probe calibration factor, and
+hbm_bytes_per_launch = FETCH_SIZE * 1024 * factor + WRITE_SIZE * 1024.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PROF = os.path.join(ROOT, "profiles")
+CALIB_BYTES = 4 << 30
+
+
+def short(name):
+    n = name.replace("(anonymous namespace)::", "")
+    return n.split("(")[0].split("<")[0].strip()
+
+
+def pmc_rows(path):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return agg
+
+
+def main(tag):
+    os.makedirs(PROF, exist_ok=True)
+    stats = glob.glob(os.path.join(OUT, f"prof_{tag}", "*kernel_stats.csv"))
+    if stats:
+        dst = os.path.join(PROF, f"{tag}_kernel_stats.csv")
+        shutil.copy(stats[0], dst)
+        rows = sorted(csv.DictReader(open(stats[0])), key=lambda r: -float(r["TotalDurationNs"]))
+        with open(os.path.join(PROF, f"{tag}_summary.md"), "w") as f:
+            f.write(f"# rocprofv3 --kernel-trace --stats ({tag})\n\n")
+            f.write("Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py "
+                    "--steps 5 --warmup 1 --checksum-steps 2 --no-cpu-baseline` (scripts/profile.sh)\n\n")
+            f.write("| kernel | calls | avg µs | total ms | % |\n|---|---|---|---|---|\n")
+            for r in rows[:20]:
+                f.write(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
+                        f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.1f} |\n")
+        print("wrote", dst)
+    pmc = {}
+    for d in sorted(glob.glob(os.path.join(OUT, f"pmc_{tag}_*"))):
+        f = glob.glob(os.path.join(d, "*counter_collection.csv"))
+        if not f:
+            continue
+        for k, cs in pmc_rows(f[0]).items():
+            for c, v in cs.items():
+                pmc.setdefault(k, {})[c] = {"launches": len(v), "per_launch": sum(v) / len(v)}
+    if not pmc:
+        return
+    calib = {}
+    cf = glob.glob(os.path.join(OUT, f"calib_{tag}", "*counter_collection.csv"))
+    if cf:
+        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(cf[0]))
+                if short(r["Kernel_Name"]) == "k_read_probe" and r["Counter_Name"] == "FETCH_SIZE"]
+        for pattern, v in zip((0, 1, 2), vals):
+            calib[pattern] = CALIB_BYTES / (v * 1024)
+    # k_cas_sampled (U = 2) reads 2 KiB per lane: probe pattern 2; whole leaf: pattern 1;
+    # checksum leaf (4 KiB per lane, same 16 B x 4 per block shape): pattern 2
+    use = {"k_cas_sampled": 2, "k_whole_leaf": 1, "k_ck_leaf": 2}
+    kern = {}
+    for k, cs in pmc.items():
+        if "FETCH_SIZE" not in cs:
+            continue
+        fac = calib.get(use.get(k, 0), 2.0)
+        fetch = cs["FETCH_SIZE"]["per_launch"] * 1024
+        write = cs.get("WRITE_SIZE", {}).get("per_launch", 0.0) * 1024
+        kern[k] = {"FETCH_SIZE_KB": cs["FETCH_SIZE"]["per_launch"],
+                   "WRITE_SIZE_KB": cs.get("WRITE_SIZE", {}).get("per_launch"),
+                   "fetch_factor": fac, "hbm_bytes_per_launch": fetch * fac + write,
+                   "counters": {c: v["per_launch"] for c, v in cs.items()}}
+    out = {"tag": tag, "calibration_fetch_factor_by_pattern": calib,
+           "note": "hbm_bytes = FETCH_SIZE*1024*factor + WRITE_SIZE*1024; factor from read probes of a known "
+                   "4 GiB byte count (scripts/pmc_calib.py), 2.0 (MI355X_MICROARCH.md gfx950 rule) if absent",
+           "kernels": kern}
+    json.dump(out, open(os.path.join(PROF, "pmc_summary.json"), "w"), indent=1)
+    print("wrote profiles/pmc_summary.json")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r1")

@@ -400,7 +400,7 @@ int32_t pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
 
 // ------------------------------------------------------------------ tuning knobs
 #include <atomic>
-static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{41}, {0}, {0}};
+static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{21}, {0}, {0}};
 int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
 
 // ============================================================================ C ABI
@@ -857,6 +857,15 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
                            int iters, void* stream, float* ms_total) {
     return time_loop(ctx, stream, iters, ms_total,
                      [&](hipStream_t s) { run_checksum_batch(batch, d_data, d_hash32, s); });
+}
+
+int sd_read_probe(sd_cas_ctx* ctx, const uint8_t* d_buf, uint64_t bytes, int pattern, void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || !d_buf || bytes % 4096) throw sd_failure(SD_ERR_INVALID, "bad argument (bytes % 4096 != 0)");
+    ctx->bind();
+    HIP_CHECK(sdk::launch_read_probe(d_buf, bytes, pattern, ctx->pick(stream)));
+    return SD_OK;
+    SD_GUARD_END
 }
 
 int sd_valu_peak(sd_cas_ctx* ctx, double* lane_ops_per_s) {

@@ -108,9 +108,47 @@ __global__ __launch_bounds__(256) void k_valu_peak(uint32_t* sink, uint32_t iter
     if (r == 0x12345678u) sink[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 
+// Read probe: XOR-reduces the buffer so nothing is dead-code eliminated; writes one word
+// per workgroup only if the reduction hits a sentinel (never, in practice).
+__global__ __launch_bounds__(256) void k_read_probe(const uint8_t* __restrict__ buf, uint64_t bytes, int pattern,
+                                                    uint32_t* __restrict__ sink) {
+    const uint4* b = reinterpret_cast<const uint4*>(buf);
+    uint32_t acc = 0;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    if (pattern == 0) {
+        for (uint64_t i = tid; i < bytes / 16; i += nthreads) {
+            const uint4 v = b[i];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    } else {
+        const uint32_t per = pattern == 2 ? 2048u : 1024u;  // bytes per lane
+        for (uint64_t lane = tid; lane < bytes / per; lane += nthreads) {
+            const uint4* q = b + lane * (per / 16);
+            for (uint32_t blk = 0; blk < per / 64; blk++) {
+                for (int k = 0; k < 4; k++) {
+                    const uint4 v = q[blk * 4 + k];
+                    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+                }
+            }
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;
+}
+
 }  // namespace
 
 namespace sdk {
+
+hipError_t launch_read_probe(const uint8_t* buf, uint64_t bytes, int pattern, hipStream_t s) {
+    static uint32_t* sink = nullptr;
+    if (!sink) {
+        hipError_t e = hipMalloc(&sink, 4096 * sizeof(uint32_t));
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_read_probe, dim3(4096), dim3(256), 0, s, buf, bytes, pattern, sink);
+    return hipGetLastError();
+}
 
 hipError_t launch_synth_stage_cas(const uint64_t* sizes, const uint64_t* cids, const uint32_t* twins,
                                   const sd_extent* ext, uint32_t n, uint8_t* staged, hipStream_t s) {
