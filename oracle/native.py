@@ -40,6 +40,12 @@ def lib():
         L.sdo_checksums.argtypes = [P, P, P, U64, P, I]
         L.sdo_checksums_synth.argtypes = [P, P, P, U64, P, I]
         L.sdo_stage_synth.argtypes = [P, P, P, P, U64, P]
+        L.sdo_cas_ids_staged_simd.argtypes = [P, P, U64, P, I, I]
+        L.sdo_cas_ids_staged_simd.restype = I
+        L.sdo_checksums_simd.argtypes = [P, P, P, U64, P, I, I]
+        L.sdo_checksums_simd.restype = I
+        L.sdo_simd_level.argtypes = [I]
+        L.sdo_simd_level.restype = I
         _lib = L
     return _lib
 
@@ -76,9 +82,22 @@ def cas_ids_synth(sizes, cids, twins=None, nthreads: int = 1) -> np.ndarray:
     return out
 
 
-def cas_ids_staged(staged: np.ndarray, extents: np.ndarray, nthreads: int = 1) -> np.ndarray:
+def cas_ids_staged(staged: np.ndarray, extents: np.ndarray, nthreads: int = 1, simd: int = 0) -> np.ndarray:
+    """simd: 0 scalar (the checker), -1 best available SIMD, 1 AVX2, 2 AVX-512."""
     out = np.empty((len(extents), 8), np.uint8)
-    lib().sdo_cas_ids_staged(_p(staged), _p(extents), len(extents), _p(out), nthreads)
+    lib().sdo_cas_ids_staged_simd(_p(staged), _p(extents), len(extents), _p(out), nthreads, simd)
+    return out
+
+
+def simd_level(requested: int = -1) -> int:
+    return lib().sdo_simd_level(requested)
+
+
+def checksums_simd(data: np.ndarray, offsets, lens, nthreads: int = 1, simd: int = -1) -> np.ndarray:
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint64)
+    out = np.empty((len(offsets), 32), np.uint8)
+    lib().sdo_checksums_simd(_p(data), _p(offsets), _p(lens), len(offsets), _p(out), nthreads, simd)
     return out
 
 

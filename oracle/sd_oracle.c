@@ -67,6 +67,17 @@ static void b3_compress(const uint32_t cv[8], const uint8_t block[64], uint64_t 
     for (int i = 0; i < 8; i++) { out16[i] = s[i] ^ s[i + 8]; out16[i + 8] = s[i + 8] ^ cv[i]; }
 }
 
+/* word-level compression (little-endian message words), used by sd_oracle_simd.c */
+void sdo_compress_words(const uint32_t cv[8], const uint32_t m[16], uint64_t counter, uint32_t block_len,
+                        uint32_t flags, uint32_t out16[16]) {
+    uint8_t blk[64];
+    for (int i = 0; i < 16; i++) {
+        blk[4 * i] = (uint8_t)m[i]; blk[4 * i + 1] = (uint8_t)(m[i] >> 8);
+        blk[4 * i + 2] = (uint8_t)(m[i] >> 16); blk[4 * i + 3] = (uint8_t)(m[i] >> 24);
+    }
+    b3_compress(cv, blk, counter, block_len, flags, out16);
+}
+
 /* ------------------------------------------------------------- incremental hasher */
 typedef struct {
     uint32_t cv[8];
@@ -228,8 +239,12 @@ typedef struct {
     uint32_t msg_len, kind;
 } sdo_extent; /* same layout as sd_extent in include/sd_cas.h */
 
+void sdo_blake3_simd(const uint8_t* data, uint64_t len, uint8_t out[32], int lvl, uint8_t* scratch);
+int sdo_simd_level(int requested);
+
 typedef struct {
     int mode;
+    int simd; /* 0 = scalar incremental hasher; 1 = AVX2, 2 = AVX-512 multi-chunk */
     uint64_t n;
     const uint8_t* staged;
     const sdo_extent* ext;
@@ -249,11 +264,21 @@ static void* worker(void* arg) {
     uint8_t* scratch = NULL;
     if (j->mode == MODE_CAS_SYNTH) scratch = (uint8_t*)malloc(8 + MINIMUM_FILE_SIZE);
     if (j->mode == MODE_CHECKSUM_SYNTH) scratch = (uint8_t*)malloc(1u << 20);
+    uint8_t* cvs = NULL;
+    uint64_t cvs_cap = 0;
     for (;;) {
         uint64_t i = atomic_fetch_add(&j->cursor, 1);
         if (i >= j->n) break;
         uint8_t h[32];
-        if (j->mode == MODE_CAS_STAGED) {
+        if (j->mode == MODE_CAS_STAGED && j->simd) {
+            uint64_t need = 32 * ((j->ext[i].msg_len + 1023) / 1024 + 1);
+            if (need > cvs_cap) { free(cvs); cvs_cap = need * 2; cvs = (uint8_t*)malloc(cvs_cap); }
+            sdo_blake3_simd(j->staged + j->ext[i].msg_offset, j->ext[i].msg_len, h, j->simd, cvs);
+        } else if (j->mode == MODE_CHECKSUM && j->simd) {
+            uint64_t need = 32 * ((j->lens[i] + 1023) / 1024 + 1);
+            if (need > cvs_cap) { free(cvs); cvs_cap = need * 2; cvs = (uint8_t*)malloc(cvs_cap); }
+            sdo_blake3_simd(j->data + j->offsets[i], j->lens[i], h, j->simd, cvs);
+        } else if (j->mode == MODE_CAS_STAGED) {
             sdo_blake3(j->staged + j->ext[i].msg_offset, j->ext[i].msg_len, h);
         } else if (j->mode == MODE_CAS_SYNTH) {
             uint64_t m = sdo_synth_cas_message(j->cids[i], j->twins ? j->twins[i] : 0, j->sizes[i], scratch);
@@ -274,6 +299,7 @@ static void* worker(void* arg) {
         memcpy(j->out + (size_t)i * j->out_stride, h, j->out_stride);
     }
     free(scratch);
+    free(cvs);
     return NULL;
 }
 
@@ -287,11 +313,30 @@ static void run_job(job_t* j, int nthreads) {
     free(th);
 }
 
-/* cas ids (first 8 hash bytes) of staged messages */
-void sdo_cas_ids_staged(const uint8_t* staged, const sdo_extent* ext, uint64_t n, uint8_t* out8, int nthreads) {
+/* cas ids (first 8 hash bytes) of staged messages; simd: -1 best available, 0 scalar,
+ * 1 AVX2, 2 AVX-512 (capped at what the CPU has).  Returns the level used. */
+int sdo_cas_ids_staged_simd(const uint8_t* staged, const sdo_extent* ext, uint64_t n, uint8_t* out8, int nthreads,
+                            int simd) {
     job_t j = {0};
     j.mode = MODE_CAS_STAGED; j.n = n; j.staged = staged; j.ext = ext; j.out = out8; j.out_stride = 8;
+    j.simd = simd == 0 ? 0 : sdo_simd_level(simd);
     run_job(&j, nthreads);
+    return j.simd;
+}
+
+void sdo_cas_ids_staged(const uint8_t* staged, const sdo_extent* ext, uint64_t n, uint8_t* out8, int nthreads) {
+    sdo_cas_ids_staged_simd(staged, ext, n, out8, nthreads, 0);
+}
+
+/* full 32-byte hashes of byte ranges with the SIMD multi-chunk hasher */
+int sdo_checksums_simd(const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
+                       uint8_t* out32, int nthreads, int simd) {
+    job_t j = {0};
+    j.mode = MODE_CHECKSUM; j.n = n; j.data = data; j.offsets = offsets; j.lens = lens;
+    j.out = out32; j.out_stride = 32;
+    j.simd = simd == 0 ? 0 : sdo_simd_level(simd);
+    run_job(&j, nthreads);
+    return j.simd;
 }
 
 /* cas ids of synthetic files: builds each message from the generator, then hashes */

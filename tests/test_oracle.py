@@ -163,3 +163,15 @@ def test_synth_generator_c_vs_python(oracle_native, golden):
         tw = int(rng.integers(0, 3))
         assert oracle_native.synth_bytes(cid, tw, off, ln) == cs.synth_bytes(cid, tw, off, ln)
     assert oracle_native.synth_bytes(3, 5, 18430, 4) == cs.synth_bytes(3, 5, 18430, 4)
+
+
+@pytest.mark.parametrize("level", [1, 2])
+def test_c_oracle_simd_multichunk(oracle_native, level):
+    # the CPU-baseline hasher (hash_many over chunks and parents) vs the scalar oracle
+    if oracle_native.simd_level(level) != level:
+        pytest.skip("CPU lacks this SIMD level")
+    rng = np.random.default_rng(level)
+    for n in [0, 1, 64, 1023, 1024, 1025, 2049, 15 * 1024, 16 * 1024, 17 * 1024 + 3, 57352, 102408, 333333]:
+        d = rng.integers(0, 256, n + 64, dtype=np.uint8)
+        want = b3.blake3(d[:n].tobytes()) if n < 5000 else oracle_native.blake3(d[:n].tobytes())
+        assert oracle_native.checksums_simd(d, [0], [n], simd=level)[0].tobytes() == want, n
