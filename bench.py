@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--checksum-steps", type=int, default=5)
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target seconds per CPU-baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--serial", action="store_true", help="run the whole-file kernels after the sampled one")
+    p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (rehearsal)")
+    p.add_argument("--share-gpu", action="store_true", help="map every rank onto the visible GPUs (rehearsal)")
     return p.parse_args()
 
 
@@ -108,9 +111,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.share_gpu:  # rehearsal of the N-rank path on a box with fewer GPUs
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     import spacedrive_amd as sd
     from spacedrive_amd import dedup, synth
 
@@ -133,20 +141,30 @@ def main():
         f"{batch.msg_bytes / 1e9:.2f} GB of messages, {batch.compressions / 1e9:.3f} G compressions")
 
     stream = torch.cuda.current_stream()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    side = torch.cuda.Stream(device=dev)  # whole-file kernels run beside the sampled kernel
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    concurrent = not args.serial
 
     def step(k=None):
         if k is not None:
             ev[k][0].record(stream)
+        if concurrent:
+            side.wait_stream(stream)
+            batch.run_part(2, d_staged, d_hash, side)  # k_whole_leaf + k_whole_tree
         batch.run_part(1, d_staged, d_hash, stream)  # k_cas_sampled
         if k is not None:
             ev[k][1].record(stream)
-        batch.run_part(2, d_staged, d_hash, stream)  # k_whole_leaf + k_whole_tree
+        if concurrent:
+            if k is not None:
+                ev[k][3].record(side)
+            stream.wait_stream(side)
+        else:
+            batch.run_part(2, d_staged, d_hash, stream)
         if k is not None:
             ev[k][2].record(stream)
         r = dedup.dedup_shard(ctx, d_hash.view(n, 32), d_valid, n, start)
         if k is not None:
-            ev[k][3].record(stream)
+            ev[k][4].record(stream)
         return r
 
     for _ in range(args.warmup):
@@ -163,13 +181,25 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     samp_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
-    whole_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
-    dedup_ms = sum(ev[k][2].elapsed_time(ev[k][3]) for k in range(args.steps)) / args.steps
+    hash_ms = sum(ev[k][0].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
+    if concurrent:  # side stream: from the step's start to its last whole-file kernel
+        whole_ms = sum(ev[k][0].elapsed_time(ev[k][3]) for k in range(args.steps)) / args.steps
+    else:
+        whole_ms = hash_ms - samp_ms
+    dedup_ms = sum(ev[k][2].elapsed_time(ev[k][4]) for k in range(args.steps)) / args.steps
     recs, rep, n_groups = res
+    # every valid file lands on exactly one rank; groups never straddle ranks
+    tot = torch.tensor([recs.shape[0], n_groups, int((sizes != 0).sum())], dtype=torch.int64,
+                       device=dev if args.dist_backend == "nccl" else "cpu")
+    if world > 1:
+        dist.all_reduce(tot)
+    dedup_totals = {"records": int(tot[0]), "groups": int(tot[1]), "valid_files": int(tot[2]),
+                    "records_on_rank0": int(recs.shape[0])}
+    assert dedup_totals["records"] == dedup_totals["valid_files"], dedup_totals
     files_total = n_total * args.steps
     value = files_total / elapsed
 
@@ -198,11 +228,12 @@ def main():
                      "frac_of_measured_peak": samp_valu / valu_peak if valu_peak else None,
                      "hbm": {"achieved": samp_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                              "frac": samp_gbps / HBM_PEAK_GBPS}},
-        "kernels": {"k_cas_sampled_ms": samp_ms, "whole_file_ms": whole_ms,
+        "kernels": {"k_cas_sampled_ms": samp_ms, "whole_file_ms": whole_ms, "hash_ms": hash_ms,
+                    "whole_file_concurrent": concurrent,
                     "whole_file_GBps": whole_bytes / (whole_ms * 1e-3) / 1e9 if whole_ms > 0 else None,
                     "dedup_and_exchange_ms": dedup_ms,
-                    "host_overhead_ms": elapsed / args.steps * 1e3 - samp_ms - whole_ms - dedup_ms},
-        "dedup": {"records_on_rank0": int(recs.shape[0]), "groups_on_rank0": int(n_groups)},
+                    "host_overhead_ms": elapsed / args.steps * 1e3 - hash_ms - dedup_ms},
+        "dedup": dedup_totals,
     }
     del d_staged, recs, rep
     torch.cuda.empty_cache()
@@ -227,7 +258,7 @@ def main():
         torch.cuda.synchronize()
         ck_ms = e0.elapsed_time(e1) / args.checksum_steps
         gbps = cb.total_bytes / (ck_ms * 1e-3) / 1e9
-        tot = torch.tensor([gbps], dtype=torch.float64, device=dev)
+        tot = torch.tensor([gbps], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(tot)
         out["checksum"] = {"GBps": float(tot.item()), "unit": "GB/s", "per_gpu_GBps": gbps, "ms_per_run": ck_ms,

@@ -22,7 +22,7 @@ CALIB_BYTES = 4 << 30
 
 
 def short(name):
-    n = name.replace("(anonymous namespace)::", "")
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
     return n.split("(")[0].split("<")[0].strip()
 
 

@@ -45,6 +45,10 @@ def exchange(send_records: torch.Tensor, send_counts: torch.Tensor,
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world == 1:
         return send_records
+    if dist.get_backend(group) == "gloo" and send_records.is_cuda:
+        # CPU transport (tests / single-GPU rehearsal): same exchange, host tensors
+        dev = send_records.device
+        return exchange(send_records.cpu(), send_counts.cpu(), group).to(dev)
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts, group=group)
     rc = recv_counts.cpu().tolist()
@@ -80,7 +84,7 @@ def dedup_shard(ctx, d_hash32: torch.Tensor, d_valid: Optional[torch.Tensor], n_
 
 # ------------------------------------------------------------------ host reference
 def partition_host(keys: np.ndarray, idx: np.ndarray, nparts: int):
-    """Host mirror of sd_dedup_partition's grouping (order within a destination unspecified)."""
+    """Host mirror of sd_dedup_partition: stable, grouped by destination, input order within one."""
     d = dest_of(keys, nparts)
     order = np.argsort(d, kind="stable")
     counts = np.bincount(d, minlength=nparts).astype(np.int64)
