@@ -100,10 +100,13 @@ struct DevBuf {
     }
     template <class T>
     T* as() const { return reinterpret_cast<T*>(p); }
+    // grow-only (never frees a buffer that is large enough: hipFree synchronises the device)
     template <class T>
-    void upload(const std::vector<T>& v) {
-        alloc(v.size() * sizeof(T));
-        if (!v.empty()) HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    void upload(const std::vector<T>& v, hipStream_t s = nullptr) {
+        ensure(v.size() * sizeof(T));
+        if (v.empty()) return;
+        if (s) HIP_CHECK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+        else HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
     }
 };
 
@@ -166,6 +169,8 @@ struct sd_cas_batch {
     uint32_t total_chunks = 0;
     uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0;
     DevBuf ext, sidx, order, prefix, hint, cvbuf;
+    std::vector<sd_extent> h_ext;  // host copies backing async uploads
+    std::vector<uint32_t> h_sidx, h_order, h_prefix, h_hint;
 };
 
 struct ck_pass {
@@ -214,11 +219,16 @@ void validate_extent(const sd_extent& e, size_t i) {
         throw sd_failure(SD_ERR_INVALID, "extent " + std::to_string(i) + ": msg_offset not 16-byte aligned");
 }
 
-sd_cas_batch* build_cas_batch(const sd_extent* ext, size_t n) {
+// (Re)plans `b` for these extents, reusing its device buffers.  With a stream, the small
+// metadata uploads are async on it and read from b's host copies, which stay valid until
+// the next rebuild of `b` (the caller syncs the stream before that).
+void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t stream) {
     if (n >= (1ull << 31)) throw sd_failure(SD_ERR_INVALID, "batch too large");
-    auto b = std::make_unique<sd_cas_batch>();
     b->n = n;
-    std::vector<uint32_t> sidx;
+    b->n_sampled = b->n_whole = b->n_multi = 0;
+    b->compressions = b->msg_bytes = 0;
+    std::vector<uint32_t>& sidx = b->h_sidx;
+    sidx.clear();
     std::vector<uint32_t> count(SD_MINIMUM_FILE_SIZE + 9 + 1, 0);
     uint64_t end = 0;
     for (size_t i = 0; i < n; i++) {
@@ -239,10 +249,12 @@ sd_cas_batch* build_cas_batch(const sd_extent* ext, size_t n) {
     // counting sort of whole files by msg_len, descending (uniform lanes in both kernels)
     std::vector<uint32_t> start(count.size() + 1, 0);
     for (size_t L = count.size(); L-- > 0;) start[L] = start[L + 1] + count[L];
-    std::vector<uint32_t> order(b->n_whole);
+    std::vector<uint32_t>& order = b->h_order;
+    order.assign(b->n_whole, 0);
     for (size_t i = 0; i < n; i++)
         if (ext[i].kind == SD_KIND_WHOLE) order[start[ext[i].msg_len + 1]++] = (uint32_t)i;
-    std::vector<uint32_t> prefix(b->n_whole + 1, 0);
+    std::vector<uint32_t>& prefix = b->h_prefix;
+    prefix.assign(b->n_whole + 1, 0);
     uint64_t total = 0;
     for (uint32_t k = 0; k < b->n_whole; k++) {
         prefix[k] = (uint32_t)total;
@@ -254,7 +266,8 @@ sd_cas_batch* build_cas_batch(const sd_extent* ext, size_t n) {
     prefix[b->n_whole] = (uint32_t)total;
     b->total_chunks = (uint32_t)total;
     const uint32_t W = (b->total_chunks + 63) / 64;
-    std::vector<uint32_t> hint(W + 1, 0);
+    std::vector<uint32_t>& hint = b->h_hint;
+    hint.assign(W + 1, 0);
     {
         uint32_t k = 0;
         for (uint32_t w = 0; w <= W; w++) {
@@ -263,13 +276,18 @@ sd_cas_batch* build_cas_batch(const sd_extent* ext, size_t n) {
             hint[w] = k;
         }
     }
-    b->ext.alloc(n * sizeof(sd_extent));
-    if (n) HIP_CHECK(hipMemcpy(b->ext.p, ext, n * sizeof(sd_extent), hipMemcpyHostToDevice));
-    b->sidx.upload(sidx);
-    b->order.upload(order);
-    b->prefix.upload(prefix);
-    b->hint.upload(hint);
-    b->cvbuf.alloc((size_t)b->total_chunks * 32);
+    b->h_ext.assign(ext, ext + n);
+    b->ext.upload(b->h_ext, stream);
+    b->sidx.upload(sidx, stream);
+    b->order.upload(order, stream);
+    b->prefix.upload(prefix, stream);
+    b->hint.upload(hint, stream);
+    b->cvbuf.ensure((size_t)b->total_chunks * 32);
+}
+
+sd_cas_batch* build_cas_batch(const sd_extent* ext, size_t n) {
+    auto b = std::make_unique<sd_cas_batch>();
+    plan_cas_batch(b.get(), ext, n, nullptr);
     return b.release();
 }
 
@@ -587,19 +605,43 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
     live.reserve(n);
     for (size_t i = 0; i < n; i++)
         if (!status || status[i] == SD_FILE_OK) live.push_back(i);
-    auto slot = ctx->acquire();
+    // windows of files (index order) whose staged span fits WINDOW bytes; two slots
+    // alternate so window k+1's H2D copy overlaps window k's kernels
+    const uint64_t WINDOW = 512ull << 20;
+    struct Win {
+        size_t gi = 0, gj = 0;
+        bool busy = false;
+    };
+    std::unique_ptr<Slot> slots[2] = {ctx->acquire(), ctx->acquire()};
     struct Rel {
         sd_cas_ctx* c;
         std::unique_ptr<Slot>* s;
-        ~Rel() { c->release(std::move(*s)); }
-    } rel{ctx, &slot};
-    // groups of files whose staged span fits the device window, in index order
-    const uint64_t WINDOW = 4ull << 30;
+        ~Rel() {
+            for (int k = 0; k < 2; k++)
+                if (s[k]) {
+                    (void)hipStreamSynchronize(s[k]->stream);
+                    c->release(std::move(s[k]));
+                }
+        }
+    } rel{ctx, slots};
+    sd_cas_batch batches[2];
+    Win wins[2];
+    auto harvest = [&](int k) {
+        if (!wins[k].busy) return;
+        HIP_CHECK(hipStreamSynchronize(slots[k]->stream));
+        const uint8_t* h = reinterpret_cast<const uint8_t*>(slots[k]->host_hashes.p);
+        for (size_t q = wins[k].gi; q < wins[k].gj; q++) {
+            to_hex(h + (q - wins[k].gi) * 32, 8, out_hex17 + live[q] * 17);  // cas.rs:61 to_hex()[..16]
+            if (status) status[live[q]] = SD_FILE_OK;
+        }
+        wins[k].busy = false;
+    };
+    std::vector<sd_extent> ext;
     size_t gi = 0;
-    while (gi < live.size()) {
+    for (int w = 0; gi < live.size(); w ^= 1) {
+        harvest(w);  // frees slot w (its previous window is done)
         uint64_t lo = UINT64_MAX, hi = 0;
         size_t gj = gi;
-        std::vector<sd_extent> ext;
         while (gj < live.size()) {
             const sd_extent& e = extents[live[gj]];
             const uint64_t nlo = std::min(lo, e.msg_offset);
@@ -610,27 +652,25 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
             gj++;
         }
         if (hi > staged_bytes) throw sd_failure(SD_ERR_INVALID, "extent beyond staged_bytes");
-        for (size_t k = gi; k < gj; k++) {
-            sd_extent e = extents[live[k]];
+        ext.clear();
+        for (size_t q = gi; q < gj; q++) {
+            sd_extent e = extents[live[q]];
             e.msg_offset -= lo;
             ext.push_back(e);
         }
-        std::unique_ptr<sd_cas_batch> b(build_cas_batch(ext.data(), ext.size()));
-        slot->staged.ensure(hi - lo);
-        slot->hashes.ensure(ext.size() * 32);
-        slot->host_hashes.ensure(ext.size() * 32);
-        HIP_CHECK(hipMemcpyAsync(slot->staged.p, staged + lo, hi - lo, hipMemcpyHostToDevice, slot->stream));
-        run_cas_batch(b.get(), slot->staged.as<uint8_t>(), slot->hashes.as<uint8_t>(), slot->stream);
-        HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, slot->hashes.p, ext.size() * 32, hipMemcpyDeviceToHost,
-                                 slot->stream));
-        HIP_CHECK(hipStreamSynchronize(slot->stream));
-        const uint8_t* h = reinterpret_cast<const uint8_t*>(slot->host_hashes.p);
-        for (size_t k = gi; k < gj; k++) {
-            to_hex(h + (k - gi) * 32, 8, out_hex17 + live[k] * 17);  // cas.rs:61 to_hex()[..16]
-            if (status) status[live[k]] = SD_FILE_OK;
-        }
+        Slot& sl = *slots[w];
+        plan_cas_batch(&batches[w], ext.data(), ext.size(), sl.stream);
+        sl.staged.ensure(hi - lo);
+        sl.hashes.ensure(ext.size() * 32);
+        sl.host_hashes.ensure(ext.size() * 32);
+        HIP_CHECK(hipMemcpyAsync(sl.staged.p, staged + lo, hi - lo, hipMemcpyHostToDevice, sl.stream));
+        run_cas_batch(&batches[w], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
+        HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, ext.size() * 32, hipMemcpyDeviceToHost, sl.stream));
+        wins[w] = Win{gi, gj, true};
         gi = gj;
     }
+    harvest(0);
+    harvest(1);
     return SD_OK;
     SD_GUARD_END
 }

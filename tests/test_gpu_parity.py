@@ -97,6 +97,29 @@ def test_cas_pattern_goldens_host_staged(ctx, golden):
         assert out.raw[17 * i:17 * i + 16].decode() == cp[s], s
 
 
+def test_sd_cas_ids_pipelined_windows(ctx):
+    # the drop-in host entry point over several 512 MiB windows (two alternating streams),
+    # with entries pre-marked failed that must be skipped and left untouched
+    import ctypes
+    from spacedrive_amd._native import check, lib
+    n = 40000
+    sizes, cids, twins = synth.library(0, n, n, small_frac=0.3)
+    h, ext, staged = gpu_cas(ctx, sizes, cids, twins, return_staged=True)
+    assert ext["msg_offset"][-1] > (1 << 30)  # more than two windows
+    host = torch.from_numpy(staged).pin_memory()
+    status = np.zeros(n, np.int32)
+    status[::1001] = 2  # staging failed upstream
+    out = ctypes.create_string_buffer(b"#" * (17 * n), 17 * n)
+    check(lib().sd_cas_ids(ctx.handle, host.data_ptr(), len(staged), ext.ctypes.data, n, out,
+                           status.ctypes.data))
+    raw = out.raw
+    for i in range(n):
+        if i % 1001 == 0:
+            assert status[i] == 2 and raw[17 * i:17 * i + 16] == b"#" * 16
+        else:
+            assert status[i] == 0 and raw[17 * i:17 * i + 16].decode() == h[i, :8].tobytes().hex(), i
+
+
 def test_cas_exhaustive_small_sizes(ctx, oracle_native):
     # every message length across the first three chunks and the whole-file threshold
     sizes = np.concatenate([np.arange(0, 3200), np.arange(101000, 102500)]).astype(np.uint64)
