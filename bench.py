@@ -52,7 +52,8 @@ def parse():
     p.add_argument("--checksum-steps", type=int, default=5)
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target seconds per CPU-baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--serial", action="store_true", help="run the whole-file kernels after the sampled one")
+    p.add_argument("--whole-variant", type=int, default=0,
+                   help="0 = fused launch (default); 1 = separate sampled / whole-leaf / whole-tree kernels")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (rehearsal)")
     p.add_argument("--share-gpu", action="store_true", help="map every rank onto the visible GPUs (rehearsal)")
     p.add_argument("--host-staged-files", type=int, default=200_000, help="PCIe-inclusive sample size (N=1)")
@@ -172,30 +173,20 @@ def main():
         f"{batch.msg_bytes / 1e9:.2f} GB of messages, {batch.compressions / 1e9:.3f} G compressions")
 
     stream = torch.cuda.current_stream()
-    side = torch.cuda.Stream(device=dev)  # whole-file kernels run beside the sampled kernel
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
-    concurrent = not args.serial
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    from spacedrive_amd._native import lib
+    lib().sd_cas_set_tuning(b"whole_variant", args.whole_variant)
+    kname = "k_cas_mixed" if args.whole_variant == 0 else "k_cas_sampled+k_whole_leaf+k_whole_tree"
 
     def step(k=None):
         if k is not None:
             ev[k][0].record(stream)
-        if concurrent:
-            side.wait_stream(stream)
-            batch.run_part(2, d_staged, d_hash, side)  # k_whole_leaf + k_whole_tree
-        batch.run_part(1, d_staged, d_hash, stream)  # k_cas_sampled
+        batch.run(d_staged, d_hash, stream)  # one fused launch: sampled + whole-file groups
         if k is not None:
             ev[k][1].record(stream)
-        if concurrent:
-            if k is not None:
-                ev[k][3].record(side)
-            stream.wait_stream(side)
-        else:
-            batch.run_part(2, d_staged, d_hash, stream)
-        if k is not None:
-            ev[k][2].record(stream)
         r = dedup.dedup_shard(ctx, d_hash.view(n, 32), d_valid, n, start)
         if k is not None:
-            ev[k][4].record(stream)
+            ev[k][2].record(stream)
         return r
 
     for _ in range(args.warmup):
@@ -215,13 +206,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    samp_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
-    hash_ms = sum(ev[k][0].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
-    if concurrent:  # side stream: from the step's start to its last whole-file kernel
-        whole_ms = sum(ev[k][0].elapsed_time(ev[k][3]) for k in range(args.steps)) / args.steps
-    else:
-        whole_ms = hash_ms - samp_ms
-    dedup_ms = sum(ev[k][2].elapsed_time(ev[k][4]) for k in range(args.steps)) / args.steps
+    hash_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
+    dedup_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
     recs, rep, n_groups = res
     # every valid file lands on exactly one rank; groups never straddle ranks
     tot = torch.tensor([recs.shape[0], n_groups, int((sizes != 0).sum())], dtype=torch.int64,
@@ -234,14 +220,13 @@ def main():
     files_total = n_total * args.steps
     value = files_total / elapsed
 
-    # roofline of the dominant kernel (k_cas_sampled): algorithmic bytes = staged message
-    # bytes read + 32 B hash written per sampled file; VALU = 953 compressions x 672 ops
-    samp_bytes = batch.n_sampled * (SAMPLED_MSG + 32)
-    samp_gbps = samp_bytes / (samp_ms * 1e-3) / 1e9 if samp_ms > 0 else 0.0
+    # roofline of the hashing launch (k_cas_mixed: every file of the shard in one grid):
+    # VALU = all BLAKE3 compressions x 672 lane-ops; bytes = staged messages + 32 B out
+    hash_bytes = batch.msg_bytes + 32 * n
+    hash_gbps = hash_bytes / (hash_ms * 1e-3) / 1e9
     valu_peak = ctx.valu_peak()
-    samp_valu = batch.n_sampled * 953 * 672 / (samp_ms * 1e-3) if samp_ms > 0 else 0.0
-    whole_bytes = (batch.msg_bytes - batch.n_sampled * SAMPLED_MSG) + 32 * batch.n_whole
-    traffic = pmc_traffic("k_cas_sampled")
+    hash_valu = batch.compressions * 672 / (hash_ms * 1e-3)
+    traffic = pmc_traffic(kname)
 
     out = {
         "metric": "cas_id files/sec (10M synthetic files) + checksum GB/s at 1/2/4/8 MI355X",
@@ -252,18 +237,18 @@ def main():
                                f"10% dups, 1% sample twins), {n} files per GPU, step = hash shard + "
                                f"cas_id-prefix all-to-all dedup",
                    "files_per_gpu": n, "global_files": n_total, "parallelism": f"file-sharded x{world}"},
-        "roofline": {"bound": "valu", "achieved": samp_valu / 1e12, "peak": VALU_PEAK_TOPS,
-                     "unit": "T int32 VALU lane-ops/s", "frac": samp_valu / 1e12 / VALU_PEAK_TOPS,
-                     "traffic": traffic, "kernel": "k_cas_sampled", "kernel_ms": samp_ms,
+        "roofline": {"bound": "valu", "achieved": hash_valu / 1e12, "peak": VALU_PEAK_TOPS,
+                     "unit": "T int32 VALU lane-ops/s", "frac": hash_valu / 1e12 / VALU_PEAK_TOPS,
+                     "traffic": traffic, "kernel": kname, "kernel_ms": hash_ms,
+                     "algorithmic": {"compressions": batch.compressions, "lane_ops_per_compression": 672,
+                                     "bytes": hash_bytes},
                      "measured_valu_peak": valu_peak / 1e12,
-                     "frac_of_measured_peak": samp_valu / valu_peak if valu_peak else None,
-                     "hbm": {"achieved": samp_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                             "frac": samp_gbps / HBM_PEAK_GBPS}},
-        "kernels": {"k_cas_sampled_ms": samp_ms, "whole_file_ms": whole_ms, "hash_ms": hash_ms,
-                    "whole_file_concurrent": concurrent,
-                    "whole_file_GBps": whole_bytes / (whole_ms * 1e-3) / 1e9 if whole_ms > 0 else None,
-                    "dedup_and_exchange_ms": dedup_ms,
-                    "host_overhead_ms": elapsed / args.steps * 1e3 - hash_ms - dedup_ms},
+                     "frac_of_measured_peak": hash_valu / valu_peak if valu_peak else None,
+                     "hbm": {"achieved": hash_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                             "frac": hash_gbps / HBM_PEAK_GBPS}},
+        "kernels": {"hash_ms": hash_ms, "dedup_and_exchange_ms": dedup_ms,
+                    "host_overhead_ms": elapsed / args.steps * 1e3 - hash_ms - dedup_ms,
+                    "sampled_files": batch.n_sampled, "whole_files": batch.n_whole},
         "dedup": dedup_totals,
     }
     if rank == 0 and world == 1 and args.host_staged_files > 0:

@@ -74,19 +74,27 @@ __device__ void lds_reduce(uint32_t (*lds)[8], uint32_t n, bool root) {
 constexpr int S_FULL = 56;       // full chunks per sampled message (57344 bytes)
 constexpr int S_THREADS = 448;
 
+template <int U>
+struct sampled_lds {
+    static constexpr int LANES = S_FULL / U;     // lanes per file
+    static constexpr int F = S_THREADS / LANES;  // files per workgroup = 8U
+    static constexpr int N0 = LANES + 1;         // nodes per file entering the tree
+    uint32_t cvs[F][N0][8];
+};
+
+// one workgroup (blockIdx-independent: `wg` is its index among sampled workgroups)
 template <int U, bool PF>
-__global__ __launch_bounds__(S_THREADS) void k_cas_sampled(const uint8_t* __restrict__ staged,
-                                                           const sd_extent* __restrict__ ext,
-                                                           const uint32_t* __restrict__ idx,
-                                                           uint32_t n, uint32_t* __restrict__ out) {
-    constexpr int LANES = S_FULL / U;     // lanes per file
-    constexpr int F = S_THREADS / LANES;  // files per workgroup = 8U
-    constexpr int N0 = LANES + 1;         // nodes per file entering the tree
-    __shared__ __attribute__((aligned(16))) uint32_t cvs[F][N0][8];
+__device__ __forceinline__ void sampled_wg(uint32_t wg, const uint8_t* __restrict__ staged,
+                                           const sd_extent* __restrict__ ext, const uint32_t* __restrict__ idx,
+                                           uint32_t n, uint32_t* __restrict__ out, sampled_lds<U>& sh) {
+    constexpr int LANES = sampled_lds<U>::LANES;
+    constexpr int F = sampled_lds<U>::F;
+    constexpr int N0 = sampled_lds<U>::N0;
+    auto& cvs = sh.cvs;
     const uint32_t t = threadIdx.x;
     {
         const uint32_t f = t / LANES, j = t % LANES;
-        const uint32_t g = blockIdx.x * F + f;
+        const uint32_t g = wg * F + f;
         if (g < n) {
             const uint8_t* msg = staged + ext[idx[g]].msg_offset;
             uint32_t cv[8];
@@ -112,7 +120,7 @@ __global__ __launch_bounds__(S_THREADS) void k_cas_sampled(const uint8_t* __rest
             have = true;
         } else if (carry) {
             if (level == 0) {  // lanes [224, 224 + F): the tail chunk (8 bytes, chunk index 56)
-                const uint32_t gt = blockIdx.x * F + (t - F * P);
+                const uint32_t gt = wg * F + (t - F * P);
                 if (t < F * P + F && gt < n) {
                     ff = t - F * P; p = P;
                     const uint8_t* msg = staged + ext[idx[gt]].msg_offset;
@@ -133,9 +141,174 @@ __global__ __launch_bounds__(S_THREADS) void k_cas_sampled(const uint8_t* __rest
     }
     if (t < F * 8) {
         const uint32_t ff = t >> 3, w = t & 7;
-        const uint32_t gg = blockIdx.x * F + ff;
+        const uint32_t gg = wg * F + ff;
         if (gg < n) out[(size_t)idx[gg] * 8 + w] = cvs[ff][0][w];
     }
+}
+
+template <int U, bool PF>
+__global__ __launch_bounds__(S_THREADS) void k_cas_sampled(const uint8_t* __restrict__ staged,
+                                                           const sd_extent* __restrict__ ext,
+                                                           const uint32_t* __restrict__ idx,
+                                                           uint32_t n, uint32_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) sampled_lds<U> sh;
+    sampled_wg<U, PF>(blockIdx.x, staged, ext, idx, n, out, sh);
+}
+
+// ------------------------------------------------------------------ whole-file groups
+// Whole-file messages (cas.rs:27-29), sorted by length (descending) on the host and packed
+// into groups of consecutive files whose chunk PAIRS fit 448 lanes.  A lane hashes one
+// aligned pair of chunks (2j, 2j+1) and merges it in-lane; each file's pair CVs are then
+// merged level-wise in LDS.  Parents of a level are assigned compactly: a block scan of
+// the per-file parent counts, and a binary search from lane to file (files with parents
+// left are a prefix of the group, because nodes shrink monotonically with length).
+constexpr int W_THREADS = 448;
+
+struct whole_lds {
+    uint32_t cvs[W_THREADS][8];
+    uint32_t off[W_THREADS];    // first lane (= first pair node) of each local file
+    uint32_t pp[W_THREADS];     // parent prefix of the current level
+    uint32_t nodes[W_THREADS];  // node count of each local file at the current level
+    uint32_t file[W_THREADS];   // global file index of each local file
+    uint32_t wsum[8];
+    uint32_t active;            // local files that still have parents at this level
+};
+
+// exclusive prefix over the workgroup's threads (blockDim a multiple of 64, <= 512)
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (uint32_t k = 0; k < blockDim.x / 64; k++) {
+        if (k < w) before += wsum[k];
+        tot += wsum[k];
+    }
+    __syncthreads();
+    total = tot;
+    return before + x - v;
+}
+
+// largest f in [0, cnt) with pref[f] <= t (pref strictly increasing on [0, cnt))
+__device__ __forceinline__ uint32_t find_owner(const uint32_t* pref, uint32_t cnt, uint32_t t) {
+    uint32_t lo = 0, hi = cnt - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (pref[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void whole_wg(uint32_t g, const uint8_t* __restrict__ staged,
+                                         const sd_extent* __restrict__ ext, const uint32_t* __restrict__ order,
+                                         const uint2* __restrict__ groups, uint32_t* __restrict__ out,
+                                         whole_lds& sh) {
+    const uint2 grp = groups[g];  // (first index in the sorted order, file count)
+    const uint32_t cnt = grp.y, t = threadIdx.x;
+    uint32_t L = 0;
+    if (t < cnt) {
+        const uint32_t fl = order[grp.x + t];
+        const uint32_t C = (ext[fl].msg_len + CHUNK_LEN - 1) / CHUNK_LEN;  // msg_len >= 8
+        L = (C + 1) / 2;
+        sh.file[t] = fl;
+        sh.nodes[t] = L;
+    }
+    uint32_t lanes;
+    const uint32_t o = block_exscan(L, sh.wsum, lanes);
+    if (t < cnt) sh.off[t] = o;
+    __syncthreads();
+    if (t < lanes) {  // leaf: one aligned chunk pair
+        const uint32_t f = find_owner(sh.off, cnt, t);
+        const uint32_t fl = sh.file[f];
+        const sd_extent e = ext[fl];
+        const uint32_t C = (e.msg_len + CHUNK_LEN - 1) / CHUNK_LEN;
+        const uint32_t c0 = 2 * (t - sh.off[f]);
+        const uint8_t* p = staged + e.msg_offset + (size_t)c0 * CHUNK_LEN;
+        const uint32_t rem0 = e.msg_len - c0 * CHUNK_LEN;
+        uint32_t res[8];
+        chunk_cv(res, p, rem0 < CHUNK_LEN ? rem0 : CHUNK_LEN, c0, C == 1);
+        if (c0 + 1 < C) {
+            uint32_t cv1[8], cv0[8];
+            const uint32_t rem1 = rem0 - CHUNK_LEN;
+#pragma unroll
+            for (int i = 0; i < 8; i++) cv0[i] = res[i];
+            chunk_cv(cv1, p + CHUNK_LEN, rem1 < CHUNK_LEN ? rem1 : CHUNK_LEN, c0 + 1, false);
+            parent(res, cv0, cv1, C == 2 ? ROOT : 0u);
+        }
+        if (C <= 2) store_cv(out + (size_t)fl * 8, res);
+        else store_cv(sh.cvs[t], res);
+    }
+    __syncthreads();
+    uint32_t maxn = sh.nodes[0];  // local file 0 is the longest
+#pragma unroll 1
+    while (maxn > 1) {
+        uint32_t n = 0, P = 0;
+        if (t < cnt) {
+            n = sh.nodes[t];
+            P = n >= 2 ? n / 2 : 0;
+            if (P && (t + 1 == cnt || sh.nodes[t + 1] < 2)) sh.active = t + 1;
+        }
+        uint32_t tp;
+        const uint32_t pp = block_exscan(P, sh.wsum, tp);  // its barriers also publish sh.active
+        if (t < cnt) sh.pp[t] = pp;
+        __syncthreads();
+        uint32_t res[8], keep[8];
+        bool have = false, root = false, carry = false;
+        uint32_t dst = 0, cdst = 0, rfile = 0;
+        if (t < tp) {
+            const uint32_t f = find_owner(sh.pp, sh.active, t);
+            const uint32_t base = sh.off[f], nf = sh.nodes[f], q = t - sh.pp[f];
+            uint32_t l[8], r[8];
+            load_cv(l, sh.cvs[base + 2 * q]);
+            load_cv(r, sh.cvs[base + 2 * q + 1]);
+            root = nf == 2;
+            parent(res, l, r, root ? ROOT : 0u);
+            have = true;
+            dst = base + q;
+            rfile = sh.file[f];
+        }
+        if (t < cnt && n >= 3 && (n & 1u)) {  // the odd node is carried up unchanged
+            load_cv(keep, sh.cvs[sh.off[t] + n - 1]);
+            carry = true;
+            cdst = sh.off[t] + n / 2;
+        }
+        __syncthreads();
+        if (have) {
+            if (root) store_cv(out + (size_t)rfile * 8, res);
+            else store_cv(sh.cvs[dst], res);
+        }
+        if (carry) store_cv(sh.cvs[cdst], keep);
+        if (t < cnt) sh.nodes[t] = (n + 1) / 2;
+        __syncthreads();
+        maxn = sh.nodes[0];
+    }
+}
+
+// One launch for a whole cas batch: workgroups [0, S) hash sampled files (8U each),
+// workgroups [S, S + G) hash whole-file groups.  The long sampled workgroups are
+// dispatched first and the shorter whole-file ones fill the tail.
+template <int U, bool PF>
+union mixed_lds {
+    sampled_lds<U> s;
+    whole_lds w;
+};
+
+template <int U, bool PF>
+__global__ __launch_bounds__(S_THREADS) void k_cas_mixed(const uint8_t* __restrict__ staged,
+                                                         const sd_extent* __restrict__ ext,
+                                                         const uint32_t* __restrict__ sidx, uint32_t n_sampled,
+                                                         uint32_t S, const uint32_t* __restrict__ order,
+                                                         const uint2* __restrict__ groups,
+                                                         uint32_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) mixed_lds<U, PF> sh;
+    if (blockIdx.x < S) sampled_wg<U, PF>(blockIdx.x, staged, ext, sidx, n_sampled, out, sh.s);
+    else whole_wg(blockIdx.x - S, staged, ext, order, groups, out, sh.w);
 }
 
 // ------------------------------------------------------------------ whole-file cas
@@ -307,6 +480,29 @@ hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const
         default: SD_LAUNCH_SAMPLED(4, true); break;
     }
 #undef SD_LAUNCH_SAMPLED
+    return hipGetLastError();
+}
+
+hipError_t launch_cas_mixed(const uint8_t* staged, const sd_extent* ext, const uint32_t* sidx, uint32_t n_sampled,
+                            const uint32_t* order, const uint2* groups, uint32_t n_groups, uint32_t* out,
+                            hipStream_t s) {
+    const int v = tuning_get(SD_TUNE_SAMPLED_VARIANT);
+#define SD_LAUNCH_MIXED(U, PF)                                                                             \
+    do {                                                                                                  \
+        const uint32_t S = (n_sampled + 8 * U - 1) / (8 * U);                                             \
+        if (S + n_groups)                                                                                 \
+            hipLaunchKernelGGL((k_cas_mixed<U, PF>), dim3(S + n_groups), dim3(S_THREADS), 0, s, staged, ext, \
+                               sidx, n_sampled, S, order, groups, out);                                   \
+    } while (0)
+    switch (v) {
+        case 10: SD_LAUNCH_MIXED(1, false); break;
+        case 11: SD_LAUNCH_MIXED(1, true); break;
+        case 20: SD_LAUNCH_MIXED(2, false); break;
+        case 40: SD_LAUNCH_MIXED(4, false); break;
+        case 41: SD_LAUNCH_MIXED(4, true); break;
+        default: SD_LAUNCH_MIXED(2, true); break;
+    }
+#undef SD_LAUNCH_MIXED
     return hipGetLastError();
 }
 

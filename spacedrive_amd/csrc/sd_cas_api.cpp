@@ -168,9 +168,11 @@ struct sd_cas_batch {
     uint32_t n_sampled = 0, n_whole = 0, n_multi = 0;
     uint32_t total_chunks = 0;
     uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0;
-    DevBuf ext, sidx, order, prefix, hint, cvbuf;
+    uint32_t n_groups = 0;  // whole-file groups of the fused kernel
+    DevBuf ext, sidx, order, prefix, hint, cvbuf, groups;
     std::vector<sd_extent> h_ext;  // host copies backing async uploads
     std::vector<uint32_t> h_sidx, h_order, h_prefix, h_hint;
+    std::vector<uint2> h_groups;
 };
 
 struct ck_pass {
@@ -276,6 +278,24 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
             hint[w] = k;
         }
     }
+    // whole-file groups for the fused kernel: consecutive (length-sorted) files whose
+    // chunk pairs fit one 448-lane workgroup
+    b->h_groups.clear();
+    {
+        uint32_t first = 0, lanes = 0;
+        for (uint32_t k = 0; k < b->n_whole; k++) {
+            const uint32_t L = (msg_chunks(ext[order[k]].msg_len) + 1) / 2;
+            if (lanes + L > 448) {
+                b->h_groups.push_back(make_uint2(first, k - first));
+                first = k;
+                lanes = 0;
+            }
+            lanes += L;
+        }
+        if (b->n_whole) b->h_groups.push_back(make_uint2(first, b->n_whole - first));
+    }
+    b->n_groups = (uint32_t)b->h_groups.size();
+    b->groups.upload(b->h_groups, stream);
     b->h_ext.assign(ext, ext + n);
     b->ext.upload(b->h_ext, stream);
     b->sidx.upload(sidx, stream);
@@ -294,13 +314,20 @@ sd_cas_batch* build_cas_batch(const sd_extent* ext, size_t n) {
 void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_hash32, hipStream_t s,
                    int parts = SD_PART_SAMPLED | SD_PART_WHOLE) {
     uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
+    if (tuning_get(SD_TUNE_WHOLE_VARIANT) == 0) {  // one fused launch (default)
+        HIP_CHECK(sdk::launch_cas_mixed(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(),
+                                        (parts & SD_PART_SAMPLED) ? b->n_sampled : 0, b->order.as<uint32_t>(),
+                                        b->groups.as<uint2>(), (parts & SD_PART_WHOLE) ? b->n_groups : 0, out, s));
+        return;
+    }
+    // variant 1: separate sampled kernel, whole-file leaf kernel, whole-file tree kernel
     if (parts & SD_PART_SAMPLED)
         HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled, out,
                                           s));
     if (parts & SD_PART_WHOLE)
         HIP_CHECK(sdk::launch_whole(d_staged, b->ext.as<sd_extent>(), b->order.as<uint32_t>(), b->prefix.as<uint32_t>(),
-                                b->hint.as<uint32_t>(), b->n_whole, b->total_chunks, b->n_multi,
-                                b->cvbuf.as<uint32_t>(), out, s));
+                                    b->hint.as<uint32_t>(), b->n_whole, b->total_chunks, b->n_multi,
+                                    b->cvbuf.as<uint32_t>(), out, s));
 }
 
 // -------------------------------------------------------------- checksum planning

@@ -120,9 +120,18 @@ def test_sd_cas_ids_pipelined_windows(ctx):
             assert status[i] == 0 and raw[17 * i:17 * i + 16].decode() == h[i, :8].tobytes().hex(), i
 
 
-def test_cas_exhaustive_small_sizes(ctx, oracle_native):
+@pytest.fixture(params=[0, 1], ids=["fused", "split"])
+def whole_variant(request):
+    from spacedrive_amd._native import lib
+    assert lib().sd_cas_set_tuning(b"whole_variant", request.param) == 0
+    yield request.param
+    lib().sd_cas_set_tuning(b"whole_variant", 0)
+
+
+def test_cas_exhaustive_small_sizes(ctx, oracle_native, whole_variant):
     # every message length across the first three chunks and the whole-file threshold
-    sizes = np.concatenate([np.arange(0, 3200), np.arange(101000, 102500)]).astype(np.uint64)
+    sizes = np.concatenate([np.arange(0, 3200), np.arange(101000, 102500), np.arange(20000, 22000, 7)]).astype(np.uint64)
+    np.random.default_rng(whole_variant).shuffle(sizes)  # group packing must not depend on input order
     cids = np.arange(len(sizes), dtype=np.uint64) + 7
     twins = np.zeros(len(sizes), np.uint32)
     h, ext, staged = gpu_cas(ctx, sizes, cids, twins, return_staged=True)
@@ -131,7 +140,7 @@ def test_cas_exhaustive_small_sizes(ctx, oracle_native):
     assert len(mism) == 0, [(int(sizes[i])) for i in mism[:10]]
 
 
-def test_cas_mixture_full_hash_vs_oracle(ctx, oracle_native):
+def test_cas_mixture_full_hash_vs_oracle(ctx, oracle_native, whole_variant):
     # configs[0]-style mixture incl. dups, twins and every edge size; full 32-byte hashes
     n = 30000
     sizes, cids, twins = synth.library(0, n, n)
@@ -143,7 +152,7 @@ def test_cas_mixture_full_hash_vs_oracle(ctx, oracle_native):
     assert np.array_equal(h[:, :8], ids)
 
 
-def test_cas_configs0_full_size_and_idempotent(ctx, oracle_native):
+def test_cas_configs0_full_size_and_idempotent(ctx, oracle_native, whole_variant):
     # configs[0]: 100k mixed files -- full size, bit-exact vs the oracle, twice
     n = 100_000
     sizes, cids, twins = synth.library(0, n, n)
