@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", default="sampled", choices=["sampled", "whole", "checksum"])
+    ap.add_argument("--what", default="sampled", choices=["sampled", "whole", "library", "checksum"])
     ap.add_argument("--variants", default="10,11,20,21,40,41")
     ap.add_argument("--files", type=int, default=500_000)
     ap.add_argument("--rounds", type=int, default=5)
@@ -29,14 +29,18 @@ def main():
     from spacedrive_amd import synth
     from spacedrive_amd._native import lib
 
-    key = {"sampled": b"sampled_variant", "whole": b"whole_variant", "checksum": b"checksum_variant"}[args.what]
+    key = {"sampled": b"sampled_variant", "whole": b"whole_variant", "library": b"whole_variant",
+           "checksum": b"checksum_variant"}[args.what]
     variants = [int(v) for v in args.variants.split(",")]
     ctx = sd.Context(0)
     dev = torch.device("cuda", 0)
-    if args.what in ("sampled", "whole"):
+    if args.what in ("sampled", "whole", "library"):
         n = args.files
-        gen = synth.sampled_library if args.what == "sampled" else synth.small_library
-        sizes, cids, twins = gen(0, n)
+        if args.what == "library":
+            sizes, cids, twins = synth.library(0, n, n)
+        else:
+            gen = synth.sampled_library if args.what == "sampled" else synth.small_library
+            sizes, cids, twins = gen(0, n)
         ext, total = sd.stage_plan(sizes)
         data = torch.empty(total + 64, dtype=torch.uint8, device=dev)
         ctx.synth_stage_cas(torch.from_numpy(sizes.view(np.int64)).to(dev), torch.from_numpy(cids.view(np.int64)).to(dev),

@@ -314,13 +314,14 @@ sd_cas_batch* build_cas_batch(const sd_extent* ext, size_t n) {
 void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_hash32, hipStream_t s,
                    int parts = SD_PART_SAMPLED | SD_PART_WHOLE) {
     uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
-    if (tuning_get(SD_TUNE_WHOLE_VARIANT) == 0) {  // one fused launch (default)
+    if (tuning_get(SD_TUNE_WHOLE_VARIANT) == 0) {  // one fused launch
         HIP_CHECK(sdk::launch_cas_mixed(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(),
                                         (parts & SD_PART_SAMPLED) ? b->n_sampled : 0, b->order.as<uint32_t>(),
                                         b->groups.as<uint2>(), (parts & SD_PART_WHOLE) ? b->n_groups : 0, out, s));
         return;
     }
-    // variant 1: separate sampled kernel, whole-file leaf kernel, whole-file tree kernel
+    // variant 1 (default): separate sampled kernel, whole-file leaf kernel, whole-file tree
+    // kernel -- 1.5% faster than the fused launch in a same-process A/B
     if (parts & SD_PART_SAMPLED)
         HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled, out,
                                           s));
@@ -445,7 +446,7 @@ int32_t pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
 
 // ------------------------------------------------------------------ tuning knobs
 #include <atomic>
-static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{21}, {0}, {0}};
+static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{21}, {1}, {0}};
 int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
 
 // ============================================================================ C ABI
