@@ -56,7 +56,8 @@ def parse():
                    help="0 = fused launch; 1 = separate sampled / whole-leaf / whole-tree kernels (default)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (rehearsal)")
     p.add_argument("--share-gpu", action="store_true", help="map every rank onto the visible GPUs (rehearsal)")
-    p.add_argument("--host-staged-files", type=int, default=200_000, help="PCIe-inclusive sample size (N=1)")
+    p.add_argument("--host-staged-files", type=int, default=0,
+                   help="N=1 only: also time the PCIe-inclusive drop-in path on this many files (DESIGN.md)")
     return p.parse_args()
 
 
