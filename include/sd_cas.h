@@ -100,6 +100,10 @@ int sd_cas_stage_plan(const uint64_t* sizes, size_t n, sd_extent* extents_out,
  * file or head/samples/tail via pread), zero-padding to SD_STAGE_ALIGN.  Sets *status
  * to an sd_file_status; returns SD_OK unless arguments are invalid. */
 int sd_cas_stage_file(const char* path, const sd_extent* ext, uint8_t* staged, int32_t* status);
+/* The same for n files on nthreads threads (the reference does these reads one tokio
+ * blocking-pool hop at a time: cas.rs:29-58).  status[n] receives each file's outcome. */
+int sd_cas_stage_files(const char* const* paths, const sd_extent* extents, size_t n, uint8_t* staged,
+                       int32_t* status, int nthreads);
 
 /* ---------------------------------------------------------------- cas ids */
 /* Drop-in batch: staged messages in host memory (pinned or pageable) -> n cas_ids as
@@ -138,8 +142,10 @@ int sd_checksum_batch_run(sd_cas_ctx* ctx, const sd_checksum_batch* batch, const
                           uint8_t* d_hash32, void* stream);
 /* [0] files, [1] total bytes, [2] BLAKE3 compressions, [3] 1 MiB leaf blocks */
 int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
-/* Drop-in: checksums of files on disk (path list, NUL-separated, n paths) streamed
- * through pinned windows -> 65-byte lowercase hex (hash.rs:21-23).  status required. */
+/* Drop-in: checksums of n files on disk -> 65-byte lowercase hex each (hash.rs:21-23);
+ * status[n] required.  Files up to 256 MiB are packed many per pinned window, larger
+ * ones are streamed window by window; two windows alternate so host reads overlap the
+ * H2D copies and the kernels.  The length hashed is the file's length at stat time. */
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65,
                       int32_t* status);
 
@@ -156,8 +162,12 @@ int sd_dedup_partition(sd_cas_ctx* ctx, const uint8_t* d_hash32, const uint8_t* 
 /* Group received records by cas_id: sorts d_records[m] (in place) by (cas_id, index) and
  * writes d_rep[m] (u64): for each record, the smallest global index with an equal
  * cas_id -- the Object-link candidate (file_identifier/mod.rs:168-225 semantics up to
- * the chunk-of-100 rule).  Returns the number of groups. */
-int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, uint64_t* d_rep,
+ * the chunk-of-100 rule).  Returns the number of groups.
+ * flags: SD_DEDUP_INDEX_SORTED promises the records are already in ascending index
+ * order -- true for sd_dedup_partition's output after an all-to-all in rank order over
+ * contiguous index shards -- and saves one radix sort. */
+#define SD_DEDUP_INDEX_SORTED 1
+int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, int flags, uint64_t* d_rep,
                    uint64_t* n_groups, void* stream);
 
 /* ---------------------------------------------------------------- synthetic data */

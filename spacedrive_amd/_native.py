@@ -58,6 +58,7 @@ SIGNATURES = [
     ("sd_cas_host_free", None, [P, P]),
     ("sd_cas_stage_plan", I32, [P, SZ, P, PU64]),
     ("sd_cas_stage_file", I32, [ctypes.c_char_p, P, P, ctypes.POINTER(ctypes.c_int32)]),
+    ("sd_cas_stage_files", I32, [P, P, SZ, P, P, I32]),
     ("sd_cas_ids", I32, [P, P, U64, P, SZ, P, P]),
     ("sd_cas_batch_create", I32, [P, P, SZ, ctypes.POINTER(P)]),
     ("sd_cas_batch_destroy", None, [P]),
@@ -70,7 +71,7 @@ SIGNATURES = [
     ("sd_checksum_batch_stats", I32, [P, P]),
     ("sd_file_checksums", I32, [P, P, SZ, P, P]),
     ("sd_dedup_partition", I32, [P, P, P, U64, U64, I32, P, P, PU64, P]),
-    ("sd_dedup_group", I32, [P, P, U64, P, PU64, P]),
+    ("sd_dedup_group", I32, [P, P, U64, I32, P, PU64, P]),
     ("sd_synth_stage_cas", I32, [P, P, P, P, P, SZ, P, P]),
     ("sd_synth_fill", I32, [P, U64, U32, U64, P, P]),
     ("sd_device_malloc", I32, [P, U64, ctypes.POINTER(P)]),

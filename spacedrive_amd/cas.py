@@ -79,11 +79,10 @@ def generate_cas_ids(paths: Sequence[Union[str, os.PathLike]], sizes: Sequence[i
     try:
         status = np.zeros(n, np.int32)
         L = lib()
-        for i, p in enumerate(paths):  # pread of header/samples/tail or the whole file
-            st = ctypes.c_int32(0)
-            check(L.sd_cas_stage_file(os.fsencode(p), ctypes.c_void_p(ext.ctypes.data + 24 * i),
-                                      staged.ptr, ctypes.byref(st)))
-            status[i] = st.value
+        enc = [os.fsencode(p) for p in paths]
+        arr = (ctypes.c_char_p * n)(*enc)
+        # pread of header/samples/tail (or the whole file) on a thread pool
+        check(L.sd_cas_stage_files(arr, _ptr(ext), n, staged.ptr, _ptr(status), min(16, os.cpu_count() or 1)))
         out = ctypes.create_string_buffer(17 * n)
         check(L.sd_cas_ids(ctx.handle, staged.ptr, total, _ptr(ext), n, out, _ptr(status)))
     finally:

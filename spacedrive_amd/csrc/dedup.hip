@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <utility>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -219,8 +220,8 @@ size_t dedup_partition_scratch(int nparts) {
 }
 
 // scratch layout: keys[m], idx[m], keys2[m], idx2[m], heads[m], then rocprim temp storage
-hipError_t dedup_group(uint64_t* records, uint64_t m, uint64_t* rep, uint64_t* n_groups_dev, void* scratch,
-                       size_t* scratch_bytes, hipStream_t s) {
+hipError_t dedup_group(uint64_t* records, uint64_t m, int flags, uint64_t* rep, uint64_t* n_groups_dev,
+                       void* scratch, size_t* scratch_bytes, hipStream_t s) {
     size_t sort_bytes = 0, scan_bytes = 0;
     uint64_t* nul = nullptr;
     hipError_t e = rocprim::radix_sort_pairs(nullptr, sort_bytes, nul, nul, nul, nul, (size_t)m, 0, 64, s);
@@ -242,18 +243,23 @@ hipError_t dedup_group(uint64_t* records, uint64_t m, uint64_t* rep, uint64_t* n
     e = hipMemsetAsync(n_groups_dev, 0, sizeof(uint64_t), s);
     if (e != hipSuccess || m == 0) return e;
     hipLaunchKernelGGL(k_split, dim3(grid_for(m)), dim3(256), 0, s, records, m, keys, idx);
-    // sort by index, then stable by cas_id: equal cas_ids end up in ascending index order
     size_t tb = temp;
-    e = rocprim::radix_sort_pairs(tmp, tb, idx, idx2, keys, keys2, (size_t)m, 0, 64, s);
+    if (!(flags & SD_DEDUP_INDEX_SORTED)) {
+        // sort by index first, so the stable cas_id sort below leaves equal cas_ids in
+        // ascending index order
+        e = rocprim::radix_sort_pairs(tmp, tb, idx, idx2, keys, keys2, (size_t)m, 0, 64, s);
+        if (e != hipSuccess) return e;
+        std::swap(keys, keys2);
+        std::swap(idx, idx2);
+        tb = temp;
+    }
+    e = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, idx, idx2, (size_t)m, 0, 64, s);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_heads, dim3(grid_for(m)), dim3(256), 0, s, keys2, m, heads, n_groups_dev);
     tb = temp;
-    e = rocprim::radix_sort_pairs(tmp, tb, keys2, keys, idx2, idx, (size_t)m, 0, 64, s);
+    e = rocprim::inclusive_scan(tmp, tb, heads, keys, (size_t)m, rocprim::maximum<uint64_t>(), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_heads, dim3(grid_for(m)), dim3(256), 0, s, keys, m, heads, n_groups_dev);
-    tb = temp;
-    e = rocprim::inclusive_scan(tmp, tb, heads, keys2, (size_t)m, rocprim::maximum<uint64_t>(), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_join, dim3(grid_for(m)), dim3(256), 0, s, keys, idx, keys2, m, records, rep);
+    hipLaunchKernelGGL(k_join, dim3(grid_for(m)), dim3(256), 0, s, keys2, idx2, keys, m, records, rep);
     return hipGetLastError();
 }
 

@@ -24,6 +24,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sd_internal.h"
@@ -177,6 +178,7 @@ struct sd_cas_batch {
 
 struct ck_pass {
     DevBuf wgs;
+    std::vector<ck_reduce_wg> h_wgs;  // host copy backing the async upload
     uint32_t n_wg = 0;
     int src = 0, dst = 1;  // which CV level buffer
 };
@@ -188,7 +190,8 @@ struct sd_checksum_batch {
     std::vector<uint2> wg_map_h;
     DevBuf files, wg_map;
     DevBuf lvl[2];
-    std::vector<std::unique_ptr<ck_pass>> passes;
+    std::vector<std::unique_ptr<ck_pass>> passes;  // capacity reused across replans
+    size_t n_passes = 0;
 };
 
 namespace {
@@ -334,37 +337,41 @@ void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_ha
 // -------------------------------------------------------------- checksum planning
 constexpr uint64_t CK_BLOCK_BYTES = 1024ull * 1024ull;  // 1024 chunks per leaf workgroup
 
-sd_checksum_batch* build_checksum_batch(const uint64_t* offsets, const uint64_t* lens, size_t n) {
+// (Re)plans `b` for these byte ranges reusing its device buffers (grow-only; see
+// plan_cas_batch for the stream / host-copy lifetime rule).
+void plan_checksum_batch(sd_checksum_batch* b, const uint64_t* offsets, const uint64_t* lens, size_t n,
+                         hipStream_t stream) {
     if (n >= (1ull << 31)) throw sd_failure(SD_ERR_INVALID, "batch too large");
-    auto b = std::make_unique<sd_checksum_batch>();
     b->n = n;
+    b->total_bytes = b->compressions = b->blocks = 0;
     b->files_h.resize(n);
-    std::vector<uint64_t> level_n;  // current level size per file
-    level_n.resize(n);
+    b->wg_map_h.clear();
+    std::vector<uint64_t> level_n(n);  // current level size per file
     uint64_t cv0 = 0;
     for (size_t i = 0; i < n; i++) {
         if (offsets[i] % 16) throw sd_failure(SD_ERR_INVALID, "checksum range " + std::to_string(i) + " not 16-byte aligned");
         const uint64_t nb = lens[i] == 0 ? 1 : (lens[i] + CK_BLOCK_BYTES - 1) / CK_BLOCK_BYTES;
+        if (nb >= (1ull << 32)) throw sd_failure(SD_ERR_INVALID, "file too large");
         b->files_h[i] = ck_file{offsets[i], lens[i], nb > 1 ? cv0 : 0};
-        for (uint64_t k = 0; k < nb; k++) {
-            if (k >= (1ull << 32)) throw sd_failure(SD_ERR_INVALID, "file too large");
-            b->wg_map_h.push_back(make_uint2((uint32_t)i, (uint32_t)k));
-        }
+        for (uint64_t k = 0; k < nb; k++) b->wg_map_h.push_back(make_uint2((uint32_t)i, (uint32_t)k));
         if (nb > 1) cv0 += nb;
         level_n[i] = nb;
         b->total_bytes += lens[i];
         b->compressions += file_compressions(lens[i]);
         b->blocks += nb;
     }
-    b->files.upload(b->files_h);
-    b->wg_map.upload(b->wg_map_h);
+    b->files.upload(b->files_h, stream);
+    b->wg_map.upload(b->wg_map_h, stream);
     // reduce passes: groups of 256 CVs per workgroup until every file has its root
     std::vector<uint64_t> base(n, 0);
     for (size_t i = 0; i < n; i++) base[i] = b->files_h[i].cv_base;
     size_t lvl_cap[2] = {cv0, 0};
     int src = 0;
+    b->n_passes = 0;
     for (;;) {
-        std::vector<ck_reduce_wg> wgs;
+        if (b->n_passes == b->passes.size()) b->passes.push_back(std::make_unique<ck_pass>());
+        ck_pass& p = *b->passes[b->n_passes];
+        p.h_wgs.clear();
         uint64_t dst_total = 0;
         std::vector<uint64_t> nbase(n, 0);
         for (size_t i = 0; i < n; i++) {
@@ -379,24 +386,28 @@ sd_checksum_batch* build_checksum_batch(const uint64_t* offsets, const uint64_t*
                 w.count = (uint32_t)std::min<uint64_t>(256, cnt - g * 256);
                 w.file = (uint32_t)i;
                 w.is_root = groups == 1;
-                wgs.push_back(w);
+                p.h_wgs.push_back(w);
             }
             dst_total += groups == 1 ? 0 : groups;
             level_n[i] = groups == 1 ? 1 : groups;
         }
-        if (wgs.empty()) break;
-        auto p = std::make_unique<ck_pass>();
-        p->wgs.upload(wgs);
-        p->n_wg = (uint32_t)wgs.size();
-        p->src = src;
-        p->dst = 1 - src;
+        if (p.h_wgs.empty()) break;
+        p.wgs.upload(p.h_wgs, stream);
+        p.n_wg = (uint32_t)p.h_wgs.size();
+        p.src = src;
+        p.dst = 1 - src;
         lvl_cap[1 - src] = std::max<size_t>(lvl_cap[1 - src], dst_total);
-        b->passes.push_back(std::move(p));
+        b->n_passes++;
         base = nbase;
         src = 1 - src;
     }
-    b->lvl[0].alloc(lvl_cap[0] * 32);
-    b->lvl[1].alloc(lvl_cap[1] * 32);
+    b->lvl[0].ensure(lvl_cap[0] * 32);
+    b->lvl[1].ensure(lvl_cap[1] * 32);
+}
+
+sd_checksum_batch* build_checksum_batch(const uint64_t* offsets, const uint64_t* lens, size_t n) {
+    auto b = std::make_unique<sd_checksum_batch>();
+    plan_checksum_batch(b.get(), offsets, lens, n, nullptr);
     return b.release();
 }
 
@@ -404,9 +415,11 @@ void run_checksum_leaf(const sd_checksum_batch* b, const uint8_t* d_data, uint64
                        uint32_t* out, hipStream_t s);
 
 void run_checksum_reduce(const sd_checksum_batch* b, uint32_t* out, hipStream_t s) {
-    for (const auto& p : b->passes)
-        HIP_CHECK(sdk::launch_ck_reduce(b->lvl[p->src].as<uint32_t>(), b->lvl[p->dst].as<uint32_t>(),
-                                        p->wgs.as<ck_reduce_wg>(), p->n_wg, out, s));
+    for (size_t k = 0; k < b->n_passes; k++) {
+        const ck_pass& p = *b->passes[k];
+        HIP_CHECK(sdk::launch_ck_reduce(b->lvl[p.src].as<uint32_t>(), b->lvl[p.dst].as<uint32_t>(),
+                                        p.wgs.as<ck_reduce_wg>(), p.n_wg, out, s));
+    }
 }
 
 void run_checksum_batch(const sd_checksum_batch* b, const uint8_t* d_data, uint8_t* d_hash32, hipStream_t s) {
@@ -440,6 +453,42 @@ int32_t pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
         off += (uint64_t)r;
     }
     return SD_FILE_OK;
+}
+
+// Reads one file into its extent exactly as generate_cas_id does (cas.rs:25-58) and
+// zero-pads the message to SD_STAGE_ALIGN.  Returns an sd_file_status.
+int32_t stage_one(const char* path, const sd_extent& e, uint8_t* staged) {
+    uint8_t* dst = staged + e.msg_offset;
+    const uint64_t size = e.size;
+    for (int i = 0; i < 8; i++) dst[i] = (uint8_t)(size >> (8 * i));  // cas.rs:25 le64
+    const uint64_t padded = align_up(e.msg_len, SD_STAGE_ALIGN);
+    memset(dst + e.msg_len, 0, padded - e.msg_len);
+    const int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return io_status(errno);
+    int32_t st = SD_FILE_OK;
+    if (e.kind == SD_KIND_WHOLE) {  // cas.rs:29 fs::read -- requires len == size
+        st = pread_exact(fd, dst + 8, size, 0);
+        if (st == SD_FILE_OK) {
+            uint8_t extra;
+            if (pread(fd, &extra, 1, (off_t)size) == 1) st = SD_FILE_SHORT_READ;  // file grew since stat
+        }
+    } else {  // cas.rs:31-58: header, 4 samples at 8192 + k*seek_jump, footer
+        const uint64_t H = SD_HEADER_OR_FOOTER_SIZE, S = SD_SAMPLE_SIZE;
+        const uint64_t jump = (size - 2 * H) / SD_SAMPLE_COUNT;
+        uint8_t* p = dst + 8;
+        st = pread_exact(fd, p, H, 0);
+        p += H;
+        uint64_t current_pos = H;
+        while (st == SD_FILE_OK) {
+            st = pread_exact(fd, p, S, current_pos);
+            p += S;
+            if (current_pos >= H + jump * (SD_SAMPLE_COUNT - 1)) break;
+            current_pos += jump;
+        }
+        if (st == SD_FILE_OK) st = pread_exact(fd, p, H, size - H);
+    }
+    close(fd);
+    return st;
 }
 
 }  // namespace
@@ -540,40 +589,30 @@ int sd_cas_stage_file(const char* path, const sd_extent* ext, uint8_t* staged, i
     SD_GUARD_BEGIN
     if (!path || !ext || !staged || !status) throw sd_failure(SD_ERR_INVALID, "null argument");
     validate_extent(*ext, 0);
-    uint8_t* dst = staged + ext->msg_offset;
-    const uint64_t size = ext->size;
-    for (int i = 0; i < 8; i++) dst[i] = (uint8_t)(size >> (8 * i));  // cas.rs:25
-    const uint64_t padded = align_up(ext->msg_len, SD_STAGE_ALIGN);
-    memset(dst + ext->msg_len, 0, padded - ext->msg_len);
-    const int fd = open(path, O_RDONLY | O_CLOEXEC);
-    if (fd < 0) {
-        *status = io_status(errno);
-        return SD_OK;
-    }
-    int32_t st = SD_FILE_OK;
-    if (ext->kind == SD_KIND_WHOLE) {  // cas.rs:29 fs::read -- requires len == size
-        st = pread_exact(fd, dst + 8, size, 0);
-        if (st == SD_FILE_OK) {
-            uint8_t extra;
-            if (pread(fd, &extra, 1, (off_t)size) == 1) st = SD_FILE_SHORT_READ;  // file grew since stat
+    *status = stage_one(path, *ext, staged);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cas_stage_files(const char* const* paths, const sd_extent* extents, size_t n, uint8_t* staged,
+                       int32_t* status, int nthreads) {
+    SD_GUARD_BEGIN
+    if (n && (!paths || !extents || !staged || !status)) throw sd_failure(SD_ERR_INVALID, "null argument");
+    for (size_t i = 0; i < n; i++) validate_extent(extents[i], i);
+    if (nthreads < 1) nthreads = 1;
+    if ((size_t)nthreads > n) nthreads = n ? (int)n : 1;
+    std::atomic<size_t> cursor{0};
+    auto work = [&]() {
+        for (;;) {
+            const size_t i = cursor.fetch_add(1, std::memory_order_relaxed);
+            if (i >= n) break;
+            status[i] = stage_one(paths[i], extents[i], staged);
         }
-    } else {  // cas.rs:31-58: header, 4 samples at 8192 + k*seek_jump, footer
-        const uint64_t H = SD_HEADER_OR_FOOTER_SIZE, S = SD_SAMPLE_SIZE;
-        const uint64_t jump = (size - 2 * H) / SD_SAMPLE_COUNT;
-        uint8_t* p = dst + 8;
-        st = pread_exact(fd, p, H, 0);
-        p += H;
-        uint64_t current_pos = H;
-        while (st == SD_FILE_OK) {
-            st = pread_exact(fd, p, S, current_pos);
-            p += S;
-            if (current_pos >= H + jump * (SD_SAMPLE_COUNT - 1)) break;
-            current_pos += jump;
-        }
-        if (st == SD_FILE_OK) st = pread_exact(fd, p, H, size - H);
-    }
-    close(fd);
-    *status = st;
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nthreads; t++) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
     return SD_OK;
     SD_GUARD_END
 }
@@ -743,62 +782,147 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
     SD_GUARD_BEGIN
     if (!ctx || (n && (!paths || !out_hex65 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
     ctx->bind();
-    auto slot = ctx->acquire();
+    // Two slots, each with a pinned window, a device window and a stream.  Files that fit
+    // a window are packed (64-B aligned) into one batch per window; larger files stream
+    // window by window into their own batch's leaf CVs, then reduce.  While the GPU hashes
+    // one slot's window, the host reads the next window into the other slot.
+    const uint64_t W = 256ull << 20;  // a multiple of the 1 MiB leaf block
+    std::unique_ptr<Slot> slots[2] = {ctx->acquire(), ctx->acquire()};
     struct Rel {
         sd_cas_ctx* c;
         std::unique_ptr<Slot>* s;
-        ~Rel() { c->release(std::move(*s)); }
-    } rel{ctx, &slot};
-    const uint64_t W = 256ull << 20;  // pinned window; a multiple of the 1 MiB leaf block
-    slot->window.ensure(W + 64);
-    slot->staged.ensure(W + 64);
-    slot->hashes.ensure(32);
-    slot->host_hashes.ensure(32);
-    uint8_t* win = reinterpret_cast<uint8_t*>(slot->window.p);
+        ~Rel() {
+            for (int k = 0; k < 2; k++)
+                if (s[k]) {
+                    (void)hipStreamSynchronize(s[k]->stream);
+                    c->release(std::move(s[k]));
+                }
+        }
+    } rel{ctx, slots};
+    for (int k = 0; k < 2; k++) {
+        slots[k]->window.ensure(W + 128);
+        slots[k]->staged.ensure(W + 128);
+    }
+    struct Pending {
+        std::vector<size_t> files;  // files whose hashes land in this slot's host_hashes
+        bool busy = false;
+    } pend[2];
+    sd_checksum_batch pack_batch[2], big;
+    int cur = 0;
+    auto harvest = [&](int k) {
+        if (!pend[k].busy) return;
+        HIP_CHECK(hipStreamSynchronize(slots[k]->stream));
+        const uint8_t* h = reinterpret_cast<const uint8_t*>(slots[k]->host_hashes.p);
+        for (size_t q = 0; q < pend[k].files.size(); q++)
+            to_hex(h + 32 * q, 32, out_hex65 + pend[k].files[q] * 65);  // hash.rs:21-23
+        pend[k].files.clear();
+        pend[k].busy = false;
+    };
+    std::vector<size_t> pack;
+    std::vector<uint64_t> pack_len;
+    uint64_t pack_bytes = 0;
+    auto submit_pack = [&]() {
+        if (pack.empty()) return;
+        const int k = cur;
+        cur ^= 1;
+        harvest(k);
+        Slot& sl = *slots[k];
+        uint8_t* win = reinterpret_cast<uint8_t*>(sl.window.p);
+        std::vector<uint64_t> offs, lens;
+        std::vector<size_t> ok;
+        uint64_t off = 0;
+        for (size_t q = 0; q < pack.size(); q++) {  // hash.rs:13-20 reads, one pread per file
+            const size_t i = pack[q];
+            const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+            if (fd < 0) {
+                status[i] = io_status(errno);
+                continue;
+            }
+            const int32_t st = pread_exact(fd, win + off, pack_len[q], 0);
+            close(fd);
+            if (st != SD_FILE_OK) {
+                status[i] = st;
+                continue;
+            }
+            memset(win + off + pack_len[q], 0, align_up(pack_len[q] + 1, 64) - pack_len[q]);
+            offs.push_back(off);
+            lens.push_back(pack_len[q]);
+            ok.push_back(i);
+            off = align_up(off + pack_len[q] + 1, 64);
+        }
+        pack.clear();
+        pack_len.clear();
+        pack_bytes = 0;
+        if (ok.empty()) return;
+        plan_checksum_batch(&pack_batch[k], offs.data(), lens.data(), ok.size(), sl.stream);
+        sl.hashes.ensure(ok.size() * 32);
+        sl.host_hashes.ensure(ok.size() * 32);
+        HIP_CHECK(hipMemcpyAsync(sl.staged.p, win, off + 64, hipMemcpyHostToDevice, sl.stream));
+        run_checksum_batch(&pack_batch[k], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
+        HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, ok.size() * 32, hipMemcpyDeviceToHost, sl.stream));
+        pend[k].files = std::move(ok);
+        pend[k].busy = true;
+    };
     for (size_t i = 0; i < n; i++) {
         status[i] = SD_FILE_OK;
+        struct stat stt;
+        if (stat(paths[i], &stt) != 0) {
+            status[i] = io_status(errno);
+            continue;
+        }
+        const uint64_t len = (uint64_t)stt.st_size;  // hash.rs reads to EOF; the length is fixed here
+        if (len + 128 <= W) {
+            if (pack_bytes + align_up(len + 1, 64) + 64 > W) submit_pack();
+            pack.push_back(i);
+            pack_len.push_back(len);
+            pack_bytes += align_up(len + 1, 64);
+            continue;
+        }
+        // a large file: flush the pack, then stream windows through alternating slots
+        submit_pack();
+        harvest(0);
+        harvest(1);
         const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
         if (fd < 0) {
             status[i] = io_status(errno);
             continue;
         }
-        struct stat stt;
-        if (fstat(fd, &stt) != 0) {
-            status[i] = io_status(errno);
-            close(fd);
-            continue;
-        }
-        // hash.rs:14-20 reads until a short read; the length is fixed at fstat here
-        const uint64_t len = (uint64_t)stt.st_size;
         const uint64_t off0 = 0;
-        std::unique_ptr<sd_checksum_batch> b(build_checksum_batch(&off0, &len, 1));
-        uint32_t* out = slot->hashes.as<uint32_t>();
-        const uint64_t blocks_per_window = W / CK_BLOCK_BYTES;
-        for (uint64_t pos = 0; pos < std::max<uint64_t>(len, 1); pos += W) {
+        plan_checksum_batch(&big, &off0, &len, 1, nullptr);
+        for (int k = 0; k < 2; k++) slots[k]->hashes.ensure(32);
+        const uint32_t blocks_per_window = (uint32_t)(W / CK_BLOCK_BYTES);
+        for (uint64_t pos = 0; pos < len && status[i] == SD_FILE_OK; pos += W) {
+            const int k = cur;
+            cur ^= 1;
+            HIP_CHECK(hipStreamSynchronize(slots[k]->stream));  // its window is free again
+            Slot& sl = *slots[k];
+            uint8_t* win = reinterpret_cast<uint8_t*>(sl.window.p);
             const uint64_t n_here = std::min<uint64_t>(W, len - pos);
-            if (n_here) {
-                HIP_CHECK(hipStreamSynchronize(slot->stream));  // window reuse
-                const int32_t st = pread_exact(fd, win, n_here, pos);
-                if (st != SD_FILE_OK) {
-                    status[i] = st;
-                    break;
-                }
+            const int32_t st = pread_exact(fd, win, n_here, pos);
+            if (st != SD_FILE_OK) {
+                status[i] = st;
+                break;
             }
             memset(win + n_here, 0, 64);
-            HIP_CHECK(hipMemcpyAsync(slot->staged.p, win, align_up(n_here, 64) + (n_here ? 0 : 64),
-                                     hipMemcpyHostToDevice, slot->stream));
+            HIP_CHECK(hipMemcpyAsync(sl.staged.p, win, align_up(n_here, 64) + 64, hipMemcpyHostToDevice, sl.stream));
             const uint32_t wg0 = (uint32_t)(pos / CK_BLOCK_BYTES);
-            const uint32_t wg1 = (uint32_t)std::min<uint64_t>(b->wg_map_h.size(), wg0 + blocks_per_window);
-            run_checksum_leaf(b.get(), slot->staged.as<uint8_t>(), pos, wg0, wg1, out, slot->stream);
-            if (len == 0) break;
+            const uint32_t wg1 = (uint32_t)std::min<uint64_t>(big.wg_map_h.size(), (uint64_t)wg0 + blocks_per_window);
+            run_checksum_leaf(&big, sl.staged.as<uint8_t>(), pos, wg0, wg1, sl.hashes.as<uint32_t>(), sl.stream);
         }
         close(fd);
+        HIP_CHECK(hipStreamSynchronize(slots[0]->stream));
+        HIP_CHECK(hipStreamSynchronize(slots[1]->stream));
         if (status[i] != SD_FILE_OK) continue;
-        run_checksum_reduce(b.get(), out, slot->stream);
-        HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, out, 32, hipMemcpyDeviceToHost, slot->stream));
-        HIP_CHECK(hipStreamSynchronize(slot->stream));
-        to_hex(reinterpret_cast<const uint8_t*>(slot->host_hashes.p), 32, out_hex65 + i * 65);  // hash.rs:21-23
+        Slot& sl = *slots[0];
+        run_checksum_reduce(&big, sl.hashes.as<uint32_t>(), sl.stream);
+        sl.host_hashes.ensure(32);
+        HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, 32, hipMemcpyDeviceToHost, sl.stream));
+        HIP_CHECK(hipStreamSynchronize(sl.stream));
+        to_hex(reinterpret_cast<const uint8_t*>(sl.host_hashes.p), 32, out_hex65 + i * 65);
     }
+    submit_pack();
+    harvest(0);
+    harvest(1);
     return SD_OK;
     SD_GUARD_END
 }
@@ -832,14 +956,14 @@ int sd_dedup_partition(sd_cas_ctx* ctx, const uint8_t* d_hash32, const uint8_t* 
     SD_GUARD_END
 }
 
-int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, uint64_t* d_rep, uint64_t* n_groups,
-                   void* stream) {
+int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, int flags, uint64_t* d_rep,
+                   uint64_t* n_groups, void* stream) {
     SD_GUARD_BEGIN
     if (!ctx || !n_groups || (m && (!d_records || !d_rep))) throw sd_failure(SD_ERR_INVALID, "null argument");
     ctx->bind();
     hipStream_t s = ctx->pick(stream);
     size_t need = 0;
-    HIP_CHECK(sdk::dedup_group(d_records, m, d_rep, nullptr, nullptr, &need, s));
+    HIP_CHECK(sdk::dedup_group(d_records, m, flags, d_rep, nullptr, nullptr, &need, s));
     auto slot = ctx->acquire();
     struct Rel {
         sd_cas_ctx* c;
@@ -850,7 +974,7 @@ int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, uint64_t* d
     slot->hashes.ensure(sizeof(uint64_t));
     slot->host_hashes.ensure(sizeof(uint64_t));
     size_t have = slot->staged.bytes;
-    HIP_CHECK(sdk::dedup_group(d_records, m, d_rep, slot->hashes.as<uint64_t>(), slot->staged.p, &have, s));
+    HIP_CHECK(sdk::dedup_group(d_records, m, flags, d_rep, slot->hashes.as<uint64_t>(), slot->staged.p, &have, s));
     HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, slot->hashes.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     *n_groups = *reinterpret_cast<uint64_t*>(slot->host_hashes.p);

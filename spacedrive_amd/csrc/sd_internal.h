@@ -49,6 +49,6 @@ hipError_t dedup_partition(const uint8_t* hash32, const uint8_t* valid, uint64_t
                            uint64_t* counts, uint64_t* records, uint64_t* scratch, hipStream_t s);
 // device scratch bytes dedup_partition needs; the valid-record total is its last u64
 size_t dedup_partition_scratch(int nparts);
-hipError_t dedup_group(uint64_t* records, uint64_t m, uint64_t* rep, uint64_t* n_groups_dev, void* scratch,
-                       size_t* scratch_bytes, hipStream_t s);
+hipError_t dedup_group(uint64_t* records, uint64_t m, int flags, uint64_t* rep, uint64_t* n_groups_dev,
+                       void* scratch, size_t* scratch_bytes, hipStream_t s);
 }  // namespace sdk

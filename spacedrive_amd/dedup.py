@@ -58,11 +58,11 @@ def exchange(send_records: torch.Tensor, send_counts: torch.Tensor,
     return out
 
 
-def group_device(ctx, records: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, int]:
+def group_device(ctx, records: torch.Tensor, index_sorted: bool = False) -> Tuple[torch.Tensor, torch.Tensor, int]:
     """Sort received records by (cas_id, index) and map each to its group's smallest index."""
     m = records.shape[0]
     rep = torch.empty(max(m, 1), dtype=torch.int64, device=records.device)
-    ng = ctx.dedup_group(records, m, rep)
+    ng = ctx.dedup_group(records, m, rep, index_sorted=index_sorted)
     return records, rep[:m], ng
 
 
@@ -79,7 +79,9 @@ def dedup_shard(ctx, d_hash32: torch.Tensor, d_valid: Optional[torch.Tensor], n_
     recs = torch.empty((max(n_local, 1), 2), dtype=torch.int64, device=dev)
     nv = ctx.dedup_partition(d_hash32, d_valid, n_local, global_base, world, counts, recs)
     recv = exchange(recs[:nv], counts, group)
-    return group_device(ctx, recv)
+    # the partition is stable and shard r holds indices [r*n, (r+1)*n): the received
+    # records are in ascending index order, so one stable cas_id sort suffices
+    return group_device(ctx, recv, index_sorted=True)
 
 
 # ------------------------------------------------------------------ host reference

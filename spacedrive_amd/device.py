@@ -94,10 +94,10 @@ class Context:
                                        _ptr(d_counts), _ptr(d_records), ctypes.byref(nv), _stream(stream)))
         return int(nv.value)
 
-    def dedup_group(self, d_records, m: int, d_rep, stream=None) -> int:
+    def dedup_group(self, d_records, m: int, d_rep, stream=None, index_sorted: bool = False) -> int:
         ng = ctypes.c_uint64(0)
-        check(lib().sd_dedup_group(self.handle, _ptr(d_records), m, _ptr(d_rep), ctypes.byref(ng),
-                                   _stream(stream)))
+        check(lib().sd_dedup_group(self.handle, _ptr(d_records), m, 1 if index_sorted else 0, _ptr(d_rep),
+                                   ctypes.byref(ng), _stream(stream)))
         return int(ng.value)
 
 

@@ -110,3 +110,34 @@ def test_no_cpu_fallback_without_gpu():
     with pytest.raises(SdCasError) as e:
         check(lib().sd_cas_ctx_create(0, ctypes.byref(h)))
     assert e.value.rc == -2
+
+
+def test_stage_files_threaded_equals_single(tmp_path):
+    # sd_cas_stage_files on 8 threads == sd_cas_stage_file one by one, incl. error statuses
+    from oracle import cas_spec as cs
+    from spacedrive_amd.device import stage_plan
+    sizes = [1, 1000, 102400, 102401, 250000, 77, 0, 150000]
+    paths = []
+    for i, sz in enumerate(sizes):
+        p = tmp_path / f"g{i}"
+        p.write_bytes(cs.synth_bytes(70 + i, 0, 0, sz if i != 7 else 140000))  # last: shorter than planned
+        paths.append(str(p))
+    paths.append(str(tmp_path / "missing"))
+    sizes.append(5000)
+    ext, total = stage_plan(np.array(sizes, np.uint64))
+    a = np.full(total, 0x11, np.uint8)
+    b = np.full(total, 0x22, np.uint8)
+    st_a = np.zeros(len(sizes), np.int32)
+    for i, p in enumerate(paths):
+        st = ctypes.c_int32()
+        check(lib().sd_cas_stage_file(os.fsencode(p), ctypes.c_void_p(ext.ctypes.data + 24 * i),
+                                      ctypes.c_void_p(a.ctypes.data), ctypes.byref(st)))
+        st_a[i] = st.value
+    arr = (ctypes.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+    st_b = np.full(len(sizes), -7, np.int32)
+    check(lib().sd_cas_stage_files(arr, ext.ctypes.data, len(paths), b.ctypes.data, st_b.ctypes.data, 8))
+    assert list(st_a) == list(st_b)
+    assert st_b[7] == _native.SD_FILE_SHORT_READ and (st_b[8] & 0xFFFF) == _native.SD_FILE_IO_ERROR
+    for i in range(7):
+        o, L = int(ext["msg_offset"][i]), int(ext["msg_len"][i])
+        assert a[o:o + L].tobytes() == b[o:o + L].tobytes() == cs.cas_message(cs.synth_reader(70 + i), sizes[i])

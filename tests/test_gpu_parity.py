@@ -284,15 +284,79 @@ def test_dedup_group_matches_host(ctx):
         for d in range(nparts):
             seg = r[start:start + hcounts[d]]
             start += hcounts[d]
-            sub = torch.from_numpy(seg.copy()).cuda()
-            rep = torch.zeros(max(len(seg), 1), dtype=torch.int64, device="cuda")
-            ng = ctx.dedup_group(sub, len(seg), rep)
             gr, grep, gng = group_host(seg)
-            assert ng == gng
-            assert np.array_equal(sub.cpu().numpy(), gr)
-            assert np.array_equal(rep.cpu().numpy()[:len(seg)], grep)
+            for sorted_flag, src in ((True, seg), (False, seg[::-1].copy())):  # fast path; general path
+                sub = torch.from_numpy(src.copy()).cuda()
+                rep = torch.zeros(max(len(seg), 1), dtype=torch.int64, device="cuda")
+                ng = ctx.dedup_group(sub, len(seg), rep, index_sorted=sorted_flag)
+                assert ng == gng
+                assert np.array_equal(sub.cpu().numpy(), gr)
+                assert np.array_equal(rep.cpu().numpy()[:len(seg)], grep)
 
 
 def test_valu_peak_plausible(ctx):
     v = ctx.valu_peak()
     assert 5e12 < v < 2e14, v
+
+
+def test_file_checksums_packing_and_streaming(ctx, tmp_path):
+    # many small files packed per window, a file larger than the 256 MiB window streamed
+    # between them, an unreadable path in the middle: results in input order
+    import spacedrive_amd as sd
+    from oracle import native
+    rng = np.random.default_rng(11)
+    sizes = [int(x) for x in rng.integers(0, 3 << 20, 150)]
+    sizes[40] = (300 << 20) + 7
+    sizes[41] = 256 << 20  # exactly one window + nothing: packed? no -> streamed (len + 128 > W)
+    sizes[42] = 0
+    paths = []
+    for i, sz in enumerate(sizes):
+        p = tmp_path / f"c{i}"
+        with open(p, "wb") as f:
+            pos = 0
+            while pos < sz:
+                k = min(64 << 20, sz - pos)
+                f.write(cs.synth_bytes(3000 + i, 0, pos, k))
+                pos += k
+        paths.append(str(p))
+    paths.insert(77, str(tmp_path / "nope"))
+    got = sd.file_checksums(paths)
+    assert isinstance(got[77], OSError)
+    del got[77]
+    want = native.checksums_synth(np.array(sizes, np.uint64), np.arange(3000, 3000 + len(sizes), dtype=np.uint64),
+                                  nthreads=NT)
+    for i in range(len(sizes)):
+        assert got[i] == want[i].tobytes().hex(), (i, sizes[i])
+
+
+def test_concurrent_callers_share_a_context(ctx, tmp_path):
+    # the C ABI is thread-safe and re-entrant: 6 host threads, one context
+    import threading
+    import spacedrive_amd as sd
+    paths, sizes = [], []
+    for i in range(60):
+        sz = [10, 5000, 102400, 300000][i % 4] + i
+        p = tmp_path / f"t{i}"
+        p.write_bytes(cs.synth_bytes(500 + i, 0, 0, sz))
+        paths.append(str(p))
+        sizes.append(sz)
+    want = [cs.generate_cas_id(cs.synth_reader(500 + i), sizes[i]) for i in range(60)]
+    errors = []
+
+    def worker(k):
+        try:
+            for _ in range(5):
+                sl = slice(k * 10, k * 10 + 10)
+                got = sd.generate_cas_ids(paths[sl], sizes[sl])
+                assert got == want[sl]
+                sums = sd.file_checksums(paths[sl])
+                assert all(isinstance(x, str) and len(x) == 64 for x in sums)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
