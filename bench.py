@@ -210,14 +210,15 @@ def main():
         elapsed = float(t.item())
     hash_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
     dedup_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
-    recs, rep, n_groups = res
+    recs, rep, n_groups, owners = res
     # every valid file lands on exactly one rank; groups never straddle ranks
     tot = torch.tensor([recs.shape[0], n_groups, int((sizes != 0).sum())], dtype=torch.int64,
                        device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(tot)
     dedup_totals = {"records": int(tot[0]), "groups": int(tot[1]), "valid_files": int(tot[2]),
-                    "records_on_rank0": int(recs.shape[0])}
+                    "records_on_rank0": int(recs.shape[0]),
+                    "objects_created_on_rank0": int((owners == recs[:, 1]).sum())}
     assert dedup_totals["records"] == dedup_totals["valid_files"], dedup_totals
     files_total = n_total * args.steps
     value = files_total / elapsed
@@ -239,7 +240,7 @@ def main():
         "vs_baseline": None, "dtype": "u32", "data": "synthetic (device-generated, SURVEY.md 8(d) generator)",
         "config": {"workload": f"10M-file library mixture (configs[0] mix: 60% <=100KiB whole-content, 40% sampled; "
                                f"10% dups, 1% sample twins), {n} files per GPU, step = hash shard + "
-                               f"cas_id-prefix all-to-all dedup",
+                               f"cas_id-prefix all-to-all dedup + Object owners (chunk-of-100 rule)",
                    "files_per_gpu": n, "global_files": n_total, "parallelism": f"file-sharded x{world}"},
         "roofline": {"bound": "valu", "achieved": hash_valu / 1e12, "peak": VALU_PEAK_TOPS,
                      "unit": "T int32 VALU lane-ops/s", "frac": hash_valu / 1e12 / VALU_PEAK_TOPS,
@@ -257,7 +258,7 @@ def main():
     }
     if rank == 0 and world == 1 and args.host_staged_files > 0:
         out["host_staged"] = host_staged(ctx, ext, d_staged, batch, args.host_staged_files, dev)
-    del d_staged, recs, rep
+    del d_staged, recs, rep, owners
     torch.cuda.empty_cache()
 
     # configs[3]: validator checksums, 16 files of (G/16) GiB per GPU

@@ -68,10 +68,12 @@ def group_device(ctx, records: torch.Tensor, index_sorted: bool = False) -> Tupl
 
 def dedup_shard(ctx, d_hash32: torch.Tensor, d_valid: Optional[torch.Tensor], n_local: int, global_base: int,
                 group: Optional[dist.ProcessGroup] = None):
-    """Full distributed step on one rank: partition -> exchange -> group.
+    """Full distributed step on one rank: partition -> exchange -> group -> Object owners.
 
-    Returns (records int64 [m, 2] sorted by (key, index), rep int64 [m], n_groups) for
-    the cas_id prefix range this rank owns.
+    Returns (records int64 [m, 2] sorted by (key, index), rep int64 [m], n_groups,
+    owner int64 [m]) for the cas_id prefix range this rank owns; owner is the file whose
+    Object each record links to under the reference's chunk-of-100 rule
+    (spacedrive_amd/identifier.py).
     """
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     dev = d_hash32.device
@@ -81,7 +83,9 @@ def dedup_shard(ctx, d_hash32: torch.Tensor, d_valid: Optional[torch.Tensor], n_
     recv = exchange(recs[:nv], counts, group)
     # the partition is stable and shard r holds indices [r*n, (r+1)*n): the received
     # records are in ascending index order, so one stable cas_id sort suffices
-    return group_device(ctx, recv, index_sorted=True)
+    records, rep, ng = group_device(ctx, recv, index_sorted=True)
+    from .identifier import object_owners
+    return records, rep, ng, object_owners(records[:, 1], rep)
 
 
 # ------------------------------------------------------------------ host reference

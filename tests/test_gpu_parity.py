@@ -360,3 +360,21 @@ def test_concurrent_callers_share_a_context(ctx, tmp_path):
     for t in th:
         t.join()
     assert not errors, errors
+
+
+def test_pipeline_object_owners_vs_reference_replay(ctx, oracle_native):
+    # hash (GPU) -> partition -> group -> owners == identifier_job_step replay on oracle cas_ids
+    from oracle.identifier_spec import identifier_replay
+    from spacedrive_amd.dedup import dedup_shard
+    n = 20000
+    sizes, cids, twins = synth.library(0, n, n, dup_frac=0.3)
+    h = gpu_cas(ctx, sizes, cids, twins)
+    d_hash = torch.from_numpy(h.copy()).cuda()
+    d_valid = torch.from_numpy((sizes != 0).astype(np.uint8)).cuda()
+    recs, rep, ng, owner = dedup_shard(ctx, d_hash, d_valid, n, 0)
+    got = np.arange(n)
+    got[recs[:, 1].cpu().numpy()] = owner.cpu().numpy()
+    ids = oracle_native.cas_ids_synth(sizes, cids, twins, nthreads=NT)
+    cas = [None if sizes[i] == 0 else ids[i].tobytes().hex() for i in range(n)]
+    want, _ = identifier_replay(cas)
+    assert got.tolist() == want
