@@ -506,6 +506,23 @@ hipError_t launch_cas_mixed(const uint8_t* staged, const sd_extent* ext, const u
     return hipGetLastError();
 }
 
+hipError_t launch_whole_leaf(const uint8_t* staged, const sd_extent* ext, const uint32_t* order,
+                             const uint32_t* chunk_prefix, const uint32_t* hint, uint32_t nw, uint32_t total_chunks,
+                             uint32_t* cvbuf, uint32_t* out, hipStream_t s) {
+    if (nw == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_whole_leaf, dim3((total_chunks + 255) / 256), dim3(256), 0, s, staged, ext, order,
+                       chunk_prefix, hint, nw, total_chunks, cvbuf, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_whole_tree(const uint32_t* order, const uint32_t* chunk_prefix, uint32_t n_multi, uint32_t* cvbuf,
+                             uint32_t* out, hipStream_t s) {
+    if (n_multi == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_whole_tree, dim3((n_multi + 255) / 256), dim3(256), 0, s, order, chunk_prefix, n_multi,
+                       cvbuf, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_whole(const uint8_t* staged, const sd_extent* ext, const uint32_t* order,
                         const uint32_t* chunk_prefix, const uint32_t* hint, uint32_t nw, uint32_t total_chunks,
                         uint32_t n_multi, uint32_t* cvbuf, uint32_t* out, hipStream_t s) {

@@ -171,6 +171,14 @@ struct sd_cas_batch {
     uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0;
     uint32_t n_groups = 0;  // whole-file groups of the fused kernel
     DevBuf ext, sidx, order, prefix, hint, cvbuf, groups;
+    // variant 2: the whole-file tree kernel runs on a side stream beside the sampled kernel
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    ~sd_cas_batch() {
+        if (side) (void)hipStreamDestroy(side);
+        if (fork) (void)hipEventDestroy(fork);
+        if (join) (void)hipEventDestroy(join);
+    }
     std::vector<sd_extent> h_ext;  // host copies backing async uploads
     std::vector<uint32_t> h_sidx, h_order, h_prefix, h_hint;
     std::vector<uint2> h_groups;
@@ -321,6 +329,28 @@ void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_ha
         HIP_CHECK(sdk::launch_cas_mixed(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(),
                                         (parts & SD_PART_SAMPLED) ? b->n_sampled : 0, b->order.as<uint32_t>(),
                                         b->groups.as<uint2>(), (parts & SD_PART_WHOLE) ? b->n_groups : 0, out, s));
+        return;
+    }
+    if (tuning_get(SD_TUNE_WHOLE_VARIANT) == 2 && (parts & SD_PART_WHOLE) && (parts & SD_PART_SAMPLED) && b->n_multi) {
+        // whole-file leaf, then the sampled kernel on `s` beside the whole-file tree on a
+        // side stream (the tree's long single-lane chains leave most issue slots idle)
+        auto* mb = const_cast<sd_cas_batch*>(b);
+        if (!mb->side) {
+            HIP_CHECK(hipStreamCreateWithFlags(&mb->side, hipStreamNonBlocking));
+            HIP_CHECK(hipEventCreateWithFlags(&mb->fork, hipEventDisableTiming));
+            HIP_CHECK(hipEventCreateWithFlags(&mb->join, hipEventDisableTiming));
+        }
+        HIP_CHECK(sdk::launch_whole_leaf(d_staged, b->ext.as<sd_extent>(), b->order.as<uint32_t>(),
+                                         b->prefix.as<uint32_t>(), b->hint.as<uint32_t>(), b->n_whole,
+                                         b->total_chunks, b->cvbuf.as<uint32_t>(), out, s));
+        HIP_CHECK(hipEventRecord(mb->fork, s));
+        HIP_CHECK(hipStreamWaitEvent(mb->side, mb->fork, 0));
+        HIP_CHECK(sdk::launch_whole_tree(b->order.as<uint32_t>(), b->prefix.as<uint32_t>(), b->n_multi,
+                                         b->cvbuf.as<uint32_t>(), out, mb->side));
+        HIP_CHECK(hipEventRecord(mb->join, mb->side));
+        HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled, out,
+                                          s));
+        HIP_CHECK(hipStreamWaitEvent(s, mb->join, 0));
         return;
     }
     // variant 1 (default): separate sampled kernel, whole-file leaf kernel, whole-file tree

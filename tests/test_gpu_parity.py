@@ -120,7 +120,7 @@ def test_sd_cas_ids_pipelined_windows(ctx):
             assert status[i] == 0 and raw[17 * i:17 * i + 16].decode() == h[i, :8].tobytes().hex(), i
 
 
-@pytest.fixture(params=[0, 1], ids=["fused", "split"])
+@pytest.fixture(params=[0, 1, 2], ids=["fused", "split", "side-stream"])
 def whole_variant(request):
     from spacedrive_amd._native import lib
     assert lib().sd_cas_set_tuning(b"whole_variant", request.param) == 0
