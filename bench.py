@@ -56,6 +56,9 @@ def parse():
                    help="0 = fused launch; 1 = separate sampled / whole-leaf / whole-tree kernels (default)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (rehearsal)")
     p.add_argument("--share-gpu", action="store_true", help="map every rank onto the visible GPUs (rehearsal)")
+    p.add_argument("--config-files", type=int, default=1_000_000,
+                   help="N=1 only: files of the configs[1] (small) and configs[2] (sampled) kernel legs; 0 = skip")
+    p.add_argument("--config-reps", type=int, default=5)
     p.add_argument("--host-staged-files", type=int, default=0,
                    help="N=1 only: also time the PCIe-inclusive drop-in path on this many files (DESIGN.md)")
     return p.parse_args()
@@ -140,6 +143,50 @@ def host_staged(ctx, ext, d_staged, batch, k, dev):
                     "not overlapped; the reference's own cost is reading the files (6 preads per sampled file)"}
 
 
+def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: float):
+    """configs[1] (1 M files <= 100 KiB, whole-content cas_id) or configs[2] (1 M files
+    > 100 KiB, sampled cas_id) on this GPU: kernel-only files/s over device-resident
+    staged messages, timed with HIP events on the launch stream, plus determinism of the
+    full 32-byte hashes across runs (a size-independent property; bit-exactness vs the
+    oracle is pinned by tests/test_gpu_parity.py on the same generator)."""
+    import spacedrive_amd as sd
+    from spacedrive_amd import synth
+    gen = synth.small_library if which == "small" else synth.sampled_library
+    sizes, cids, twins = gen(0, nfiles)
+    ext, total = sd.stage_plan(sizes)
+    d_staged = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    d_ext = torch.from_numpy(ext.view(np.uint8).copy()).to(dev)
+    ctx.synth_stage_cas(torch.from_numpy(sizes.view(np.int64)).to(dev), torch.from_numpy(cids.view(np.int64)).to(dev),
+                        torch.from_numpy(twins.astype(np.int32)).to(dev), d_ext, nfiles, d_staged, stream)
+    b = ctx.cas_batch(ext)
+    h0 = torch.zeros(nfiles * 32, dtype=torch.uint8, device=dev)
+    h1 = torch.zeros(nfiles * 32, dtype=torch.uint8, device=dev)
+    b.run(d_staged, h0, stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(reps):
+        b.run(d_staged, h1, stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    deterministic = bool(torch.equal(h0, h1))
+    valu = b.compressions * 672 / (ms * 1e-3)
+    res = {"workload": ("configs[1]: 1M files <= 100 KiB, whole-content cas_id (log-uniform sizes 1..102400)"
+                        if which == "small" else
+                        "configs[2]: 1M files > 100 KiB, sampled cas_id (log-uniform sizes 102401..4 GiB)"),
+           "files": nfiles, "kernel_ms": ms, "files_per_s": nfiles / (ms * 1e-3),
+           "msg_GBps": b.msg_bytes / (ms * 1e-3) / 1e9, "compressions": b.compressions,
+           "valu_frac": valu / 1e12 / VALU_PEAK_TOPS,
+           "valu_frac_of_measured_peak": valu / valu_peak if valu_peak else None,
+           "kernels": ["k_cas_sampled"] if which == "sampled" else ["k_whole_leaf", "k_whole_tree"],
+           "deterministic": deterministic}
+    del d_staged, h0, h1, b
+    torch.cuda.empty_cache()
+    assert deterministic, which
+    return res
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -175,20 +222,28 @@ def main():
         f"{batch.msg_bytes / 1e9:.2f} GB of messages, {batch.compressions / 1e9:.3f} G compressions")
 
     stream = torch.cuda.current_stream()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     from spacedrive_amd._native import lib
     lib().sd_cas_set_tuning(b"whole_variant", args.whole_variant)
-    kname = "k_cas_mixed" if args.whole_variant == 0 else "k_cas_sampled"
+    split = args.whole_variant == 1  # separate launches: the dominant kernel is timed on its own
 
     def step(k=None):
         if k is not None:
             ev[k][0].record(stream)
-        batch.run(d_staged, d_hash, stream)  # k_cas_sampled, k_whole_leaf, k_whole_tree
-        if k is not None:
-            ev[k][1].record(stream)
-        r = dedup.dedup_shard(ctx, d_hash.view(n, 32), d_valid, n, start)
+        if split:
+            batch.run_part(1, d_staged, d_hash, stream)  # k_cas_sampled
+            if k is not None:
+                ev[k][1].record(stream)
+            batch.run_part(2, d_staged, d_hash, stream)  # k_whole_leaf + k_whole_tree
+        else:
+            batch.run(d_staged, d_hash, stream)
+            if k is not None:
+                ev[k][1].record(stream)
         if k is not None:
             ev[k][2].record(stream)
+        r = dedup.dedup_shard(ctx, d_hash.view(n, 32), d_valid, n, start)
+        if k is not None:
+            ev[k][3].record(stream)
         return r
 
     for _ in range(args.warmup):
@@ -208,8 +263,9 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    hash_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
-    dedup_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
+    def avg(a, b):
+        return sum(ev[k][a].elapsed_time(ev[k][b]) for k in range(args.steps)) / args.steps
+    hash_ms, sampled_ms, dedup_ms = avg(0, 2), avg(0, 1), avg(2, 3)
     recs, rep, n_groups, owners = res
     # every valid file lands on exactly one rank; groups never straddle ranks
     tot = torch.tensor([recs.shape[0], n_groups, int((sizes != 0).sum())], dtype=torch.int64,
@@ -223,15 +279,23 @@ def main():
     files_total = n_total * args.steps
     value = files_total / elapsed
 
-    # roofline of the hashing phase (its dominant kernel is k_cas_sampled, 81 % of the work;
-    # the three launches run back to back on one stream, bracketed by events): VALU = all
-    # BLAKE3 compressions x 672 lane-ops; bytes = staged messages + 32 B hash out per file
-    hash_bytes = batch.msg_bytes + 32 * n
-    hash_gbps = hash_bytes / (hash_ms * 1e-3) / 1e9
+    # roofline of the dominant kernel, k_cas_sampled (81 % of the shard's compressions),
+    # timed on its own with HIP events on its launch stream: 953 compressions x 672 VALU
+    # lane-ops per sampled file; bytes = 57 352 B message read + 32 B hash written per file
     valu_peak = ctx.valu_peak()
+    if split:
+        dom_kernel, dom_ms = "k_cas_sampled", sampled_ms
+        dom_comp = 953 * batch.n_sampled
+        dom_bytes = batch.n_sampled * (SAMPLED_MSG + 32)
+    else:  # fused / side-stream variants: the whole hashing phase
+        dom_kernel, dom_ms = ("k_cas_mixed" if args.whole_variant == 0 else "hash phase"), hash_ms
+        dom_comp, dom_bytes = batch.compressions, batch.msg_bytes + 32 * n
+    dom_valu = dom_comp * 672 / (dom_ms * 1e-3)
+    dom_gbps = dom_bytes / (dom_ms * 1e-3) / 1e9
+    hash_bytes = batch.msg_bytes + 32 * n
     hash_valu = batch.compressions * 672 / (hash_ms * 1e-3)
     phase = ["k_cas_mixed"] if args.whole_variant == 0 else ["k_cas_sampled", "k_whole_leaf", "k_whole_tree"]
-    traffic = pmc_traffic(phase)
+    traffic = pmc_traffic(dom_kernel) if split else pmc_traffic(phase)
 
     out = {
         "metric": "cas_id files/sec (10M synthetic files) + checksum GB/s at 1/2/4/8 MI355X",
@@ -242,16 +306,22 @@ def main():
                                f"10% dups, 1% sample twins), {n} files per GPU, step = hash shard + "
                                f"cas_id-prefix all-to-all dedup + Object owners (chunk-of-100 rule)",
                    "files_per_gpu": n, "global_files": n_total, "parallelism": f"file-sharded x{world}"},
-        "roofline": {"bound": "valu", "achieved": hash_valu / 1e12, "peak": VALU_PEAK_TOPS,
-                     "unit": "T int32 VALU lane-ops/s", "frac": hash_valu / 1e12 / VALU_PEAK_TOPS,
-                     "traffic": traffic, "kernel": kname, "kernels_in_phase": phase, "kernel_ms": hash_ms,
-                     "algorithmic": {"compressions": batch.compressions, "lane_ops_per_compression": 672,
-                                     "bytes": hash_bytes},
+        "roofline": {"bound": "valu", "achieved": dom_valu / 1e12, "peak": VALU_PEAK_TOPS,
+                     "unit": "T int32 VALU lane-ops/s", "frac": dom_valu / 1e12 / VALU_PEAK_TOPS,
+                     "traffic": traffic, "kernel": dom_kernel, "kernel_ms": dom_ms,
+                     "algorithmic": {"compressions_per_launch": dom_comp, "lane_ops_per_compression": 672,
+                                     "bytes_per_launch": dom_bytes,
+                                     "per_unit": "sampled file: 953 compressions, 57352 B read + 32 B written"},
                      "measured_valu_peak": valu_peak / 1e12,
-                     "frac_of_measured_peak": hash_valu / valu_peak if valu_peak else None,
-                     "hbm": {"achieved": hash_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                             "frac": hash_gbps / HBM_PEAK_GBPS}},
-        "kernels": {"hash_ms": hash_ms, "dedup_and_exchange_ms": dedup_ms,
+                     "frac_of_measured_peak": dom_valu / valu_peak if valu_peak else None,
+                     "hbm": {"achieved": dom_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                             "frac": dom_gbps / HBM_PEAK_GBPS},
+                     "phase": {"kernels": phase, "ms": hash_ms, "compressions": batch.compressions,
+                               "bytes": hash_bytes, "achieved": hash_valu / 1e12,
+                               "frac": hash_valu / 1e12 / VALU_PEAK_TOPS,
+                               "traffic": pmc_traffic(phase)}},
+        "kernels": {"hash_ms": hash_ms, "sampled_ms": sampled_ms if split else None,
+                    "whole_ms": hash_ms - sampled_ms if split else None, "dedup_and_exchange_ms": dedup_ms,
                     "host_overhead_ms": elapsed / args.steps * 1e3 - hash_ms - dedup_ms,
                     "sampled_files": batch.n_sampled, "whole_files": batch.n_whole},
         "dedup": dedup_totals,
@@ -295,6 +365,10 @@ def main():
                            "traffic": pmc_traffic("k_ck_leaf")}
         del d_data
         torch.cuda.empty_cache()
+
+    if world == 1 and args.config_files > 0:
+        out["configs"] = {k: config_leg(ctx, k, args.config_files, args.config_reps, dev, stream, valu_peak)
+                          for k in ("small", "sampled")}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sizes, cids, twins, args.cpu_seconds)

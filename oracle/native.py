@@ -44,6 +44,8 @@ def lib():
         L.sdo_cas_ids_staged_simd.restype = I
         L.sdo_checksums_simd.argtypes = [P, P, P, U64, P, I, I]
         L.sdo_checksums_simd.restype = I
+        L.sdo_cas_ids_files.argtypes = [P, P, U64, P, P, I, I]
+        L.sdo_cas_ids_files.restype = I
         L.sdo_simd_level.argtypes = [I]
         L.sdo_simd_level.restype = I
         _lib = L
@@ -87,6 +89,18 @@ def cas_ids_staged(staged: np.ndarray, extents: np.ndarray, nthreads: int = 1, s
     out = np.empty((len(extents), 8), np.uint8)
     lib().sdo_cas_ids_staged_simd(_p(staged), _p(extents), len(extents), _p(out), nthreads, simd)
     return out
+
+
+def cas_ids_files(paths, sizes, nthreads: int = 1, simd: int = -1):
+    """generate_cas_id over files on disk with the reference's read schedule (cas.rs:27-58)
+    -> (cas_id bytes [n, 8], sd_file_status [n])."""
+    n = len(paths)
+    sizes = np.ascontiguousarray(sizes, np.uint64)
+    arr = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
+    out = np.zeros((n, 8), np.uint8)
+    status = np.zeros(n, np.int32)
+    lib().sdo_cas_ids_files(arr, _p(sizes), n, _p(out), _p(status), nthreads, simd)
+    return out, status
 
 
 def simd_level(requested: int = -1) -> int:

@@ -21,11 +21,15 @@
  * identifier step, core/src/object/file_identifier/mod.rs:107-134, no rayon), and
  * nthreads = nproc is the all-cores variant of the CPU baseline.
  */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #define B3_BLOCK 64u
 #define B3_CHUNK 1024u
@@ -252,25 +256,87 @@ typedef struct {
     const uint32_t* twins;
     const uint8_t* data;
     const uint64_t *offsets, *lens;
+    const char* const* paths;
+    int32_t* status;
     uint8_t* out;
     uint32_t out_stride;
     atomic_ullong cursor;
 } job_t;
 
-enum { MODE_CAS_STAGED = 0, MODE_CAS_SYNTH = 1, MODE_CHECKSUM = 2, MODE_CHECKSUM_SYNTH = 3 };
+enum { MODE_CAS_STAGED = 0, MODE_CAS_SYNTH = 1, MODE_CHECKSUM = 2, MODE_CHECKSUM_SYNTH = 3, MODE_CAS_FILES = 4 };
+
+/* read exactly n bytes at the current position (read_exact); 0 ok, -1 EOF, else errno */
+static int read_exact_fd(int fd, uint8_t* p, uint64_t n) {
+    while (n) {
+        ssize_t r = read(fd, p, n);
+        if (r < 0) { if (errno == EINTR) continue; return errno; }
+        if (r == 0) return -1;
+        p += r; n -= (uint64_t)r;
+    }
+    return 0;
+}
+
+/* generate_cas_id (cas.rs:23-62) with the reference's own read schedule: fs::read of
+ * the whole file (size <= 102400, :27-29), else open + read_exact(head) + 4 x
+ * (seek, read_exact sample) + seek(End(-8192)) + read_exact(tail) (:31-58).  The
+ * message is assembled in `msg` (the le64 header first, :25); returns its length, or
+ * -1 with *st = 2 | errno << 16 (I/O error) or 3 (UnexpectedEof), as sd_file_status. */
+static int64_t read_cas_message(const char* path, uint64_t size, uint8_t* msg, int32_t* st) {
+    for (int i = 0; i < 8; i++) msg[i] = (uint8_t)(size >> (8 * i));
+    int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) { *st = 2 | (errno << 16); return -1; }
+    int64_t len = 8;
+    int rc = 0;
+    if (size <= MINIMUM_FILE_SIZE) { /* fs::read: the file's actual bytes, up to EOF */
+        for (;;) {
+            ssize_t r = read(fd, msg + len, 8 + MINIMUM_FILE_SIZE + 1 - (uint64_t)len);
+            if (r < 0) { if (errno == EINTR) continue; rc = errno; break; }
+            if (r == 0) break;
+            len += r;
+            if ((uint64_t)len > 8 + MINIMUM_FILE_SIZE) { rc = EFBIG; break; }
+        }
+    } else {
+        uint64_t off[6], wl[6];
+        int k = cas_windows(size, off, wl);
+        for (int i = 0; i < k && !rc; i++) {
+            if (lseek(fd, (off_t)off[i], SEEK_SET) < 0) { rc = errno; break; }
+            rc = read_exact_fd(fd, msg + len, wl[i]);
+            len += (int64_t)wl[i];
+        }
+    }
+    close(fd);
+    if (rc == -1) { *st = 3; return -1; }
+    if (rc) { *st = 2 | (rc << 16); return -1; }
+    *st = 0;
+    return len;
+}
+
 
 static void* worker(void* arg) {
     job_t* j = (job_t*)arg;
     uint8_t* scratch = NULL;
     if (j->mode == MODE_CAS_SYNTH) scratch = (uint8_t*)malloc(8 + MINIMUM_FILE_SIZE);
     if (j->mode == MODE_CHECKSUM_SYNTH) scratch = (uint8_t*)malloc(1u << 20);
+    if (j->mode == MODE_CAS_FILES) scratch = (uint8_t*)malloc(8 + MINIMUM_FILE_SIZE + 64);
     uint8_t* cvs = NULL;
     uint64_t cvs_cap = 0;
     for (;;) {
         uint64_t i = atomic_fetch_add(&j->cursor, 1);
         if (i >= j->n) break;
         uint8_t h[32];
-        if (j->mode == MODE_CAS_STAGED && j->simd) {
+        if (j->mode == MODE_CAS_FILES) {
+            int32_t st = 0;
+            int64_t m = read_cas_message(j->paths[i], j->sizes[i], scratch, &st);
+            j->status[i] = st;
+            if (m < 0) { memset(h, 0, 32); }
+            else if (j->simd) {
+                uint64_t need = 32 * (((uint64_t)m + 1023) / 1024 + 1);
+                if (need > cvs_cap) { free(cvs); cvs_cap = need * 2; cvs = (uint8_t*)malloc(cvs_cap); }
+                sdo_blake3_simd(scratch, (uint64_t)m, h, j->simd, cvs);
+            } else {
+                sdo_blake3(scratch, (uint64_t)m, h);
+            }
+        } else if (j->mode == MODE_CAS_STAGED && j->simd) {
             uint64_t need = 32 * ((j->ext[i].msg_len + 1023) / 1024 + 1);
             if (need > cvs_cap) { free(cvs); cvs_cap = need * 2; cvs = (uint8_t*)malloc(cvs_cap); }
             sdo_blake3_simd(j->staged + j->ext[i].msg_offset, j->ext[i].msg_len, h, j->simd, cvs);
@@ -371,4 +437,16 @@ void sdo_stage_synth(const uint64_t* sizes, const uint64_t* cids, const uint32_t
                      const uint64_t* offsets, uint64_t n, uint8_t* buf) {
     for (uint64_t i = 0; i < n; i++)
         sdo_synth_cas_message(cids[i], twins ? twins[i] : 0, sizes[i], buf + offsets[i]);
+}
+
+/* cas ids of files on disk through the reference's read schedule (read_cas_message);
+ * status[n] as sd_file_status.  simd as sdo_cas_ids_staged_simd.  Returns the level. */
+int sdo_cas_ids_files(const char* const* paths, const uint64_t* sizes, uint64_t n, uint8_t* out8, int32_t* status,
+                      int nthreads, int simd) {
+    job_t j = {0};
+    j.mode = MODE_CAS_FILES; j.n = n; j.paths = paths; j.sizes = sizes; j.status = status;
+    j.out = out8; j.out_stride = 8;
+    j.simd = simd == 0 ? 0 : sdo_simd_level(simd);
+    run_job(&j, nthreads);
+    return j.simd;
 }

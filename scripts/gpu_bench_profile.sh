@@ -1,0 +1,7 @@
+set -u
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.err; cat gpurun_out/bench.json
+[ $rc -eq 0 ] || exit $rc
+TAG=r1b bash scripts/profile.sh

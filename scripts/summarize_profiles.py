@@ -19,6 +19,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
 CALIB_BYTES = 4 << 30
+CMD = os.environ.get("PROF_CMD", "python3 bench.py --steps 5 --warmup 1 --checksum-steps 2 --no-cpu-baseline")
+WARMUP = int(os.environ.get("PROF_WARMUP", "1"))
 
 
 def short(name):
@@ -42,12 +44,28 @@ def main(tag):
         rows = sorted(csv.DictReader(open(stats[0])), key=lambda r: -float(r["TotalDurationNs"]))
         with open(os.path.join(PROF, f"{tag}_summary.md"), "w") as f:
             f.write(f"# rocprofv3 --kernel-trace --stats ({tag})\n\n")
-            f.write("Command: `rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py "
-                    "--steps 5 --warmup 1 --checksum-steps 2 --no-cpu-baseline` (scripts/profile.sh)\n\n")
+            f.write(f"Command: `rocprofv3 --kernel-trace --stats --output-format csv -- {CMD}` "
+                    "(scripts/profile.sh)\n\n")
             f.write("| kernel | calls | avg µs | total ms | % |\n|---|---|---|---|---|\n")
             for r in rows[:20]:
                 f.write(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                         f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.1f} |\n")
+            tr = glob.glob(os.path.join(OUT, f"prof_{tag}", "*kernel_trace.csv"))
+            if tr:  # per launch shape: bench.py's timed launches vs the warm-up ones
+                shapes = collections.defaultdict(list)
+                for r in csv.DictReader(open(tr[0])):
+                    shapes[(short(r["Kernel_Name"]), int(r["Grid_Size_X"]))].append(
+                        (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+                f.write("\nPer launch shape (kernel, grid size in work-items) for the hashing kernels, from "
+                        "the kernel trace. `steady avg` drops the first `warmup` launches of the shape "
+                        "(clock ramp), i.e. it covers the launches bench.py times.\n\n")
+                f.write("| kernel | grid | calls | avg µs | steady avg µs | min µs |\n|---|---|---|---|---|---|\n")
+                for (k, g), v in sorted(shapes.items(), key=lambda kv: -sum(kv[1])):
+                    if not k.startswith(("k_cas", "k_whole", "k_ck")):
+                        continue
+                    st = v[WARMUP:] if len(v) > WARMUP else v
+                    f.write(f"| `{k}` | {g} | {len(v)} | {sum(v) / len(v):.1f} | {sum(st) / len(st):.1f} | "
+                            f"{min(v):.1f} |\n")
         print("wrote", dst)
     pmc = {}
     for d in sorted(glob.glob(os.path.join(OUT, f"pmc_{tag}_*"))):

@@ -91,3 +91,37 @@ def small_library(start: int, n: int, seed: int = LIB_SEED, **kw):
 def sampled_library(start: int, n: int, seed: int = LIB_SEED, **kw):
     """configs[2]: files > 100 KiB, sampled cas_id."""
     return library(start, n, kw.pop("n_total", start + n), small_frac=0.0, edge=False, seed=seed, **kw)
+
+
+def sample_windows(size: int):
+    """(file offset, length) of the byte windows generate_cas_id reads from a file of
+    `size` bytes, in message order (cas.rs:27-58): the whole file, or head / 4 samples /
+    tail."""
+    if size <= SMALL_MAX:
+        return [(0, size)]
+    jump = (size - 2 * 8192) // 4
+    return [(0, 8192)] + [(8192 + k * jump, 10240) for k in range(4)] + [(size - 8192, 8192)]
+
+
+def write_files(directory: str, sizes, staged: np.ndarray, extents: np.ndarray, prefix: str = "f"):
+    """Materialise synthetic files from their staged cas messages: a whole-content file is
+    its message minus the 8-byte header; a sampled file is written sparse (ftruncate to
+    its size, then only the windows generate_cas_id reads), so multi-GB files cost only
+    their 56 KiB of sampled bytes.  Returns the paths."""
+    import os
+    paths = []
+    for i, size in enumerate(np.asarray(sizes, np.uint64).tolist()):
+        p = os.path.join(directory, f"{prefix}{i:07d}")
+        off = int(extents["msg_offset"][i]) + 8
+        fd = os.open(p, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        try:
+            if size > SMALL_MAX:
+                os.ftruncate(fd, size)
+            for fo, ln in sample_windows(size):
+                if ln:
+                    os.pwrite(fd, staged[off:off + ln].tobytes(), fo)
+                off += ln
+        finally:
+            os.close(fd)
+        paths.append(p)
+    return paths

@@ -175,3 +175,25 @@ def test_c_oracle_simd_multichunk(oracle_native, level):
         d = rng.integers(0, 256, n + 64, dtype=np.uint8)
         want = b3.blake3(d[:n].tobytes()) if n < 5000 else oracle_native.blake3(d[:n].tobytes())
         assert oracle_native.checksums_simd(d, [0], [n], simd=level)[0].tobytes() == want, n
+
+
+def test_c_oracle_file_backed_reads(oracle_native, tmp_path):
+    """The reference's read schedule from files (cas.rs:27-58) equals the staged path;
+    missing and short files map to IO_ERROR(ENOENT) and SHORT_READ."""
+    from spacedrive_amd import synth
+    from spacedrive_amd.device import stage_plan
+    sizes = np.array([1, 1016, 1017, 102400, 102401, 555555, (1 << 32) + 1, 3 << 20], np.uint64)
+    cids = np.arange(40, 40 + len(sizes), dtype=np.uint64)
+    twins = np.zeros(len(sizes), np.uint32)
+    twins[-1] = 5
+    ext, total = stage_plan(sizes)
+    buf = oracle_native.stage_synth(sizes, cids, twins, ext["msg_offset"], total)
+    paths = synth.write_files(str(tmp_path), sizes, buf, ext)
+    want = oracle_native.cas_ids_synth(sizes, cids, twins)
+    for simd, nt in ((0, 1), (-1, 3)):
+        got, st = oracle_native.cas_ids_files(paths, sizes, nthreads=nt, simd=simd)
+        assert (st == 0).all(), st
+        assert np.array_equal(got, want)
+    got, st = oracle_native.cas_ids_files([str(tmp_path / "missing"), paths[5]], [10, 555555 + 9000])
+    assert st[0] & 0xFFFF == 2 and st[0] >> 16 == 2  # ENOENT
+    assert st[1] == 3  # read_exact past EOF
