@@ -52,13 +52,17 @@ def parse():
     p.add_argument("--checksum-steps", type=int, default=5)
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target seconds per CPU-baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--whole-variant", type=int, default=1,
-                   help="0 = fused launch; 1 = separate sampled / whole-leaf / whole-tree kernels (default)")
+    p.add_argument("--whole-variant", type=int, default=3,
+                   help="0/4 = fused launch; 1 = separate sampled / whole-leaf / whole-tree kernels; 3 = separate "
+                        "sampled / prefetching pair-leaf / pair-tree kernels (default); see sd_cas.h")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (rehearsal)")
     p.add_argument("--share-gpu", action="store_true", help="map every rank onto the visible GPUs (rehearsal)")
     p.add_argument("--config-files", type=int, default=1_000_000,
                    help="N=1 only: files of the configs[1] (small) and configs[2] (sampled) kernel legs; 0 = skip")
     p.add_argument("--config-reps", type=int, default=5)
+    p.add_argument("--file-backed-files", type=int, default=20000,
+                   help="N=1 only: time the drop-in from files on disk (pread stager + sd_cas_ids) on this many "
+                        "files of the shard, beside the reference's read schedule on the CPU; 0 = skip")
     p.add_argument("--host-staged-files", type=int, default=0,
                    help="N=1 only: also time the PCIe-inclusive drop-in path on this many files (DESIGN.md)")
     return p.parse_args()
@@ -179,12 +183,104 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
            "msg_GBps": b.msg_bytes / (ms * 1e-3) / 1e9, "compressions": b.compressions,
            "valu_frac": valu / 1e12 / VALU_PEAK_TOPS,
            "valu_frac_of_measured_peak": valu / valu_peak if valu_peak else None,
-           "kernels": ["k_cas_sampled"] if which == "sampled" else ["k_whole_leaf", "k_whole_tree"],
+           "kernels": ["k_cas_sampled"] if which == "sampled" else ["k_whole_pair_leaf", "k_whole_tree"],
            "deterministic": deterministic}
     del d_staged, h0, h1, b
     torch.cuda.empty_cache()
     assert deterministic, which
     return res
+
+
+def _fs_type(path: str) -> str:
+    best, fstype = "", "?"
+    try:
+        for line in open("/proc/mounts"):
+            parts = line.split()
+            if len(parts) > 2 and path.startswith(parts[1]) and len(parts[1]) > len(best):
+                best, fstype = parts[1], parts[2]
+    except OSError:
+        pass
+    return fstype
+
+
+def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool):
+    """The drop-in path from files on disk, as identifier_job_step would drive it
+    (file_identifier/mod.rs:107-134): the first k files of this shard are written to a
+    scratch directory (sampled files sparse: only the windows cas.rs reads are
+    materialised), then timed end to end -- stage (sd_cas_stage_files: head / 4 samples /
+    tail by pread on 16 threads into pinned memory) + sd_cas_ids (H2D, kernels, D2H, hex)
+    -- and, as the CPU baseline, the reference's own read schedule (open, read_exact,
+    seek; cas.rs:27-58) + the SIMD C restatement on 1 and 16 threads.  Both read from
+    the page cache (files just written).  The two outputs are asserted equal."""
+    import ctypes
+    import shutil
+    import tempfile
+    import spacedrive_amd as sd
+    from spacedrive_amd import synth
+    from spacedrive_amd._native import check, lib
+    k = min(k, len(sizes))
+    sub_sizes = np.ascontiguousarray(sizes[:k])
+    sub_ext, total = sd.stage_plan(sub_sizes)
+    nbytes = int(ext["msg_offset"][k - 1]) + int(ext["msg_len"][k - 1])
+    host = d_staged[:nbytes].cpu().numpy()  # messages in the shard layout (same offsets)
+    base = "/dev/shm"
+    try:
+        st = os.statvfs(base)
+        if st.f_bavail * st.f_frsize < 4 * nbytes:
+            base = None
+    except OSError:
+        base = None
+    d = tempfile.mkdtemp(prefix="sd_fb_", dir=base)
+    try:
+        t0 = time.perf_counter()
+        paths = synth.write_files(d, sub_sizes, host, ext[:k])
+        write_s = time.perf_counter() - t0
+        L = lib()
+        arr = (ctypes.c_char_p * k)(*[os.fsencode(p) for p in paths])
+        pin = ctypes.c_void_p()
+        check(L.sd_cas_host_alloc(ctx.handle, total, ctypes.byref(pin)))
+        out = ctypes.create_string_buffer(17 * k)
+        status = np.zeros(k, np.int32)
+        threads = 16
+        runs = []
+        try:
+            for _ in range(3):  # first run warms the stager's threads and the context's slots
+                status[:] = 0
+                t0 = time.perf_counter()
+                check(L.sd_cas_stage_files(arr, sub_ext.ctypes.data, k, pin, status.ctypes.data, threads))
+                t1 = time.perf_counter()
+                check(L.sd_cas_ids(ctx.handle, pin, total, sub_ext.ctypes.data, k, out, status.ctypes.data))
+                t2 = time.perf_counter()
+                runs.append((t1 - t0, t2 - t1))
+        finally:
+            L.sd_cas_host_free(ctx.handle, pin)
+        assert (status == 0).all(), np.unique(status)
+        stage_s = min(r[0] for r in runs[1:])
+        hash_s = min(r[1] for r in runs[1:])
+        e2e_s = min(r[0] + r[1] for r in runs[1:])
+        gpu_ids = [out.raw[17 * i:17 * i + 16].decode() for i in range(k)]
+        res = {"files": k, "dir_fs": _fs_type(d), "write_s": write_s,
+               "message_bytes": int(sub_ext["msg_len"].astype(np.int64).sum()),
+               "gpu": {"files_per_s": k / e2e_s, "stage_ms": stage_s * 1e3, "hash_ms": hash_s * 1e3,
+                       "stage_threads": threads,
+                       "note": "sd_cas_stage_files (pread into pinned memory) + sd_cas_ids (H2D + kernels + "
+                               "D2H + hex), best of 2 warm runs"}}
+        if with_cpu:
+            from oracle import native
+            cpu = {}
+            for nt in (1, threads):
+                t0 = time.perf_counter()
+                got, cst = native.cas_ids_files(paths, sub_sizes, nthreads=nt, simd=-1)
+                dt = time.perf_counter() - t0
+                cpu[f"threads_{nt}"] = {"files_per_s": k / dt, "seconds": dt}
+            assert (cst == 0).all()
+            want = [got[i].tobytes().hex() for i in range(k)]
+            res["cpu_reference_schedule"] = cpu
+            res["equal_to_cpu"] = want == gpu_ids
+            assert res["equal_to_cpu"], "file-backed GPU cas_ids differ from the CPU restatement"
+        return res
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def main():
@@ -225,7 +321,7 @@ def main():
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     from spacedrive_amd._native import lib
     lib().sd_cas_set_tuning(b"whole_variant", args.whole_variant)
-    split = args.whole_variant == 1  # separate launches: the dominant kernel is timed on its own
+    split = args.whole_variant in (1, 3, 5)  # separate launches: the dominant kernel is timed on its own
 
     def step(k=None):
         if k is not None:
@@ -234,7 +330,7 @@ def main():
             batch.run_part(1, d_staged, d_hash, stream)  # k_cas_sampled
             if k is not None:
                 ev[k][1].record(stream)
-            batch.run_part(2, d_staged, d_hash, stream)  # k_whole_leaf + k_whole_tree
+            batch.run_part(2, d_staged, d_hash, stream)  # whole-file leaf + tree kernels
         else:
             batch.run(d_staged, d_hash, stream)
             if k is not None:
@@ -294,7 +390,9 @@ def main():
     dom_gbps = dom_bytes / (dom_ms * 1e-3) / 1e9
     hash_bytes = batch.msg_bytes + 32 * n
     hash_valu = batch.compressions * 672 / (hash_ms * 1e-3)
-    phase = ["k_cas_mixed"] if args.whole_variant == 0 else ["k_cas_sampled", "k_whole_leaf", "k_whole_tree"]
+    phase = {0: ["k_cas_mixed"], 4: ["k_cas_mixed"], 1: ["k_cas_sampled", "k_whole_leaf", "k_whole_tree"],
+             5: ["k_cas_sampled", "k_whole_pair_leaf", "k_whole_forest"]}.get(
+        args.whole_variant, ["k_cas_sampled", "k_whole_pair_leaf", "k_whole_tree"])
     traffic = pmc_traffic(dom_kernel) if split else pmc_traffic(phase)
 
     out = {
@@ -328,6 +426,9 @@ def main():
     }
     if rank == 0 and world == 1 and args.host_staged_files > 0:
         out["host_staged"] = host_staged(ctx, ext, d_staged, batch, args.host_staged_files, dev)
+    if rank == 0 and world == 1 and args.file_backed_files > 0:
+        out["file_backed"] = file_backed(ctx, sizes, ext, d_staged, args.file_backed_files,
+                                         with_cpu=not args.no_cpu_baseline)
     del d_staged, recs, rep, owners
     torch.cuda.empty_cache()
 
@@ -372,6 +473,10 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sizes, cids, twins, args.cpu_seconds)
+        if "cpu_reference_schedule" in out.get("file_backed", {}):
+            out["cpu_baseline"]["file_backed"] = dict(out["file_backed"]["cpu_reference_schedule"],
+                                                      files=out["file_backed"]["files"],
+                                                      note="reference read schedule from files (page cache)")
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -195,9 +195,11 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
 /* Process-wide kernel-variant knobs for A/B measurement (results are identical for
  * every value): "sampled_variant" = 10*U + prefetch with U in {1,2,4} chunks per lane
  * (default 21); "whole_variant" 0 = one fused launch (sampled workgroups + whole-file
- * groups with LDS trees), 1 = separate sampled / whole-leaf / whole-tree kernels
- * (default), 2 = whole-leaf, then the sampled kernel beside the whole-tree kernel on a
- * batch-internal side stream (joined back into `stream`); "checksum_variant" (default 0). */
+ * groups with LDS trees), 1 = separate sampled / whole-leaf / whole-tree kernels, 2 = whole-leaf, then the sampled kernel beside the whole-tree kernel on a
+ * batch-internal side stream (joined back into `stream`), 3 = sampled kernel + prefetching
+ * chunk-pair leaf + tree over pair nodes (default), 4 = variant 0 with prefetching chunk-pair leaves,
+ * 5 = variant 3 with the pair-node trees merged level-wise in LDS (k_whole_forest);
+ * "checksum_variant" (default 0). */
 int sd_cas_set_tuning(const char* key, int value);
 /* Read-only probe over d_buf[0, bytes) (bytes a multiple of 4096) for calibrating the
  * PMC byte counters on this kernel family's access patterns: pattern 0 = coalesced

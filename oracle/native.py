@@ -46,6 +46,8 @@ def lib():
         L.sdo_checksums_simd.restype = I
         L.sdo_cas_ids_files.argtypes = [P, P, U64, P, P, I, I]
         L.sdo_cas_ids_files.restype = I
+        L.sdo_checksum_synth_mt.argtypes = [U64, U64, ctypes.c_uint32, I, I, P]
+        L.sdo_checksum_synth_mt.restype = I
         L.sdo_simd_level.argtypes = [I]
         L.sdo_simd_level.restype = I
         _lib = L
@@ -101,6 +103,13 @@ def cas_ids_files(paths, sizes, nthreads: int = 1, simd: int = -1):
     status = np.zeros(n, np.int32)
     lib().sdo_cas_ids_files(arr, _p(sizes), n, _p(out), _p(status), nthreads, simd)
     return out, status
+
+
+def checksum_synth_mt(size: int, cid: int, twin: int = 0, nthreads: int = 8, simd: int = -1) -> bytes:
+    """Full BLAKE3 of one synthetic file, chunk-parallel on nthreads (multi-GiB files)."""
+    out = ctypes.create_string_buffer(32)
+    lib().sdo_checksum_synth_mt(size, cid, twin, nthreads, simd, out)
+    return out.raw
 
 
 def simd_level(requested: int = -1) -> int:

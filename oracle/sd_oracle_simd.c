@@ -319,3 +319,90 @@ void sdo_blake3_simd(const uint8_t* data, uint64_t len, uint8_t out[32], int lvl
     sdo_compress_words(IV_, m, 0, 64, FS_PARENT | FS_ROOT, o);
     memcpy(out, o, 32);
 }
+
+/* ----------------------------------------------- multi-threaded checksum of one file */
+/* Full BLAKE3 (hash.rs:10-24) of one synthetic file of `size` bytes (content cid/twin of
+ * sdo_synth_fill) on nthreads threads: the threads generate 1 MiB windows and hash their
+ * chunks with hash_many into one CV array, then the CVs merge level-wise as in
+ * sdo_blake3_simd.  Test infrastructure for files of several GiB, where the streaming
+ * scalar restatement (sdo_checksums_synth) takes minutes. */
+#include <pthread.h>
+#include <stdatomic.h>
+void sdo_synth_fill(uint64_t cid, uint32_t twin, uint64_t offset, uint64_t length, uint8_t* out);
+
+typedef struct {
+    uint64_t size, C, cid;
+    uint32_t twin;
+    int lvl;
+    uint8_t* cvs;
+    atomic_ullong next;
+} mt_job;
+
+static void* mt_worker(void* arg) {
+    mt_job* j = (mt_job*)arg;
+    uint8_t* buf = (uint8_t*)malloc(1u << 20);
+    const uint8_t* ptrs[64];
+    for (;;) {
+        uint64_t w = atomic_fetch_add(&j->next, 1);
+        uint64_t c_begin = w * 1024;
+        if (c_begin >= j->C) break;
+        uint64_t off = c_begin * 1024;
+        uint64_t n = j->size - off < (1u << 20) ? j->size - off : (1u << 20);
+        sdo_synth_fill(j->cid, j->twin, off, n, buf);
+        uint64_t c_end = c_begin + 1024 < j->C ? c_begin + 1024 : j->C;
+        uint64_t full_end = c_end == j->C ? j->C - 1 : c_end; /* the file's last chunk: scalar */
+        for (uint64_t c0 = c_begin; c0 < full_end; c0 += 64) {
+            int k = (int)((full_end - c0) < 64 ? (full_end - c0) : 64);
+            for (int i = 0; i < k; i++) ptrs[i] = buf + 1024 * (c0 + i - c_begin);
+            hash_many(j->lvl, ptrs, k, 16, c0, 1, 0, FS_CHUNK_START, FS_CHUNK_END, j->cvs + 32 * c0);
+        }
+        if (c_end == j->C) {
+            uint32_t cv[8];
+            scalar_chunk(buf + 1024 * (j->C - 1 - c_begin), (uint32_t)(j->size - 1024 * (j->C - 1)), j->C - 1, 0, cv);
+            memcpy(j->cvs + 32 * (j->C - 1), cv, 32);
+        }
+    }
+    free(buf);
+    return NULL;
+}
+
+int sdo_checksum_synth_mt(uint64_t size, uint64_t cid, uint32_t twin, int nthreads, int simd, uint8_t out[32]) {
+    int lvl = sdo_simd_level(simd < 0 ? -1 : simd);
+    if (lvl == 0 || size <= 1024) { /* scalar path or a single chunk */
+        uint8_t* b = (uint8_t*)malloc(size ? size : 1);
+        sdo_synth_fill(cid, twin, 0, size, b);
+        void sdo_blake3(const uint8_t*, size_t, uint8_t*);
+        sdo_blake3(b, size, out);
+        free(b);
+        return lvl;
+    }
+    mt_job j;
+    j.size = size; j.C = (size + 1023) / 1024; j.cid = cid; j.twin = twin; j.lvl = lvl;
+    j.cvs = (uint8_t*)malloc(32 * j.C);
+    atomic_store(&j.next, 0);
+    if (nthreads < 1) nthreads = 1;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, mt_worker, &j);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th);
+    const uint8_t* ptrs[64];
+    uint64_t nodes = j.C;
+    while (nodes > 2) {
+        uint64_t P = nodes / 2;
+        for (uint64_t p0 = 0; p0 < P; p0 += 64) {
+            int k = (int)((P - p0) < 64 ? (P - p0) : 64);
+            uint8_t tmp[64 * 32];
+            for (int i = 0; i < k; i++) ptrs[i] = j.cvs + 64 * (p0 + i);
+            hash_many(lvl, ptrs, k, 1, 0, 0, FS_PARENT, 0, 0, tmp);
+            memcpy(j.cvs + 32 * p0, tmp, 32 * (size_t)k);
+        }
+        if (nodes & 1) memmove(j.cvs + 32 * P, j.cvs + 32 * (nodes - 1), 32);
+        nodes = P + (nodes & 1);
+    }
+    uint32_t m[16], o[16];
+    memcpy(m, j.cvs, 64);
+    sdo_compress_words(IV_, m, 0, 64, FS_PARENT | FS_ROOT, o);
+    memcpy(out, o, 32);
+    free(j.cvs);
+    return lvl;
+}

@@ -211,4 +211,53 @@ __device__ __forceinline__ void full_chunks_cv(uint32_t (&out)[8], const uint8_t
     }
 }
 
+// 64-byte block q of a message group whose last block (lastq) holds `tail` bytes (1..64)
+__device__ __forceinline__ void load_block_q(uint32_t (&m)[16], const uint8_t* __restrict__ p, uint32_t q,
+                                             uint32_t lastq, uint32_t tail) {
+    if (q == lastq && tail < 64u) load_block_partial(m, p + 64u * q, tail);
+    else load_block(m, p + 64u * q);
+}
+
+// Chaining value of an aligned chunk PAIR (c0, c0 + 1) of a message: `glen` (1..2048)
+// bytes at p, i.e. chunk c0 is full when glen > 1024.  The pair's blocks are consecutive,
+// so the message streams through two register buffers with block q+1 loading while q
+// compresses (as full_chunks_cv does for full chunks).  root: the pair is the whole
+// message -- ROOT goes on the last block of a single chunk, or on the pair's parent.
+__device__ __forceinline__ void pair_cv(uint32_t (&out)[8], const uint8_t* __restrict__ p, uint32_t glen,
+                                        uint64_t c0, bool root) {
+    const uint32_t nq = (glen + 63u) >> 6;
+    const uint32_t lastq = nq - 1u, tail = glen - 64u * lastq;
+    const bool two = glen > CHUNK_LEN;
+    uint32_t cv[8], held[8], ma[16], mb[16];
+    set_iv(cv);
+    load_block_q(ma, p, 0u, lastq, tail);
+#define SD_PAIR_STEP(Q, M)                                                                               \
+    do {                                                                                                 \
+        const uint32_t b_ = (Q) & 15u, u_ = (Q) >> 4;                                                    \
+        const bool endc_ = b_ == 15u || (Q) == lastq;                                                    \
+        const uint32_t fl_ = (b_ == 0u ? CHUNK_START : 0u) | (endc_ ? CHUNK_END : 0u) |                  \
+                             (((Q) == lastq && root && !two) ? ROOT : 0u);                                \
+        const uint64_t ctr_ = c0 + u_;                                                                   \
+        compress(cv, M, (uint32_t)ctr_, (uint32_t)(ctr_ >> 32), (Q) == lastq ? tail : BLOCK_LEN, fl_);   \
+        if (b_ == 15u && u_ == 0u && two) {                                                              \
+            _Pragma("unroll") for (int i_ = 0; i_ < 8; i_++) held[i_] = cv[i_];                          \
+            set_iv(cv);                                                                                  \
+        }                                                                                                \
+    } while (0)
+#pragma unroll 1
+    for (uint32_t q = 0; q < nq; q += 2) {
+        if (q + 1u < nq) load_block_q(mb, p, q + 1u, lastq, tail);
+        SD_PAIR_STEP(q, ma);
+        if (q + 1u >= nq) break;
+        if (q + 2u < nq) load_block_q(ma, p, q + 2u, lastq, tail);
+        SD_PAIR_STEP(q + 1u, mb);
+    }
+#undef SD_PAIR_STEP
+    if (two) parent(out, held, cv, root ? ROOT : 0u);
+    else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) out[i] = cv[i];
+    }
+}
+
 }  // namespace sdb3

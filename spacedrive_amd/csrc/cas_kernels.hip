@@ -205,46 +205,14 @@ __device__ __forceinline__ uint32_t find_owner(const uint32_t* pref, uint32_t cn
     return lo;
 }
 
-__device__ __forceinline__ void whole_wg(uint32_t g, const uint8_t* __restrict__ staged,
-                                         const sd_extent* __restrict__ ext, const uint32_t* __restrict__ order,
-                                         const uint2* __restrict__ groups, uint32_t* __restrict__ out,
-                                         whole_lds& sh) {
-    const uint2 grp = groups[g];  // (first index in the sorted order, file count)
-    const uint32_t cnt = grp.y, t = threadIdx.x;
-    uint32_t L = 0;
-    if (t < cnt) {
-        const uint32_t fl = order[grp.x + t];
-        const uint32_t C = (ext[fl].msg_len + CHUNK_LEN - 1) / CHUNK_LEN;  // msg_len >= 8
-        L = (C + 1) / 2;
-        sh.file[t] = fl;
-        sh.nodes[t] = L;
-    }
-    uint32_t lanes;
-    const uint32_t o = block_exscan(L, sh.wsum, lanes);
-    if (t < cnt) sh.off[t] = o;
-    __syncthreads();
-    if (t < lanes) {  // leaf: one aligned chunk pair
-        const uint32_t f = find_owner(sh.off, cnt, t);
-        const uint32_t fl = sh.file[f];
-        const sd_extent e = ext[fl];
-        const uint32_t C = (e.msg_len + CHUNK_LEN - 1) / CHUNK_LEN;
-        const uint32_t c0 = 2 * (t - sh.off[f]);
-        const uint8_t* p = staged + e.msg_offset + (size_t)c0 * CHUNK_LEN;
-        const uint32_t rem0 = e.msg_len - c0 * CHUNK_LEN;
-        uint32_t res[8];
-        chunk_cv(res, p, rem0 < CHUNK_LEN ? rem0 : CHUNK_LEN, c0, C == 1);
-        if (c0 + 1 < C) {
-            uint32_t cv1[8], cv0[8];
-            const uint32_t rem1 = rem0 - CHUNK_LEN;
-#pragma unroll
-            for (int i = 0; i < 8; i++) cv0[i] = res[i];
-            chunk_cv(cv1, p + CHUNK_LEN, rem1 < CHUNK_LEN ? rem1 : CHUNK_LEN, c0 + 1, false);
-            parent(res, cv0, cv1, C == 2 ? ROOT : 0u);
-        }
-        if (C <= 2) store_cv(out + (size_t)fl * 8, res);
-        else store_cv(sh.cvs[t], res);
-    }
-    __syncthreads();
+// Level-wise merge of a forest held in LDS: local file f (f < cnt, longest first) has
+// sh.nodes[f] CVs at sh.cvs[sh.off[f] ...].  Parents of a level are assigned compactly: a
+// block scan of the per-file parent counts, and a binary search from lane to file (files
+// with parents left are a prefix, since node counts shrink monotonically with length).
+// ROOT goes on each file's final parent, whose CV is the hash written to out[file].
+// Every thread of the workgroup must call it.
+__device__ __forceinline__ void lds_forest(whole_lds& sh, uint32_t cnt, uint32_t* __restrict__ out) {
+    const uint32_t t = threadIdx.x;
     uint32_t maxn = sh.nodes[0];  // local file 0 is the longest
 #pragma unroll 1
     while (maxn > 1) {
@@ -290,25 +258,73 @@ __device__ __forceinline__ void whole_wg(uint32_t g, const uint8_t* __restrict__
     }
 }
 
+template <bool PAIRPF>
+__device__ __forceinline__ void whole_wg(uint32_t g, const uint8_t* __restrict__ staged,
+                                         const sd_extent* __restrict__ ext, const uint32_t* __restrict__ order,
+                                         const uint2* __restrict__ groups, uint32_t* __restrict__ out,
+                                         whole_lds& sh) {
+    const uint2 grp = groups[g];  // (first index in the sorted order, file count)
+    const uint32_t cnt = grp.y, t = threadIdx.x;
+    uint32_t L = 0;
+    if (t < cnt) {
+        const uint32_t fl = order[grp.x + t];
+        const uint32_t C = (ext[fl].msg_len + CHUNK_LEN - 1) / CHUNK_LEN;  // msg_len >= 8
+        L = (C + 1) / 2;
+        sh.file[t] = fl;
+        sh.nodes[t] = L;
+    }
+    uint32_t lanes;
+    const uint32_t o = block_exscan(L, sh.wsum, lanes);
+    if (t < cnt) sh.off[t] = o;
+    __syncthreads();
+    if (t < lanes) {  // leaf: one aligned chunk pair
+        const uint32_t f = find_owner(sh.off, cnt, t);
+        const uint32_t fl = sh.file[f];
+        const sd_extent e = ext[fl];
+        const uint32_t C = (e.msg_len + CHUNK_LEN - 1) / CHUNK_LEN;
+        const uint32_t c0 = 2 * (t - sh.off[f]);
+        const uint8_t* p = staged + e.msg_offset + (size_t)c0 * CHUNK_LEN;
+        const uint32_t rem0 = e.msg_len - c0 * CHUNK_LEN;
+        uint32_t res[8];
+        if (PAIRPF) {
+            pair_cv(res, p, rem0 < 2 * CHUNK_LEN ? rem0 : 2 * CHUNK_LEN, c0, C <= 2);
+        } else {
+            chunk_cv(res, p, rem0 < CHUNK_LEN ? rem0 : CHUNK_LEN, c0, C == 1);
+            if (c0 + 1 < C) {
+                uint32_t cv1[8], cv0[8];
+                const uint32_t rem1 = rem0 - CHUNK_LEN;
+#pragma unroll
+                for (int i = 0; i < 8; i++) cv0[i] = res[i];
+                chunk_cv(cv1, p + CHUNK_LEN, rem1 < CHUNK_LEN ? rem1 : CHUNK_LEN, c0 + 1, false);
+                parent(res, cv0, cv1, C == 2 ? ROOT : 0u);
+            }
+        }
+        if (C <= 2) store_cv(out + (size_t)fl * 8, res);
+        else store_cv(sh.cvs[t], res);
+    }
+    __syncthreads();
+    lds_forest(sh, cnt, out);
+}
+
 // One launch for a whole cas batch: workgroups [0, S) hash sampled files (8U each),
 // workgroups [S, S + G) hash whole-file groups.  The long sampled workgroups are
 // dispatched first and the shorter whole-file ones fill the tail.
-template <int U, bool PF>
+template <int U>
 union mixed_lds {
     sampled_lds<U> s;
     whole_lds w;
 };
 
-template <int U, bool PF>
+template <int U, bool PF, bool PAIRPF>
 __global__ __launch_bounds__(S_THREADS) void k_cas_mixed(const uint8_t* __restrict__ staged,
                                                          const sd_extent* __restrict__ ext,
                                                          const uint32_t* __restrict__ sidx, uint32_t n_sampled,
                                                          uint32_t S, const uint32_t* __restrict__ order,
                                                          const uint2* __restrict__ groups,
                                                          uint32_t* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) mixed_lds<U, PF> sh;
+    __shared__ __attribute__((aligned(16))) mixed_lds<U> sh;
     if (blockIdx.x < S) sampled_wg<U, PF>(blockIdx.x, staged, ext, sidx, n_sampled, out, sh.s);
-    else whole_wg(blockIdx.x - S, staged, ext, order, groups, out, sh.w);
+    else whole_wg<PAIRPF>(blockIdx.x - S, staged, ext, order, groups, out, sh.w);
 }
 
 // ------------------------------------------------------------------ whole-file cas
@@ -341,6 +357,70 @@ __global__ __launch_bounds__(256) void k_whole_leaf(const uint8_t* __restrict__ 
     chunk_cv(cv, staged + e.msg_offset + (size_t)c * CHUNK_LEN, len, c, C == 1);
     if (C == 1) store_cv(out + (size_t)file * 8, cv);
     else store_cv(cvbuf + (size_t)g * 8, cv);
+}
+
+// Pair leaf: one lane per aligned chunk PAIR of a whole-file message (pair_prefix[k] =
+// first pair of sorted file k, hint[w] = sorted file holding pair 64*w), prefetching
+// block q+1 while q compresses and merging the pair in-lane.  Messages of <= 2 chunks end
+// here (ROOT inside the lane); longer ones leave one CV per pair for k_whole_tree, which
+// then merges half as many nodes as after the one-chunk-per-lane leaf.
+__global__ __launch_bounds__(256) void k_whole_pair_leaf(const uint8_t* __restrict__ staged,
+                                                         const sd_extent* __restrict__ ext,
+                                                         const uint32_t* __restrict__ order,
+                                                         const uint32_t* __restrict__ pair_prefix,
+                                                         const uint32_t* __restrict__ hint, uint32_t nw,
+                                                         uint32_t total_pairs, uint32_t* __restrict__ cvbuf,
+                                                         uint32_t* __restrict__ out) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total_pairs) return;
+    const uint32_t w = g >> 6;
+    uint32_t lo = hint[w], hi = hint[w + 1];
+    if (hi > nw - 1) hi = nw - 1;
+    while (lo < hi) {  // largest k in [lo, hi] with pair_prefix[k] <= g
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (pair_prefix[mid] <= g) lo = mid; else hi = mid - 1;
+    }
+    const uint32_t k = lo;
+    const uint32_t file = order[k];
+    const uint32_t j = g - pair_prefix[k];
+    const bool root = pair_prefix[k + 1] - pair_prefix[k] == 1u;  // <= 2 chunks
+    const sd_extent e = ext[file];
+    const uint32_t rem = e.msg_len - j * 2u * CHUNK_LEN;
+    uint32_t cv[8];
+    pair_cv(cv, staged + e.msg_offset + (size_t)j * 2u * CHUNK_LEN, rem < 2u * CHUNK_LEN ? rem : 2u * CHUNK_LEN,
+            2ull * j, root);
+    if (root) store_cv(out + (size_t)file * 8, cv);
+    else store_cv(cvbuf + (size_t)g * 8, cv);
+}
+
+// Forest merge after the pair leaf: workgroup g takes consecutive multi-pair files
+// (groups[g] = (first sorted index, count), their pair nodes summing to <= 448), copies
+// their node CVs -- one contiguous cvbuf range -- into LDS and merges every file's tree
+// level-wise with all lanes (lds_forest): the critical path is log2(nodes) parents
+// instead of k_whole_tree's nodes - 1 serial ones per lane.
+__global__ __launch_bounds__(W_THREADS) void k_whole_forest(const uint32_t* __restrict__ order,
+                                                            const uint32_t* __restrict__ pair_prefix,
+                                                            const uint2* __restrict__ groups,
+                                                            const uint32_t* __restrict__ cvbuf,
+                                                            uint32_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) whole_lds sh;
+    const uint2 grp = groups[blockIdx.x];
+    const uint32_t cnt = grp.y, t = threadIdx.x;
+    const uint32_t base = pair_prefix[grp.x];
+    const uint32_t total = pair_prefix[grp.x + cnt] - base;
+    if (t < cnt) {
+        const uint32_t k = grp.x + t;
+        sh.file[t] = order[k];
+        sh.nodes[t] = pair_prefix[k + 1] - pair_prefix[k];
+        sh.off[t] = pair_prefix[k] - base;
+    }
+    if (t < total) {
+        uint32_t cv[8];
+        load_cv(cv, cvbuf + (size_t)(base + t) * 8);
+        store_cv(sh.cvs[t], cv);
+    }
+    __syncthreads();
+    lds_forest(sh, cnt, out);
 }
 
 // one lane per multi-chunk file (sorted files 0..n_multi-1 all have C >= 2)
@@ -485,24 +565,51 @@ hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const
 
 hipError_t launch_cas_mixed(const uint8_t* staged, const sd_extent* ext, const uint32_t* sidx, uint32_t n_sampled,
                             const uint32_t* order, const uint2* groups, uint32_t n_groups, uint32_t* out,
-                            hipStream_t s) {
+                            hipStream_t s, bool pairpf) {
     const int v = tuning_get(SD_TUNE_SAMPLED_VARIANT);
-#define SD_LAUNCH_MIXED(U, PF)                                                                             \
+#define SD_LAUNCH_MIXED(U, PF, W)                                                                          \
     do {                                                                                                  \
         const uint32_t S = (n_sampled + 8 * U - 1) / (8 * U);                                             \
         if (S + n_groups)                                                                                 \
-            hipLaunchKernelGGL((k_cas_mixed<U, PF>), dim3(S + n_groups), dim3(S_THREADS), 0, s, staged, ext, \
-                               sidx, n_sampled, S, order, groups, out);                                   \
+            hipLaunchKernelGGL((k_cas_mixed<U, PF, W>), dim3(S + n_groups), dim3(S_THREADS), 0, s, staged, \
+                               ext, sidx, n_sampled, S, order, groups, out);                              \
     } while (0)
-    switch (v) {
-        case 10: SD_LAUNCH_MIXED(1, false); break;
-        case 11: SD_LAUNCH_MIXED(1, true); break;
-        case 20: SD_LAUNCH_MIXED(2, false); break;
-        case 40: SD_LAUNCH_MIXED(4, false); break;
-        case 41: SD_LAUNCH_MIXED(4, true); break;
-        default: SD_LAUNCH_MIXED(2, true); break;
+    if (pairpf) {
+        switch (v) {
+            case 10: SD_LAUNCH_MIXED(1, false, true); break;
+            case 11: SD_LAUNCH_MIXED(1, true, true); break;
+            case 20: SD_LAUNCH_MIXED(2, false, true); break;
+            case 40: SD_LAUNCH_MIXED(4, false, true); break;
+            case 41: SD_LAUNCH_MIXED(4, true, true); break;
+            default: SD_LAUNCH_MIXED(2, true, true); break;
+        }
+    } else {
+        switch (v) {
+            case 10: SD_LAUNCH_MIXED(1, false, false); break;
+            case 11: SD_LAUNCH_MIXED(1, true, false); break;
+            case 20: SD_LAUNCH_MIXED(2, false, false); break;
+            case 40: SD_LAUNCH_MIXED(4, false, false); break;
+            case 41: SD_LAUNCH_MIXED(4, true, false); break;
+            default: SD_LAUNCH_MIXED(2, true, false); break;
+        }
     }
 #undef SD_LAUNCH_MIXED
+    return hipGetLastError();
+}
+
+hipError_t launch_whole_forest(const uint32_t* order, const uint32_t* pair_prefix, const uint2* groups,
+                               uint32_t n_groups, const uint32_t* cvbuf, uint32_t* out, hipStream_t s) {
+    if (n_groups == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_whole_forest, dim3(n_groups), dim3(W_THREADS), 0, s, order, pair_prefix, groups, cvbuf, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_whole_pair_leaf(const uint8_t* staged, const sd_extent* ext, const uint32_t* order,
+                                  const uint32_t* pair_prefix, const uint32_t* hint, uint32_t nw, uint32_t total_pairs,
+                                  uint32_t* cvbuf, uint32_t* out, hipStream_t s) {
+    if (nw == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_whole_pair_leaf, dim3((total_pairs + 255) / 256), dim3(256), 0, s, staged, ext, order,
+                       pair_prefix, hint, nw, total_pairs, cvbuf, out);
     return hipGetLastError();
 }
 

@@ -170,7 +170,9 @@ struct sd_cas_batch {
     uint32_t total_chunks = 0;
     uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0;
     uint32_t n_groups = 0;  // whole-file groups of the fused kernel
-    DevBuf ext, sidx, order, prefix, hint, cvbuf, groups;
+    uint32_t total_pairs = 0, n_multi2 = 0;  // pair leaf: chunk pairs; files with >= 3 chunks
+    uint32_t n_groups2 = 0;                  // forest groups over the multi-pair files
+    DevBuf ext, sidx, order, prefix, hint, cvbuf, groups, prefix2, hint2, groups2;
     // variant 2: the whole-file tree kernel runs on a side stream beside the sampled kernel
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
@@ -180,8 +182,8 @@ struct sd_cas_batch {
         if (join) (void)hipEventDestroy(join);
     }
     std::vector<sd_extent> h_ext;  // host copies backing async uploads
-    std::vector<uint32_t> h_sidx, h_order, h_prefix, h_hint;
-    std::vector<uint2> h_groups;
+    std::vector<uint32_t> h_sidx, h_order, h_prefix, h_hint, h_prefix2, h_hint2;
+    std::vector<uint2> h_groups, h_groups2;
 };
 
 struct ck_pass {
@@ -289,6 +291,44 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
             hint[w] = k;
         }
     }
+    // the same in units of aligned chunk pairs (pair leaf kernel)
+    {
+        std::vector<uint32_t>& p2 = b->h_prefix2;
+        p2.assign(b->n_whole + 1, 0);
+        uint32_t tp = 0;
+        b->n_multi2 = 0;
+        for (uint32_t k = 0; k < b->n_whole; k++) {
+            p2[k] = tp;
+            const uint32_t C = msg_chunks(ext[order[k]].msg_len);
+            tp += (C + 1) / 2;
+            if (C >= 3) b->n_multi2 = k + 1;
+        }
+        p2[b->n_whole] = tp;
+        b->total_pairs = tp;
+        // forest groups: consecutive multi-pair files whose pair nodes fit 448 lanes
+        b->h_groups2.clear();
+        uint32_t first = 0, lanes = 0;
+        for (uint32_t k = 0; k < b->n_multi2; k++) {
+            const uint32_t L = p2[k + 1] - p2[k];
+            if (lanes + L > 448) {
+                b->h_groups2.push_back(make_uint2(first, k - first));
+                first = k;
+                lanes = 0;
+            }
+            lanes += L;
+        }
+        if (b->n_multi2) b->h_groups2.push_back(make_uint2(first, b->n_multi2 - first));
+        b->n_groups2 = (uint32_t)b->h_groups2.size();
+        const uint32_t W2 = (tp + 63) / 64;
+        std::vector<uint32_t>& h2 = b->h_hint2;
+        h2.assign(W2 + 1, 0);
+        uint32_t k = 0;
+        for (uint32_t w = 0; w <= W2; w++) {
+            const uint64_t c = std::min<uint64_t>((uint64_t)w * 64, tp ? tp - 1 : 0);
+            while (k + 1 < b->n_whole && p2[k + 1] <= c) k++;
+            h2[w] = k;
+        }
+    }
     // whole-file groups for the fused kernel: consecutive (length-sorted) files whose
     // chunk pairs fit one 448-lane workgroup
     b->h_groups.clear();
@@ -313,6 +353,9 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
     b->order.upload(order, stream);
     b->prefix.upload(prefix, stream);
     b->hint.upload(hint, stream);
+    b->prefix2.upload(b->h_prefix2, stream);
+    b->hint2.upload(b->h_hint2, stream);
+    b->groups2.upload(b->h_groups2, stream);
     b->cvbuf.ensure((size_t)b->total_chunks * 32);
 }
 
@@ -325,10 +368,30 @@ sd_cas_batch* build_cas_batch(const sd_extent* ext, size_t n) {
 void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_hash32, hipStream_t s,
                    int parts = SD_PART_SAMPLED | SD_PART_WHOLE) {
     uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
-    if (tuning_get(SD_TUNE_WHOLE_VARIANT) == 0) {  // one fused launch
+    const int wv = tuning_get(SD_TUNE_WHOLE_VARIANT);
+    if (wv == 0 || wv == 4) {  // one fused launch (4: prefetching pair leaves)
         HIP_CHECK(sdk::launch_cas_mixed(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(),
                                         (parts & SD_PART_SAMPLED) ? b->n_sampled : 0, b->order.as<uint32_t>(),
-                                        b->groups.as<uint2>(), (parts & SD_PART_WHOLE) ? b->n_groups : 0, out, s));
+                                        b->groups.as<uint2>(), (parts & SD_PART_WHOLE) ? b->n_groups : 0, out, s,
+                                        wv == 4));
+        return;
+    }
+    if (wv == 3 || wv == 5) {  // sampled kernel; prefetching pair leaf + tree (3) / LDS forest (5) over pair nodes
+        if (parts & SD_PART_SAMPLED)
+            HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled,
+                                              out, s));
+        if (parts & SD_PART_WHOLE) {
+            HIP_CHECK(sdk::launch_whole_pair_leaf(d_staged, b->ext.as<sd_extent>(), b->order.as<uint32_t>(),
+                                                  b->prefix2.as<uint32_t>(), b->hint2.as<uint32_t>(), b->n_whole,
+                                                  b->total_pairs, b->cvbuf.as<uint32_t>(), out, s));
+            if (wv == 3)
+                HIP_CHECK(sdk::launch_whole_tree(b->order.as<uint32_t>(), b->prefix2.as<uint32_t>(), b->n_multi2,
+                                                 b->cvbuf.as<uint32_t>(), out, s));
+            else
+                HIP_CHECK(sdk::launch_whole_forest(b->order.as<uint32_t>(), b->prefix2.as<uint32_t>(),
+                                                   b->groups2.as<uint2>(), b->n_groups2, b->cvbuf.as<uint32_t>(), out,
+                                                   s));
+        }
         return;
     }
     if (tuning_get(SD_TUNE_WHOLE_VARIANT) == 2 && (parts & SD_PART_WHOLE) && (parts & SD_PART_SAMPLED) && b->n_multi) {
@@ -525,7 +588,7 @@ int32_t stage_one(const char* path, const sd_extent& e, uint8_t* staged) {
 
 // ------------------------------------------------------------------ tuning knobs
 #include <atomic>
-static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{21}, {1}, {0}};
+static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{21}, {3}, {0}};
 int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
 
 // ============================================================================ C ABI

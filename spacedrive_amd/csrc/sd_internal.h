@@ -31,7 +31,12 @@ hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const
                               uint32_t* out, hipStream_t s);
 hipError_t launch_cas_mixed(const uint8_t* staged, const sd_extent* ext, const uint32_t* sidx, uint32_t n_sampled,
                             const uint32_t* order, const uint2* groups, uint32_t n_groups, uint32_t* out,
-                            hipStream_t s);
+                            hipStream_t s, bool pairpf);
+hipError_t launch_whole_forest(const uint32_t* order, const uint32_t* pair_prefix, const uint2* groups,
+                               uint32_t n_groups, const uint32_t* cvbuf, uint32_t* out, hipStream_t s);
+hipError_t launch_whole_pair_leaf(const uint8_t* staged, const sd_extent* ext, const uint32_t* order,
+                                  const uint32_t* pair_prefix, const uint32_t* hint, uint32_t nw, uint32_t total_pairs,
+                                  uint32_t* cvbuf, uint32_t* out, hipStream_t s);
 hipError_t launch_whole_leaf(const uint8_t* staged, const sd_extent* ext, const uint32_t* order,
                              const uint32_t* chunk_prefix, const uint32_t* hint, uint32_t nw, uint32_t total_chunks,
                              uint32_t* cvbuf, uint32_t* out, hipStream_t s);

@@ -120,12 +120,12 @@ def test_sd_cas_ids_pipelined_windows(ctx):
             assert status[i] == 0 and raw[17 * i:17 * i + 16].decode() == h[i, :8].tobytes().hex(), i
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["fused", "split", "side-stream"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=["fused", "split", "side-stream", "pair-leaf", "fused-pair", "pair-forest"])
 def whole_variant(request):
     from spacedrive_amd._native import lib
     assert lib().sd_cas_set_tuning(b"whole_variant", request.param) == 0
     yield request.param
-    lib().sd_cas_set_tuning(b"whole_variant", 0)
+    lib().sd_cas_set_tuning(b"whole_variant", 3)  # the default
 
 
 def test_cas_exhaustive_small_sizes(ctx, oracle_native, whole_variant):
@@ -224,6 +224,19 @@ def test_checksum_sizes_vs_oracle(ctx, oracle_native):
                                          np.array(twins, np.uint32), nthreads=NT)
     bad = [lens[i] for i in range(len(lens)) if h[i].tobytes() != want[i].tobytes()]
     assert not bad, bad
+
+
+def test_checksum_multi_gib_vs_oracle(ctx, oracle_native):
+    """configs[3] sizes: a 4 GiB file exactly as bench.py hashes it (content id 10000),
+    the SURVEY.md 8(d) edge size 2^32 + 1, and an odd 5 GiB + 12345 twin -- byte offsets
+    past 2^32 and multi-level reduce passes -- against the chunk-parallel C oracle."""
+    lens = [4 << 30, (1 << 32) + 1, (5 << 30) + 12345]
+    cids, twins = [10_000, 77, 78], [0, 0, 9]
+    h = gpu_checksums(ctx, lens, cids, twins)
+    torch.cuda.empty_cache()
+    for i, L in enumerate(lens):
+        want = oracle_native.checksum_synth_mt(L, cids[i], twins[i], nthreads=NT)
+        assert h[i].tobytes() == want, L
 
 
 def test_file_api_on_disk(ctx, tmp_path, golden):

@@ -197,3 +197,13 @@ def test_c_oracle_file_backed_reads(oracle_native, tmp_path):
     got, st = oracle_native.cas_ids_files([str(tmp_path / "missing"), paths[5]], [10, 555555 + 9000])
     assert st[0] & 0xFFFF == 2 and st[0] >> 16 == 2  # ENOENT
     assert st[1] == 3  # read_exact past EOF
+
+
+def test_c_oracle_checksum_mt_equals_streaming(oracle_native):
+    """The chunk-parallel checker (used for multi-GiB GPU parity) equals the streaming
+    restatement of hash.rs:14-20 across block, chunk and 1 MiB window boundaries."""
+    for size in [0, 1, 1024, 1025, 2048, (1 << 20) - 1, 1 << 20, (1 << 20) + 1, 3 * (1 << 20) + 5, 9_999_999]:
+        want = oracle_native.checksums_synth(np.array([size], np.uint64), np.array([9], np.uint64),
+                                             np.array([3], np.uint32))[0].tobytes()
+        for nt in (1, 3):
+            assert oracle_native.checksum_synth_mt(size, 9, 3, nthreads=nt) == want, (size, nt)
