@@ -257,14 +257,27 @@ def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool):
         assert (status == 0).all(), np.unique(status)
         stage_s = min(r[0] for r in runs[1:])
         hash_s = min(r[1] for r in runs[1:])
-        e2e_s = min(r[0] + r[1] for r in runs[1:])
         gpu_ids = [out.raw[17 * i:17 * i + 16].decode() for i in range(k)]
+        # the pipelined path-based drop-in: stager pool preads window k+1 while window k
+        # is copied and hashed (sd_cas_ids_files)
+        out2 = ctypes.create_string_buffer(17 * k)
+        st2 = np.zeros(k, np.int32)
+        sz = np.ascontiguousarray(sub_sizes, np.uint64)
+        pipe = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            check(L.sd_cas_ids_files(ctx.handle, arr, sz.ctypes.data, k, out2, st2.ctypes.data, threads))
+            pipe.append(time.perf_counter() - t0)
+        assert (st2 == 0).all() and out2.raw == out.raw
+        pipe_s = min(pipe[1:])
         res = {"files": k, "dir_fs": _fs_type(d), "write_s": write_s,
                "message_bytes": int(sub_ext["msg_len"].astype(np.int64).sum()),
-               "gpu": {"files_per_s": k / e2e_s, "stage_ms": stage_s * 1e3, "hash_ms": hash_s * 1e3,
-                       "stage_threads": threads,
-                       "note": "sd_cas_stage_files (pread into pinned memory) + sd_cas_ids (H2D + kernels + "
-                               "D2H + hex), best of 2 warm runs"}}
+               "gpu": {"files_per_s": k / pipe_s, "ms": pipe_s * 1e3, "stage_threads": threads,
+                       "note": "sd_cas_ids_files: pread on the library's stager pool into pinned windows, "
+                               "overlapped with H2D + kernels + D2H + hex; best of 2 warm runs",
+                       "unpipelined": {"files_per_s": k / (stage_s + hash_s), "stage_ms": stage_s * 1e3,
+                                       "hash_ms": hash_s * 1e3,
+                                       "note": "sd_cas_stage_files then sd_cas_ids, one after the other"}}}
         if with_cpu:
             from oracle import native
             cpu = {}

@@ -112,6 +112,15 @@ int sd_cas_stage_files(const char* const* paths, const sd_extent* extents, size_
 int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes,
                const sd_extent* extents, size_t n, char* out_hex17, int32_t* status);
 
+/* Path-based drop-in batch (SURVEY.md §8(b)'s "library does pread" entry): n (path,
+ * size) pairs -> cas_ids, sizes as the caller's metadata reported them (the size is
+ * hashed as given, cas.rs:25).  The library plans the messages, preads them on a
+ * persistent pool of nthreads stager threads into pinned windows ("files_window_mb",
+ * default 32), and overlaps staging window k+1 with window k's H2D copy and kernels.
+ * status[n] (required) receives each file's sd_file_status. */
+int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n,
+                     char* out_hex17, int32_t* status, int nthreads);
+
 /* Prepared batch for device-resident data: builds the work lists for these extents once
  * (host arithmetic + one upload).  extents are host pointers. */
 int sd_cas_batch_create(sd_cas_ctx* ctx, const sd_extent* extents, size_t n, sd_cas_batch** out);
@@ -148,6 +157,19 @@ int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
  * H2D copies and the kernels.  The length hashed is the file's length at stat time. */
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65,
                       int32_t* status);
+
+/* ---------------------------------------------------------------- latency path */
+/* Single-file generate_cas_id (cas.rs:23) / file_checksum (hash.rs:10) for the
+ * reference's per-file callers -- the location watcher (core/src/location/manager/
+ * watcher/utils.rs:235,393,438-446) and non_indexed::walk (core/src/location/
+ * non_indexed.rs:164-187).  Blocking and thread-safe: concurrent calls on one context
+ * are coalesced by a dispatcher thread into one staged GPU batch per window (tuning
+ * "coalesce_window_us", default 200, or "coalesce_max" requests, default 4096).  Return
+ * SD_OK with *status = sd_file_status (the hex is written only for SD_FILE_OK). */
+int sd_cas_id_path(sd_cas_ctx* ctx, const char* path, uint64_t size, char* out_hex17, int32_t* status);
+int sd_file_checksum_path(sd_cas_ctx* ctx, const char* path, char* out_hex65, int32_t* status);
+/* [0] single-file requests, [1] batches they were coalesced into, [2] largest batch */
+int sd_coalescer_stats(sd_cas_ctx* ctx, uint64_t out[3]);
 
 /* ---------------------------------------------------------------- dedup (post-hash) */
 /* Bucket records (cas_id as big-endian u64 of the first 8 hash bytes, global file
@@ -199,7 +221,8 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * batch-internal side stream (joined back into `stream`), 3 = sampled kernel + prefetching
  * chunk-pair leaf + tree over pair nodes (default), 4 = variant 0 with prefetching chunk-pair leaves,
  * 5 = variant 3 with the pair-node trees merged level-wise in LDS (k_whole_forest);
- * "checksum_variant" (default 0). */
+ * "checksum_variant" (default 0); "coalesce_window_us" / "coalesce_max" (latency path);
+ * "files_window_mb" (sd_cas_ids_files). */
 int sd_cas_set_tuning(const char* key, int value);
 /* Read-only probe over d_buf[0, bytes) (bytes a multiple of 4096) for calibrating the
  * PMC byte counters on this kernel family's access patterns: pattern 0 = coalesced

@@ -8,10 +8,10 @@ re-implemented as hand-written gfx950 HIP kernels behind the C ABI in include/sd
 (``libsdcas.so``).  See DESIGN.md.
 """
 from ._native import SdCasError, lib  # noqa: F401  (raises ImportError if libsdcas.so is missing)
-from .cas import (FileMetadata, UnexpectedEofError, file_checksum, file_checksums,  # noqa: F401
+from .cas import (FileMetadata, UnexpectedEofError, coalescer_stats, file_checksum, file_checksums,  # noqa: F401
                   generate_cas_id, generate_cas_ids)
 from .device import CasBatch, ChecksumBatch, Context, default_context, stage_plan  # noqa: F401
 
 __all__ = ["generate_cas_id", "generate_cas_ids", "file_checksum", "file_checksums", "FileMetadata",
            "UnexpectedEofError", "Context", "CasBatch", "ChecksumBatch", "default_context", "stage_plan",
-           "SdCasError"]
+           "SdCasError", "coalescer_stats"]

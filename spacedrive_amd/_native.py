@@ -60,6 +60,7 @@ SIGNATURES = [
     ("sd_cas_stage_file", I32, [ctypes.c_char_p, P, P, ctypes.POINTER(ctypes.c_int32)]),
     ("sd_cas_stage_files", I32, [P, P, SZ, P, P, I32]),
     ("sd_cas_ids", I32, [P, P, U64, P, SZ, P, P]),
+    ("sd_cas_ids_files", I32, [P, P, P, SZ, P, P, I32]),
     ("sd_cas_batch_create", I32, [P, P, SZ, ctypes.POINTER(P)]),
     ("sd_cas_batch_destroy", None, [P]),
     ("sd_cas_batch_run", I32, [P, P, P, P, P]),
@@ -70,6 +71,9 @@ SIGNATURES = [
     ("sd_checksum_batch_run", I32, [P, P, P, P, P]),
     ("sd_checksum_batch_stats", I32, [P, P]),
     ("sd_file_checksums", I32, [P, P, SZ, P, P]),
+    ("sd_cas_id_path", I32, [P, ctypes.c_char_p, U64, P, ctypes.POINTER(ctypes.c_int32)]),
+    ("sd_file_checksum_path", I32, [P, ctypes.c_char_p, P, ctypes.POINTER(ctypes.c_int32)]),
+    ("sd_coalescer_stats", I32, [P, P]),
     ("sd_dedup_partition", I32, [P, P, P, U64, U64, I32, P, P, PU64, P]),
     ("sd_dedup_group", I32, [P, P, U64, I32, P, PU64, P]),
     ("sd_synth_stage_cas", I32, [P, P, P, P, P, SZ, P, P]),

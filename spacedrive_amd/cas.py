@@ -30,9 +30,10 @@ from typing import List, Optional, Sequence, Union
 import numpy as np
 
 from ._native import (SD_FILE_IO_ERROR, SD_FILE_OK, SD_FILE_SHORT_READ, check, lib)
-from .device import _ptr, default_context, stage_plan
+from .device import _ptr, default_context
 
 MINIMUM_FILE_SIZE = 1024 * 100  # cas.rs:15
+STAGE_THREADS = 16  # host reader threads (the CPU share of one GPU on an MI355X node)
 
 
 class UnexpectedEofError(OSError):
@@ -49,22 +50,6 @@ def _status_error(st: int, path: str) -> OSError:
     return OSError(_errno.EIO, f"sd_cas status {st}", path)
 
 
-class _PinnedHost:
-    """Pinned host staging buffer from sd_cas_host_alloc, viewed as numpy."""
-
-    def __init__(self, ctx, nbytes: int):
-        self.ctx = ctx
-        p = ctypes.c_void_p()
-        check(lib().sd_cas_host_alloc(ctx.handle, max(nbytes, 16), ctypes.byref(p)))
-        self.ptr = p
-        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(nbytes, 16)).from_address(p.value))
-
-    def free(self) -> None:
-        if self.ptr:
-            lib().sd_cas_host_free(self.ctx.handle, self.ptr)
-            self.ptr = None
-
-
 def generate_cas_ids(paths: Sequence[Union[str, os.PathLike]], sizes: Sequence[int],
                      device: Optional[int] = None) -> List[Union[str, OSError]]:
     """Batched generate_cas_id: one cas_id string or OSError per (path, size)."""
@@ -74,19 +59,13 @@ def generate_cas_ids(paths: Sequence[Union[str, os.PathLike]], sizes: Sequence[i
     if n == 0:
         return []
     ctx = default_context(device)
-    ext, total = stage_plan(sizes)
-    staged = _PinnedHost(ctx, total)
-    try:
-        status = np.zeros(n, np.int32)
-        L = lib()
-        enc = [os.fsencode(p) for p in paths]
-        arr = (ctypes.c_char_p * n)(*enc)
-        # pread of header/samples/tail (or the whole file) on a thread pool
-        check(L.sd_cas_stage_files(arr, _ptr(ext), n, staged.ptr, _ptr(status), min(16, os.cpu_count() or 1)))
-        out = ctypes.create_string_buffer(17 * n)
-        check(L.sd_cas_ids(ctx.handle, staged.ptr, total, _ptr(ext), n, out, _ptr(status)))
-    finally:
-        staged.free()
+    sizes_a = np.ascontiguousarray(sizes, dtype=np.uint64)
+    status = np.zeros(n, np.int32)
+    arr = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
+    out = ctypes.create_string_buffer(17 * n)
+    # library-side pread of header/samples/tail (or the whole file) on its stager pool,
+    # overlapped window by window with the H2D copies and kernels
+    check(lib().sd_cas_ids_files(ctx.handle, arr, _ptr(sizes_a), n, out, _ptr(status), STAGE_THREADS))
     raw = out.raw
     res: List[Union[str, OSError]] = []
     for i in range(n):
@@ -98,11 +77,17 @@ def generate_cas_ids(paths: Sequence[Union[str, os.PathLike]], sizes: Sequence[i
 
 
 def generate_cas_id(path: Union[str, os.PathLike], size: int, device: Optional[int] = None) -> str:
-    """cas.rs:23 ``generate_cas_id(path, size) -> Result<String, io::Error>``."""
-    r = generate_cas_ids([path], [size], device)[0]
-    if isinstance(r, OSError):
-        raise r
-    return r
+    """cas.rs:23 ``generate_cas_id(path, size) -> Result<String, io::Error>``.
+
+    The single-file latency path (watcher / non_indexed callers): concurrent calls from
+    any number of threads are coalesced into GPU batches by the library (sd_cas_id_path)."""
+    ctx = default_context(device)
+    out = ctypes.create_string_buffer(17)
+    st = ctypes.c_int32(0)
+    check(lib().sd_cas_id_path(ctx.handle, os.fsencode(path), int(size), out, ctypes.byref(st)))
+    if st.value != SD_FILE_OK:
+        raise _status_error(st.value, os.fsdecode(path))
+    return out.raw[:16].decode()
 
 
 def file_checksums(paths: Sequence[Union[str, os.PathLike]],
@@ -123,11 +108,22 @@ def file_checksums(paths: Sequence[Union[str, os.PathLike]],
 
 
 def file_checksum(path: Union[str, os.PathLike], device: Optional[int] = None) -> str:
-    """hash.rs:10 ``file_checksum(path) -> Result<String, io::Error>``."""
-    r = file_checksums([path], device)[0]
-    if isinstance(r, OSError):
-        raise r
-    return r
+    """hash.rs:10 ``file_checksum(path) -> Result<String, io::Error>`` (coalesced like
+    generate_cas_id: sd_file_checksum_path)."""
+    ctx = default_context(device)
+    out = ctypes.create_string_buffer(65)
+    st = ctypes.c_int32(0)
+    check(lib().sd_file_checksum_path(ctx.handle, os.fsencode(path), out, ctypes.byref(st)))
+    if st.value != SD_FILE_OK:
+        raise _status_error(st.value, os.fsdecode(path))
+    return out.raw[:64].decode()
+
+
+def coalescer_stats(device: Optional[int] = None) -> dict:
+    """Latency-path counters of the device's default context."""
+    v = np.zeros(3, np.uint64)
+    check(lib().sd_coalescer_stats(default_context(device).handle, _ptr(v)))
+    return {"requests": int(v[0]), "batches": int(v[1]), "max_batch": int(v[2])}
 
 
 @dataclass

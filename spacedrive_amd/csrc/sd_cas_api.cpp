@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "sd_internal.h"
+#include "stage_pool.h"
 
 namespace {
 
@@ -141,6 +142,20 @@ struct sd_cas_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
+    std::mutex coal_mu;
+    sd_coalescer* coal = nullptr;  // latency path, created on the first single-file call
+    std::mutex pool_mu;
+    std::unique_ptr<StagePool> pool;  // file stager threads (sd_cas_ids_files)
+    StagePool& stage_pool(int nthreads) {
+        std::lock_guard<std::mutex> g(pool_mu);
+        if (!pool || pool->threads() != nthreads) pool = std::make_unique<StagePool>(nthreads);
+        return *pool;
+    }
+    sd_coalescer* coalescer() {
+        std::lock_guard<std::mutex> g(coal_mu);
+        if (!coal) coal = coalescer_create(this);
+        return coal;
+    }
     std::vector<std::unique_ptr<Slot>> free_slots;
 
     std::unique_ptr<Slot> acquire() {
@@ -588,7 +603,7 @@ int32_t stage_one(const char* path, const sd_extent& e, uint8_t* staged) {
 
 // ------------------------------------------------------------------ tuning knobs
 #include <atomic>
-static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{21}, {3}, {0}};
+static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{21}, {3}, {0}, {200}, {4096}, {32}};
 int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
 
 // ============================================================================ C ABI
@@ -597,7 +612,8 @@ extern "C" {
 int sd_cas_set_tuning(const char* key, int value) {
     SD_GUARD_BEGIN
     if (!key) throw sd_failure(SD_ERR_INVALID, "null key");
-    static const char* names[SD_TUNE_NKEYS] = {"sampled_variant", "whole_variant", "checksum_variant"};
+    static const char* names[SD_TUNE_NKEYS] = {"sampled_variant", "whole_variant", "checksum_variant",
+                                               "coalesce_window_us", "coalesce_max", "files_window_mb"};
     for (int k = 0; k < SD_TUNE_NKEYS; k++)
         if (strcmp(key, names[k]) == 0) {
             g_tune[k].store(value, std::memory_order_relaxed);
@@ -635,6 +651,8 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
 void sd_cas_ctx_destroy(sd_cas_ctx* ctx) {
     if (!ctx) return;
     try {
+        if (ctx->coal) coalescer_destroy(ctx->coal);  // drains its queue, joins the dispatcher
+        ctx->coal = nullptr;
         ctx->bind();
         (void)hipDeviceSynchronize();
         for (auto& s : ctx->free_slots)
@@ -831,6 +849,123 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
     }
     harvest(0);
     harvest(1);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+// Path-based drop-in batch: generate_cas_id (cas.rs:23-62) for n (path, size) pairs,
+// the sizes being the ones the caller's metadata reported (FileMetadata::new,
+// file_identifier/mod.rs:65-97).  Files are planned into windows of consecutive files;
+// the stager pool preads window k+1 into one pinned slot while window k's H2D copy,
+// kernels and D2H run on the other slot's stream.
+int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n, char* out_hex17,
+                     int32_t* status, int nthreads) {
+    SD_GUARD_BEGIN
+    if (!ctx || (n && (!paths || !sizes || !out_hex17 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    StagePool& pool = ctx->stage_pool(nthreads);
+    const uint64_t WINDOW = (uint64_t)std::max(1, tuning_get(SD_TUNE_FILES_WINDOW_MB)) << 20;
+    std::unique_ptr<Slot> slots[2] = {ctx->acquire(), ctx->acquire()};
+    struct Rel {
+        sd_cas_ctx* c;
+        std::unique_ptr<Slot>* s;
+        ~Rel() {
+            for (int k = 0; k < 2; k++)
+                if (s[k]) {
+                    (void)hipStreamSynchronize(s[k]->stream);
+                    c->release(std::move(s[k]));
+                }
+        }
+    } rel{ctx, slots};
+    sd_cas_batch batches[2];
+    struct Win {
+        std::vector<size_t> files;  // hashed files of the window, in extent order
+        bool busy = false;
+    } wins[2];
+    auto harvest = [&](int k) {
+        if (!wins[k].busy) return;
+        HIP_CHECK(hipStreamSynchronize(slots[k]->stream));
+        const uint8_t* h = reinterpret_cast<const uint8_t*>(slots[k]->host_hashes.p);
+        for (size_t q = 0; q < wins[k].files.size(); q++)
+            to_hex(h + q * 32, 8, out_hex17 + wins[k].files[q] * 17);  // cas.rs:61 to_hex()[..16]
+        wins[k].busy = false;
+    };
+    std::vector<sd_extent> ext;
+    std::vector<size_t> idx;
+    size_t i = 0;
+    for (int w = 0; i < n; w ^= 1) {
+        // the next window: consecutive files whose messages fit WINDOW bytes
+        ext.clear();
+        idx.clear();
+        uint64_t off = 0;
+        while (i < n) {
+            const bool whole = sizes[i] <= SD_MINIMUM_FILE_SIZE;  // cas.rs:27
+            const uint32_t len = whole ? (uint32_t)(8 + sizes[i]) : SD_SAMPLED_MSG_LEN;
+            const uint64_t next = align_up(off + len, SD_STAGE_ALIGN);
+            if (!ext.empty() && next > WINDOW) break;
+            ext.push_back(sd_extent{sizes[i], off, len, whole ? (uint32_t)SD_KIND_WHOLE : (uint32_t)SD_KIND_SAMPLED});
+            idx.push_back(i);
+            off = next;
+            i++;
+        }
+        harvest(w);  // slot w's previous window is done: its pinned buffer is free
+        Slot& sl = *slots[w];
+        sl.window.ensure(off + 64);
+        uint8_t* win = reinterpret_cast<uint8_t*>(sl.window.p);
+        pool.run(ext.size(), [&](size_t q) { status[idx[q]] = stage_one(paths[idx[q]], ext[q], win); });
+        // failed files (I/O error, short read) keep their status and leave the window
+        size_t m = 0;
+        for (size_t q = 0; q < ext.size(); q++)
+            if (status[idx[q]] == SD_FILE_OK) {
+                ext[m] = ext[q];
+                idx[m++] = idx[q];
+            }
+        ext.resize(m);
+        idx.resize(m);
+        if (m == 0) continue;
+        plan_cas_batch(&batches[w], ext.data(), m, sl.stream);
+        sl.staged.ensure(off + 64);
+        sl.hashes.ensure(m * 32);
+        sl.host_hashes.ensure(m * 32);
+        HIP_CHECK(hipMemcpyAsync(sl.staged.p, win, off, hipMemcpyHostToDevice, sl.stream));
+        run_cas_batch(&batches[w], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
+        HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, m * 32, hipMemcpyDeviceToHost, sl.stream));
+        wins[w].files = idx;
+        wins[w].busy = true;
+    }
+    harvest(0);
+    harvest(1);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+// ------------------------------------------------------------------- latency path
+int sd_cas_id_path(sd_cas_ctx* ctx, const char* path, uint64_t size, char* out_hex17, int32_t* status) {
+    SD_GUARD_BEGIN
+    if (!ctx || !path || !out_hex17 || !status) throw sd_failure(SD_ERR_INVALID, "null argument");
+    std::string err;
+    const int rc = coalescer_submit(ctx->coalescer(), 0, path, size, out_hex17, status, &err);
+    if (rc != SD_OK) set_err("%s", err.c_str());
+    return rc;
+    SD_GUARD_END
+}
+
+int sd_file_checksum_path(sd_cas_ctx* ctx, const char* path, char* out_hex65, int32_t* status) {
+    SD_GUARD_BEGIN
+    if (!ctx || !path || !out_hex65 || !status) throw sd_failure(SD_ERR_INVALID, "null argument");
+    std::string err;
+    const int rc = coalescer_submit(ctx->coalescer(), 1, path, 0, out_hex65, status, &err);
+    if (rc != SD_OK) set_err("%s", err.c_str());
+    return rc;
+    SD_GUARD_END
+}
+
+int sd_coalescer_stats(sd_cas_ctx* ctx, uint64_t out[3]) {
+    SD_GUARD_BEGIN
+    if (!ctx || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    coalescer_stats(ctx->coalescer(), out);
     return SD_OK;
     SD_GUARD_END
 }

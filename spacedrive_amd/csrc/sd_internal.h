@@ -23,8 +23,25 @@ struct ck_reduce_wg {
 };
 
 // process-wide tuning knobs (sd_cas_set_tuning); read at launch time
-enum sd_tune_key { SD_TUNE_SAMPLED_VARIANT = 0, SD_TUNE_WHOLE_VARIANT = 1, SD_TUNE_CK_VARIANT = 2, SD_TUNE_NKEYS = 3 };
+enum sd_tune_key {
+    SD_TUNE_SAMPLED_VARIANT = 0,
+    SD_TUNE_WHOLE_VARIANT = 1,
+    SD_TUNE_CK_VARIANT = 2,
+    SD_TUNE_COALESCE_US = 3,
+    SD_TUNE_COALESCE_MAX = 4,
+    SD_TUNE_FILES_WINDOW_MB = 5,
+    SD_TUNE_NKEYS = 6
+};
 int tuning_get(int key);
+
+// latency path (coalesce.cpp)
+#include <string>
+struct sd_coalescer;
+sd_coalescer* coalescer_create(sd_cas_ctx* ctx);
+void coalescer_destroy(sd_coalescer* c);
+int coalescer_submit(sd_coalescer* c, int kind, const char* path, uint64_t size, char* out, int32_t* status,
+                     std::string* err);
+void coalescer_stats(sd_coalescer* c, uint64_t out[3]);
 
 namespace sdk {
 hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const uint32_t* idx, uint32_t n,

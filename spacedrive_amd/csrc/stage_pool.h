@@ -1,0 +1,73 @@
+// stage_pool.h -- persistent host thread pool for the file stager (pread of the byte
+// windows generate_cas_id reads, cas.rs:27-58).  run(n, f) calls f(0..n-1) on the pool
+// and the calling thread and returns when all are done; one run at a time per pool.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+class StagePool {
+public:
+    explicit StagePool(int nthreads) {
+        for (int t = 1; t < nthreads; t++) th_.emplace_back([this] { worker(); });
+    }
+    ~StagePool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int threads() const { return (int)th_.size() + 1; }
+    void run(size_t n, const std::function<void(size_t)>& f) {
+        std::lock_guard<std::mutex> serial(run_mu_);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &f;
+            n_ = n;
+            next_.store(0);
+            busy_ = (int)th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [&] { return busy_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    void drain() {
+        for (;;) {
+            const size_t i = next_.fetch_add(1, std::memory_order_relaxed);
+            if (i >= n_) break;
+            (*fn_)(i);
+        }
+    }
+    void worker() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            g.unlock();
+            drain();
+            g.lock();
+            if (--busy_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_, run_mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(size_t)>* fn_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    int busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};

@@ -375,6 +375,85 @@ def test_concurrent_callers_share_a_context(ctx, tmp_path):
     assert not errors, errors
 
 
+def test_cas_ids_files_pipelined_windows(ctx, tmp_path, oracle_native):
+    """sd_cas_ids_files over many 1 MiB windows (stage k+1 while k hashes), with I/O
+    errors and short files interleaved, equals the reference read schedule on the CPU."""
+    import spacedrive_amd as sd
+    from spacedrive_amd import synth
+    from spacedrive_amd._native import lib
+    from spacedrive_amd.device import stage_plan
+    n = 400
+    sizes, cids, twins = synth.library(0, n, n)
+    sizes = np.minimum(sizes, np.uint64(1 << 34))
+    ext, total = stage_plan(sizes)
+    buf = oracle_native.stage_synth(sizes, cids, twins, ext["msg_offset"], total)
+    paths = synth.write_files(str(tmp_path), sizes, buf, ext)
+    plan = [int(x) for x in sizes]
+    paths[7] = str(tmp_path / "missing")  # IO_ERROR(ENOENT)
+    big = [i for i in range(n) if sizes[i] > 102400 and i != 7][0]
+    plan[big] = int(sizes[big]) + (1 << 20)  # planned past EOF: the tail read hits EOF
+    want, wst = oracle_native.cas_ids_files(paths, np.array(plan, np.uint64), nthreads=4)
+    assert lib().sd_cas_set_tuning(b"files_window_mb", 1) == 0
+    try:
+        got = sd.generate_cas_ids(paths, plan)
+    finally:
+        lib().sd_cas_set_tuning(b"files_window_mb", 32)
+    for i in range(n):
+        if wst[i] == 0:
+            assert got[i] == want[i].tobytes().hex(), i
+        elif wst[i] == 3:
+            assert isinstance(got[i], sd.UnexpectedEofError), i
+        else:
+            assert isinstance(got[i], FileNotFoundError), i
+    assert wst[7] != 0 and wst[big] == 3
+
+
+def test_latency_path_coalesces_concurrent_single_file_calls(ctx, tmp_path):
+    """Watcher / non_indexed callers (watcher/utils.rs:235,393,438-446, non_indexed.rs:164-187)
+    hash one file per call from many tasks: sd_cas_id_path / sd_file_checksum_path must
+    return exactly what the batch path returns, with errors per call, while the library
+    folds the concurrent calls into fewer GPU batches."""
+    import threading
+    import spacedrive_amd as sd
+    from oracle import native
+    sizes = [1, 1017, 5000, 102400, 102401, 700_000, 3 << 20] * 6
+    paths = []
+    for i, s in enumerate(sizes):
+        p = tmp_path / f"w{i}.bin"
+        p.write_bytes(native.synth_bytes(300 + i, 0, 0, s))
+        paths.append(str(p))
+    want_ids = sd.generate_cas_ids(paths, sizes)
+    want_sums = sd.file_checksums(paths)
+    before = sd.coalescer_stats()
+    got_ids, got_sums, errs = [None] * len(paths), [None] * len(paths), []
+    barrier = threading.Barrier(len(paths))
+
+    def worker(i):
+        barrier.wait()
+        got_ids[i] = sd.generate_cas_id(paths[i], sizes[i])
+        got_sums[i] = sd.file_checksum(paths[i])
+        try:
+            sd.generate_cas_id(str(tmp_path / f"missing{i}"), 10)
+        except FileNotFoundError:
+            errs.append(i)
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(len(paths))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert got_ids == want_ids and got_sums == want_sums
+    assert sorted(errs) == list(range(len(paths)))
+    after = sd.coalescer_stats()
+    calls = after["requests"] - before["requests"]
+    batches = after["batches"] - before["batches"]
+    assert calls == 3 * len(paths)
+    assert batches < calls and after["max_batch"] > 1, after
+    # short file planned with a larger size: read_exact's UnexpectedEof (cas.rs:36,43,56)
+    with pytest.raises(sd.UnexpectedEofError):
+        sd.generate_cas_id(paths[5], 900_000)
+
+
 def test_pipeline_object_owners_vs_reference_replay(ctx, oracle_native):
     # hash (GPU) -> partition -> group -> owners == identifier_job_step replay on oracle cas_ids
     from oracle.identifier_spec import identifier_replay
