@@ -141,3 +141,29 @@ def test_stage_files_threaded_equals_single(tmp_path):
     for i in range(7):
         o, L = int(ext["msg_offset"][i]), int(ext["msg_len"][i])
         assert a[o:o + L].tobytes() == b[o:o + L].tobytes() == cs.cas_message(cs.synth_reader(70 + i), sizes[i])
+
+
+def _header_param_counts():
+    src = open(_native.HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(sd_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", src, flags=re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_rust_shim_matches_header():
+    """integration/rust/sd-cas-sys (the binding a maintainer adds as crates/sd-cas-sys)
+    declares only functions the header has, with the header's parameter counts."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "integration", "rust", "sd-cas-sys", "src", "lib.rs")).read()
+    block = src[src.index('extern "C" {'):]
+    block = block[:block.index("\n}\n")]
+    decls = re.findall(r"pub fn (sd_[a-z0-9_]+)\s*\(([^)]*)\)", block, flags=re.S)
+    assert len(decls) >= 8
+    hdr = _header_param_counts()
+    for name, args in decls:
+        n = 0 if not args.strip() else args.count(",") + 1 - (1 if args.strip().endswith(",") else 0)
+        assert name in hdr, name
+        assert hdr[name] == n, (name, hdr[name], n)
