@@ -24,14 +24,19 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--checksum-gib", type=int, default=16)
+    ap.add_argument("--key", default=None, help="tuning key the variants set (default: by --what)")
+    ap.add_argument("--set", default="", help="extra fixed tuning, e.g. whole_variant=7")
     args = ap.parse_args()
     import spacedrive_amd as sd
     from spacedrive_amd import synth
     from spacedrive_amd._native import lib
 
     key = {"sampled": b"sampled_variant", "whole": b"whole_variant", "library": b"whole_variant",
-           "checksum": b"checksum_variant"}[args.what]
+           "checksum": b"checksum_variant"}[args.what] if args.key is None else args.key.encode()
     variants = [int(v) for v in args.variants.split(",")]
+    for kv in filter(None, args.set.split(",")):
+        k, v = kv.split("=")
+        assert lib().sd_cas_set_tuning(k.encode(), int(v)) == 0
     ctx = sd.Context(0)
     dev = torch.device("cuda", 0)
     if args.what in ("sampled", "whole", "library"):

@@ -86,7 +86,8 @@ def main(tag):
             calib[pattern] = CALIB_BYTES / (v * 1024)
     # k_cas_sampled (U = 2) reads 2 KiB per lane: probe pattern 2; whole leaf: pattern 1;
     # checksum leaf (4 KiB per lane, same 16 B x 4 per block shape): pattern 2
-    use = {"k_cas_sampled": 2, "k_whole_leaf": 1, "k_whole_pair_leaf": 2, "k_ck_leaf": 2}
+    use = {"k_cas_sampled": 2, "k_whole_leaf": 1, "k_whole_pair_leaf": 2, "k_whole_items": 2, "k_whole_full": 2,
+           "k_ck_leaf": 2}
     kern = {}
     for k, cs in pmc.items():
         if "FETCH_SIZE" not in cs:

@@ -451,6 +451,115 @@ __global__ __launch_bounds__(256) void k_whole_tree(const uint32_t* __restrict__
     store_cv(out + (size_t)order[k] * 8, res);
 }
 
+// ------------------------------------------------- whole-file work lists (variant 6)
+// The pair leaf splits into two launches over host-built item lists, so every wave runs
+// lanes of equal trip count:
+//   k_whole_full   every aligned chunk pair lying wholly inside a message of >= 3 chunks:
+//                  32 full blocks + one parent, never ROOT -- the sampled kernel's
+//                  branch-free loop (full_chunks_cv<2, true>).  91 % of configs[1]'s
+//                  compressions.  Item = (u64 pair offset, cv slot, first chunk index).
+//   k_whole_tail   the other pairs (a message's partial last pair, or the whole message
+//                  when it has <= 2 chunks, then ROOT), sorted on the host by compression
+//                  count.  Item = (u64 offset, cv slot or file, glen | c0 << 12 | root << 31).
+// and the pair-node trees merge in two launches of k_whole_merge8 (aligned groups of up to
+// 8 nodes per lane, level-wise in registers): a critical path of <= 7 + 6 serial parents
+// where k_whole_tree's longest lane runs nodes - 1 (50 for a 100 KiB file).
+__global__ __launch_bounds__(256) void k_whole_full(const uint8_t* __restrict__ staged, const uint4* __restrict__ items,
+                                                    uint32_t n, uint32_t* __restrict__ cvbuf) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    const uint4 it = items[g];
+    const uint64_t off = (uint64_t)it.x | ((uint64_t)it.y << 32);
+    uint32_t cv[8];
+    full_chunks_cv<2, true>(cv, staged + off, it.w);
+    store_cv(cvbuf + (size_t)it.z * 8, cv);
+}
+
+__global__ __launch_bounds__(256) void k_whole_tail(const uint8_t* __restrict__ staged, const uint4* __restrict__ items,
+                                                    uint32_t n, uint32_t* __restrict__ cvbuf,
+                                                    uint32_t* __restrict__ out) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    const uint4 it = items[g];
+    const uint64_t off = (uint64_t)it.x | ((uint64_t)it.y << 32);
+    const uint32_t glen = it.w & 0xFFFu, c0 = (it.w >> 12) & 0x7FFFFu;
+    const bool root = (it.w >> 31) != 0u;
+    uint32_t cv[8];
+    pair_cv(cv, staged + off, glen, c0, root);
+    store_cv((root ? out : cvbuf) + (size_t)it.z * 8, cv);
+}
+
+// Both lists in one launch: workgroups [0, wf) take full-pair items, the rest tail items
+// (a workgroup-uniform branch).  The tail path hashes its chunks one after the other
+// without the prefetch buffer, so the kernel keeps the full path's register budget
+// (8 waves/SIMD), and its latency-bound lanes run while the last full-pair waves drain.
+__global__ __launch_bounds__(256) void k_whole_items(const uint8_t* __restrict__ staged,
+                                                     const uint4* __restrict__ full, uint32_t n_full, uint32_t wf,
+                                                     const uint4* __restrict__ tail, uint32_t n_tail,
+                                                     uint32_t* __restrict__ cvbuf, uint32_t* __restrict__ out) {
+    if (blockIdx.x < wf) {
+        const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+        if (g >= n_full) return;
+        const uint4 it = full[g];
+        const uint64_t off = (uint64_t)it.x | ((uint64_t)it.y << 32);
+        uint32_t cv[8];
+        full_chunks_cv<2, true>(cv, staged + off, it.w);
+        store_cv(cvbuf + (size_t)it.z * 8, cv);
+        return;
+    }
+    const uint32_t g = (blockIdx.x - wf) * blockDim.x + threadIdx.x;
+    if (g >= n_tail) return;
+    const uint4 it = tail[g];
+    const uint8_t* p = staged + ((uint64_t)it.x | ((uint64_t)it.y << 32));
+    const uint32_t glen = it.w & 0xFFFu, c0 = (it.w >> 12) & 0x7FFFFu;
+    const bool root = (it.w >> 31) != 0u;
+    uint32_t cv[8];
+    if (glen <= CHUNK_LEN) {
+        chunk_cv(cv, p, glen, c0, root);
+    } else {
+        uint32_t l[8], r[8];
+        chunk_cv(l, p, CHUNK_LEN, c0, false);
+        chunk_cv(r, p + CHUNK_LEN, glen - CHUNK_LEN, c0 + 1, false);
+        parent(cv, l, r, root ? ROOT : 0u);
+    }
+    store_cv((root ? out : cvbuf) + (size_t)it.z * 8, cv);
+}
+
+// Item = (first node slot in src, m | root << 31, dst slot or file): merges nodes
+// src[first .. first + m), m in 1..8, an aligned group of one file's node list, level-wise
+// with the odd node carried up; ROOT on the final parent when the group is the whole file.
+__global__ __launch_bounds__(256) void k_whole_merge8(const uint4* __restrict__ items, uint32_t n,
+                                                      const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                      uint32_t* __restrict__ out) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    const uint4 it = items[g];
+    const uint32_t m = it.y & 0xFu;
+    const bool root = (it.y >> 31) != 0u;
+    uint32_t v[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if ((uint32_t)i < m) load_cv(v[i], src + (size_t)(it.x + i) * 8);
+    uint32_t nn = m;
+#pragma unroll
+    for (int lvl = 0; lvl < 3; lvl++) {
+#pragma unroll
+        for (int q = 0; q < (4 >> lvl); q++) {
+            if ((uint32_t)(2 * q + 1) < nn) {
+                uint32_t t[8];
+                parent(t, v[2 * q], v[2 * q + 1], (root && nn == 2) ? ROOT : 0u);
+#pragma unroll
+                for (int i = 0; i < 8; i++) v[q][i] = t[i];
+            } else if ((uint32_t)(2 * q) < nn) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) v[q][i] = v[2 * q][i];
+            }
+        }
+        nn = (nn + 1) >> 1;
+    }
+    store_cv((root ? out : dst) + (size_t)it.z * 8, v[0]);
+}
+
 // ------------------------------------------------------------------------ checksums
 // Leaf: workgroup (256 lanes) = 1 MiB block = 1024 chunks of one file; lane l hashes
 // chunks [4l, 4l+4) and merges them in-lane; then the lane CVs merge in LDS.
@@ -639,6 +748,30 @@ hipError_t launch_whole(const uint8_t* staged, const sd_extent* ext, const uint3
     if (n_multi)
         hipLaunchKernelGGL(k_whole_tree, dim3((n_multi + 255) / 256), dim3(256), 0, s, order, chunk_prefix,
                            n_multi, cvbuf, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_whole_items(const uint8_t* staged, const uint4* full, uint32_t n_full, const uint4* tail,
+                              uint32_t n_tail, const uint4* merge_a, uint32_t n_a, const uint4* merge_b, uint32_t n_b,
+                              uint32_t* cvbuf, uint32_t* cv2, uint32_t* out, hipStream_t s, bool combined) {
+    if (combined) {
+        const uint32_t wf = (n_full + 255) / 256, wt = (n_tail + 255) / 256;
+        if (wf + wt)
+            hipLaunchKernelGGL(k_whole_items, dim3(wf + wt), dim3(256), (size_t)tuning_get(SD_TUNE_WHOLE_LDS_KB) << 10, s,
+                               staged, full, n_full, wf, tail, n_tail, cvbuf, out);
+    } else {
+        if (n_full)
+            hipLaunchKernelGGL(k_whole_full, dim3((n_full + 255) / 256), dim3(256), 0, s, staged, full, n_full, cvbuf);
+        if (n_tail)
+            hipLaunchKernelGGL(k_whole_tail, dim3((n_tail + 255) / 256), dim3(256), 0, s, staged, tail, n_tail,
+                               cvbuf, out);
+    }
+    if (n_a)
+        hipLaunchKernelGGL(k_whole_merge8, dim3((n_a + 255) / 256), dim3(256), 0, s, merge_a, n_a,
+                           (const uint32_t*)cvbuf, cv2, out);
+    if (n_b)
+        hipLaunchKernelGGL(k_whole_merge8, dim3((n_b + 255) / 256), dim3(256), 0, s, merge_b, n_b,
+                           (const uint32_t*)cv2, (uint32_t*)nullptr, out);
     return hipGetLastError();
 }
 

@@ -187,7 +187,11 @@ struct sd_cas_batch {
     uint32_t n_groups = 0;  // whole-file groups of the fused kernel
     uint32_t total_pairs = 0, n_multi2 = 0;  // pair leaf: chunk pairs; files with >= 3 chunks
     uint32_t n_groups2 = 0;                  // forest groups over the multi-pair files
+    // variant 6 item lists (kernel formats in cas_kernels.hip, k_whole_full / _tail / _merge8)
+    uint32_t n_full = 0, n_tail = 0, n_merge_a = 0, n_merge_b = 0, n_cv2 = 0;
     DevBuf ext, sidx, order, prefix, hint, cvbuf, groups, prefix2, hint2, groups2;
+    DevBuf full_items, tail_items, merge_a, merge_b, cv2;
+    std::vector<uint4> h_full, h_tail, h_merge_a, h_merge_b;
     // variant 2: the whole-file tree kernel runs on a side stream beside the sampled kernel
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
@@ -247,6 +251,86 @@ void validate_extent(const sd_extent& e, size_t i) {
         throw sd_failure(SD_ERR_INVALID, "extent " + std::to_string(i) + ": kind/msg_len do not match size");
     if (e.msg_offset % 16)
         throw sd_failure(SD_ERR_INVALID, "extent " + std::to_string(i) + ": msg_offset not 16-byte aligned");
+}
+
+// compressions of aligned chunk pair (c0, c0 + 1) holding glen (1..2048) message bytes
+uint32_t pair_compressions(uint32_t glen) {
+    const uint32_t l0 = std::min<uint32_t>(glen, 1024), l1 = glen - l0;
+    return (l0 + 63) / 64 + (l1 ? (l1 + 63) / 64 + 1 : 0);
+}
+
+// Variant-6 work lists over the length-sorted whole files (b->h_order, pair prefix
+// b->h_prefix2): full-pair items in (file, pair) order; tail items counting-sorted by
+// compressions, descending; merge8 items -- pass A over aligned groups of <= 8 pair nodes
+// (the whole tree when a file has <= 8 nodes), pass B over the pass-A nodes of files with
+// more than 8.
+void plan_whole_items(sd_cas_batch* b, const sd_extent* ext) {
+    auto& full = b->h_full;
+    auto& tail = b->h_tail;
+    auto& ma = b->h_merge_a;
+    auto& mb = b->h_merge_b;
+    full.clear();
+    tail.clear();
+    ma.clear();
+    mb.clear();
+    std::vector<uint32_t> tail_cost;
+    const auto& p2 = b->h_prefix2;
+    // items are emitted in file (= staged address) order, so the full-pair waves sweep the
+    // staged buffer front to back as the sampled kernel does, instead of hopping between
+    // the length-sorted files' scattered messages; the cv slot still follows the sorted order
+    std::vector<uint32_t> rank(b->n, 0);
+    for (uint32_t k = 0; k < b->n_whole; k++) rank[b->h_order[k]] = k;
+    for (uint32_t file = 0; file < b->n; file++) {
+        const sd_extent& e = ext[file];
+        if (e.kind != SD_KIND_WHOLE) continue;
+        const uint32_t k = rank[file];
+        const uint32_t C = msg_chunks(e.msg_len), P = (C + 1) / 2;
+        const bool multi = C >= 3;
+        for (uint32_t j = 0; j < P; j++) {
+            const uint64_t off = e.msg_offset + 2048ull * j;
+            const uint32_t glen = std::min<uint32_t>(2048, e.msg_len - 2048 * j);
+            const uint32_t lo = (uint32_t)off, hi = (uint32_t)(off >> 32);
+            if (multi && glen == 2048) {
+                full.push_back(make_uint4(lo, hi, p2[k] + j, 2 * j));
+            } else {
+                const uint32_t w = glen | ((2 * j) << 12) | (multi ? 0u : 0x80000000u);
+                tail.push_back(make_uint4(lo, hi, multi ? p2[k] + j : file, w));
+                tail_cost.push_back(pair_compressions(glen));
+            }
+        }
+    }
+    // stable counting sort of the tail items by cost, descending (cost 1..33)
+    {
+        std::vector<uint32_t> start(35, 0);
+        for (uint32_t c : tail_cost) start[34 - c]++;
+        uint32_t acc = 0;
+        for (auto& s : start) {
+            const uint32_t t = s;
+            s = acc;
+            acc += t;
+        }
+        std::vector<uint4> sorted(tail.size());
+        for (size_t i = 0; i < tail.size(); i++) sorted[start[34 - tail_cost[i]]++] = tail[i];
+        tail.swap(sorted);
+    }
+    uint32_t cv2 = 0;
+    for (uint32_t k = 0; k < b->n_multi2; k++) {
+        const uint32_t P = p2[k + 1] - p2[k], file = b->h_order[k];
+        if (P <= 8) {
+            ma.push_back(make_uint4(p2[k], P | 0x80000000u, file, 0));
+            continue;
+        }
+        const uint32_t G = (P + 7) / 8;
+        for (uint32_t a = 0; a < G; a++) ma.push_back(make_uint4(p2[k] + 8 * a, std::min<uint32_t>(8, P - 8 * a), cv2 + a, 0));
+        if (G > 8) throw sd_failure(SD_ERR_INTERNAL, "whole-file message with more than 64 pair nodes");
+        mb.push_back(make_uint4(cv2, G | 0x80000000u, file, 0));
+        cv2 += G;
+    }
+    b->n_full = (uint32_t)full.size();
+    b->n_tail = (uint32_t)tail.size();
+    b->n_merge_a = (uint32_t)ma.size();
+    b->n_merge_b = (uint32_t)mb.size();
+    b->n_cv2 = cv2;
 }
 
 // (Re)plans `b` for these extents, reusing its device buffers.  With a stream, the small
@@ -344,6 +428,7 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
             h2[w] = k;
         }
     }
+    plan_whole_items(b, ext);
     // whole-file groups for the fused kernel: consecutive (length-sorted) files whose
     // chunk pairs fit one 448-lane workgroup
     b->h_groups.clear();
@@ -371,6 +456,11 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
     b->prefix2.upload(b->h_prefix2, stream);
     b->hint2.upload(b->h_hint2, stream);
     b->groups2.upload(b->h_groups2, stream);
+    b->full_items.upload(b->h_full, stream);
+    b->tail_items.upload(b->h_tail, stream);
+    b->merge_a.upload(b->h_merge_a, stream);
+    b->merge_b.upload(b->h_merge_b, stream);
+    b->cv2.ensure((size_t)b->n_cv2 * 32);
     b->cvbuf.ensure((size_t)b->total_chunks * 32);
 }
 
@@ -389,6 +479,17 @@ void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_ha
                                         (parts & SD_PART_SAMPLED) ? b->n_sampled : 0, b->order.as<uint32_t>(),
                                         b->groups.as<uint2>(), (parts & SD_PART_WHOLE) ? b->n_groups : 0, out, s,
                                         wv == 4));
+        return;
+    }
+    if (wv == 6 || wv == 7) {  // sampled kernel; full-pair / cost-sorted tail-pair items (7: one launch); two merge8 passes
+        if (parts & SD_PART_SAMPLED)
+            HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled,
+                                              out, s));
+        if (parts & SD_PART_WHOLE)
+            HIP_CHECK(sdk::launch_whole_items(d_staged, b->full_items.as<uint4>(), b->n_full, b->tail_items.as<uint4>(),
+                                              b->n_tail, b->merge_a.as<uint4>(), b->n_merge_a, b->merge_b.as<uint4>(),
+                                              b->n_merge_b, b->cvbuf.as<uint32_t>(), b->cv2.as<uint32_t>(), out, s,
+                                              wv == 7));
         return;
     }
     if (wv == 3 || wv == 5) {  // sampled kernel; prefetching pair leaf + tree (3) / LDS forest (5) over pair nodes
@@ -603,7 +704,7 @@ int32_t stage_one(const char* path, const sd_extent& e, uint8_t* staged) {
 
 // ------------------------------------------------------------------ tuning knobs
 #include <atomic>
-static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{21}, {3}, {0}, {200}, {4096}, {32}};
+static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{21}, {7}, {0}, {200}, {4096}, {32}, {0}};
 int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
 
 // ============================================================================ C ABI
@@ -613,7 +714,8 @@ int sd_cas_set_tuning(const char* key, int value) {
     SD_GUARD_BEGIN
     if (!key) throw sd_failure(SD_ERR_INVALID, "null key");
     static const char* names[SD_TUNE_NKEYS] = {"sampled_variant", "whole_variant", "checksum_variant",
-                                               "coalesce_window_us", "coalesce_max", "files_window_mb"};
+                                               "coalesce_window_us", "coalesce_max", "files_window_mb",
+                                               "whole_lds_kb"};
     for (int k = 0; k < SD_TUNE_NKEYS; k++)
         if (strcmp(key, names[k]) == 0) {
             g_tune[k].store(value, std::memory_order_relaxed);

@@ -30,7 +30,8 @@ enum sd_tune_key {
     SD_TUNE_COALESCE_US = 3,
     SD_TUNE_COALESCE_MAX = 4,
     SD_TUNE_FILES_WINDOW_MB = 5,
-    SD_TUNE_NKEYS = 6
+    SD_TUNE_WHOLE_LDS_KB = 6,  // dynamic LDS per k_whole_items workgroup (occupancy A/B; 0 = none)
+    SD_TUNE_NKEYS = 7
 };
 int tuning_get(int key);
 
@@ -62,6 +63,10 @@ hipError_t launch_whole_tree(const uint32_t* order, const uint32_t* chunk_prefix
 hipError_t launch_whole(const uint8_t* staged, const sd_extent* ext, const uint32_t* order,
                         const uint32_t* chunk_prefix, const uint32_t* hint, uint32_t nw, uint32_t total_chunks,
                         uint32_t n_multi, uint32_t* cvbuf, uint32_t* out, hipStream_t s);
+// variant 6: full-pair items, cost-sorted tail items, two merge8 passes (cv2 = pass-A output)
+hipError_t launch_whole_items(const uint8_t* staged, const uint4* full, uint32_t n_full, const uint4* tail,
+                              uint32_t n_tail, const uint4* merge_a, uint32_t n_a, const uint4* merge_b, uint32_t n_b,
+                              uint32_t* cvbuf, uint32_t* cv2, uint32_t* out, hipStream_t s, bool combined);
 hipError_t launch_ck_leaf(const uint8_t* data, uint64_t shift, const ck_file* files, const uint2* wg_map,
                           uint32_t n_wg, uint32_t* cvbuf, uint32_t* out, hipStream_t s);
 hipError_t launch_ck_reduce(const uint32_t* src, uint32_t* dst, const ck_reduce_wg* wgs, uint32_t n_wg,

@@ -120,12 +120,13 @@ def test_sd_cas_ids_pipelined_windows(ctx):
             assert status[i] == 0 and raw[17 * i:17 * i + 16].decode() == h[i, :8].tobytes().hex(), i
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=["fused", "split", "side-stream", "pair-leaf", "fused-pair", "pair-forest"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7],
+                ids=["fused", "split", "side-stream", "pair-leaf", "fused-pair", "pair-forest", "items", "items1"])
 def whole_variant(request):
     from spacedrive_amd._native import lib
     assert lib().sd_cas_set_tuning(b"whole_variant", request.param) == 0
     yield request.param
-    lib().sd_cas_set_tuning(b"whole_variant", 3)  # the default
+    lib().sd_cas_set_tuning(b"whole_variant", 7)  # the default
 
 
 def test_cas_exhaustive_small_sizes(ctx, oracle_native, whole_variant):
