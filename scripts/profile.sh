@@ -7,7 +7,7 @@ TAG=${TAG:-r1}
 mkdir -p gpurun_out
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o trace \
-    -- python3 bench.py --steps 5 --warmup 1 --checksum-steps 2 --no-cpu-baseline --config-files 0 \
+    -- python3 bench.py --steps 5 --warmup 1 --checksum-steps 2 --no-cpu-baseline --config-files 0 --file-backed-files 0 \
     > gpurun_out/prof_bench_$TAG.json 2> gpurun_out/prof_bench_$TAG.err
 rc=$?; echo "trace rc=$rc"; if fatal $rc; then exit $rc; fi
 [ "${PMC:-1}" = "1" ] || exit 0
@@ -17,7 +17,7 @@ rc=$?; echo "calib rc=$rc"; if fatal $rc; then exit $rc; fi
 for C in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE"; do
   N=$(echo $C | cut -d' ' -f1)
   timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_${TAG}_$N -o pmc \
-      -- python3 bench.py --steps 1 --warmup 0 --checksum-steps 1 --no-cpu-baseline --config-files 0 \
+      -- python3 bench.py --steps 1 --warmup 0 --checksum-steps 1 --no-cpu-baseline --config-files 0 --file-backed-files 0 \
       > gpurun_out/pmc_${TAG}_$N.json 2> gpurun_out/pmc_${TAG}_$N.err
   rc=$?; echo "pmc $N rc=$rc"; if fatal $rc; then exit $rc; fi
 done
