@@ -37,6 +37,8 @@ def lib():
         L.sdo_synth_cas_message.restype = U64
         L.sdo_cas_ids_staged.argtypes = [P, P, U64, P, I]
         L.sdo_cas_ids_synth.argtypes = [P, P, P, U64, P, I]
+        L.sdo_cas_ids_synth_simd.argtypes = [P, P, P, U64, P, I, I]
+        L.sdo_cas_ids_synth_simd.restype = I
         L.sdo_checksums.argtypes = [P, P, P, U64, P, I]
         L.sdo_checksums_synth.argtypes = [P, P, P, U64, P, I]
         L.sdo_stage_synth.argtypes = [P, P, P, P, U64, P]
@@ -83,6 +85,17 @@ def cas_ids_synth(sizes, cids, twins=None, nthreads: int = 1) -> np.ndarray:
     tw = None if twins is None else np.ascontiguousarray(twins, np.uint32)
     out = np.empty((len(sizes), 8), np.uint8)
     lib().sdo_cas_ids_synth(_p(sizes), _p(cids), _p(tw), len(sizes), _p(out), nthreads)
+    return out
+
+
+def cas_ids_synth_simd(sizes, cids, twins=None, nthreads: int = 1, simd: int = -1) -> np.ndarray:
+    """cas_ids_synth with the SIMD hasher (itself checked against the scalar one in
+    tests/test_oracle.py) -- for library-scale parity runs."""
+    sizes = np.ascontiguousarray(sizes, np.uint64)
+    cids = np.ascontiguousarray(cids, np.uint64)
+    tw = None if twins is None else np.ascontiguousarray(twins, np.uint32)
+    out = np.empty((len(sizes), 8), np.uint8)
+    lib().sdo_cas_ids_synth_simd(_p(sizes), _p(cids), _p(tw), len(sizes), _p(out), nthreads, simd)
     return out
 
 

@@ -348,7 +348,13 @@ static void* worker(void* arg) {
             sdo_blake3(j->staged + j->ext[i].msg_offset, j->ext[i].msg_len, h);
         } else if (j->mode == MODE_CAS_SYNTH) {
             uint64_t m = sdo_synth_cas_message(j->cids[i], j->twins ? j->twins[i] : 0, j->sizes[i], scratch);
-            sdo_blake3(scratch, m, h);
+            if (j->simd) {
+                uint64_t need = 32 * ((m + 1023) / 1024 + 1);
+                if (need > cvs_cap) { free(cvs); cvs_cap = need * 2; cvs = (uint8_t*)malloc(cvs_cap); }
+                sdo_blake3_simd(scratch, m, h, j->simd, cvs);
+            } else {
+                sdo_blake3(scratch, m, h);
+            }
         } else if (j->mode == MODE_CHECKSUM) {
             sdo_blake3(j->data + j->offsets[i], j->lens[i], h);
         } else { /* hash.rs:14-20: 1 MiB reads streamed through one hasher */
@@ -412,6 +418,18 @@ void sdo_cas_ids_synth(const uint64_t* sizes, const uint64_t* cids, const uint32
     j.mode = MODE_CAS_SYNTH; j.n = n; j.sizes = sizes; j.cids = cids; j.twins = twins;
     j.out = out8; j.out_stride = 8;
     run_job(&j, nthreads);
+}
+
+/* the same with the SIMD multi-chunk hasher (library-scale parity runs: 10 M files);
+ * simd as in sdo_cas_ids_staged_simd.  Returns the level used. */
+int sdo_cas_ids_synth_simd(const uint64_t* sizes, const uint64_t* cids, const uint32_t* twins, uint64_t n,
+                           uint8_t* out8, int nthreads, int simd) {
+    job_t j = {0};
+    j.mode = MODE_CAS_SYNTH; j.n = n; j.sizes = sizes; j.cids = cids; j.twins = twins;
+    j.out = out8; j.out_stride = 8;
+    j.simd = simd == 0 ? 0 : sdo_simd_level(simd);
+    run_job(&j, nthreads);
+    return j.simd;
 }
 
 /* full 32-byte BLAKE3 of n byte ranges of one buffer */

@@ -471,3 +471,20 @@ def test_pipeline_object_owners_vs_reference_replay(ctx, oracle_native):
     cas = [None if sizes[i] == 0 else ids[i].tobytes().hex() for i in range(n)]
     want, _ = identifier_replay(cas)
     assert got.tolist() == want
+
+
+def test_library_pipeline_parity_sharded(ctx):
+    """scripts/parity_full.py at a reduced size: 4 shards of the library, cas_ids vs the
+    oracle, and the 4-rank dedup exchange emulated with device partitions + device
+    grouping vs the host grouping of the oracle's ids.  (The committed full-size run,
+    10 M files over 8 shards + configs[3], is profiles/r1d_parity_full.json.)"""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "parity_full", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
+                                    "parity_full.py"))
+    pf = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(pf)
+    r = pf.cas_library(ctx, 400_000, 4, NT)
+    assert r["cas_id_mismatches"] == 0, r["first_mismatches"]
+    assert r["dedup"]["bucket_record_mismatches"] == 0 and r["dedup"]["bucket_rep_mismatches"] == 0
+    assert r["dedup"]["duplicate_files"] > 0 and r["empty_files"] > 0

@@ -177,6 +177,18 @@ def test_c_oracle_simd_multichunk(oracle_native, level):
         assert oracle_native.checksums_simd(d, [0], [n], simd=level)[0].tobytes() == want, n
 
 
+@pytest.mark.parametrize("level", [1, 2])
+def test_c_oracle_simd_synth_cas_ids(oracle_native, level):
+    # the library-scale parity checker (SIMD hasher over generated messages) == scalar
+    if oracle_native.simd_level(level) != level:
+        pytest.skip("CPU lacks this SIMD level")
+    from spacedrive_amd import synth
+    sizes, cids, twins = synth.library(0, 4000, 4000)
+    want = oracle_native.cas_ids_synth(sizes, cids, twins, nthreads=4)
+    got = oracle_native.cas_ids_synth_simd(sizes, cids, twins, nthreads=4, simd=level)
+    assert np.array_equal(got, want)
+
+
 def test_c_oracle_file_backed_reads(oracle_native, tmp_path):
     """The reference's read schedule from files (cas.rs:27-58) equals the staged path;
     missing and short files map to IO_ERROR(ENOENT) and SHORT_READ."""
