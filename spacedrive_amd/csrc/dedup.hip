@@ -9,6 +9,8 @@
 // smallest file index of its equal-cas_id group (the Object-link candidate).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstring>
 #include <utility>
 
@@ -255,7 +257,10 @@ hipError_t dedup_group(uint64_t* records, uint64_t m, int flags, uint64_t* rep, 
     }
     e = rocprim::radix_sort_pairs(tmp, tb, keys, keys2, idx, idx2, (size_t)m, 0, 64, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_heads, dim3(grid_for(m)), dim3(256), 0, s, keys2, m, heads, n_groups_dev);
+    // grid-stride over at most 1024 workgroups: one global atomic per workgroup, so the
+    // count does not serialise ~m/256 atomics on one L2 line
+    hipLaunchKernelGGL(k_heads, dim3(std::min<unsigned>(grid_for(m), 1024u)), dim3(256), 0, s, keys2, m, heads,
+                       n_groups_dev);
     tb = temp;
     e = rocprim::inclusive_scan(tmp, tb, heads, keys, (size_t)m, rocprim::maximum<uint64_t>(), s);
     if (e != hipSuccess) return e;
