@@ -44,8 +44,10 @@ extern "C" {
 #define SD_MINIMUM_FILE_SIZE 102400u
 /* le64 header + head + 4 samples + tail */
 #define SD_SAMPLED_MSG_LEN 57352u
-/* staged messages start on this alignment and are zero-padded up to it */
-#define SD_STAGE_ALIGN 64u
+/* sd_cas_stage_plan starts staged messages on this alignment (one 128-byte cache line, so
+ * a lane's 2 KiB chunk pair is whole lines) and zero-pads them up to it.  The kernels need
+ * only 16-byte aligned offsets (sd_extent.msg_offset) and zero padding to a 64-byte boundary. */
+#define SD_STAGE_ALIGN 128u
 
 typedef enum sd_rc {
     SD_OK = 0,
@@ -72,7 +74,7 @@ typedef enum sd_kind {
 /* One file of a cas batch: where its hashed message sits in the staged buffer. 24 bytes. */
 typedef struct sd_extent {
     uint64_t size;       /* file size as passed to generate_cas_id (hashed as le64)  */
-    uint64_t msg_offset; /* byte offset of the message in the staged buffer (64-B aligned) */
+    uint64_t msg_offset; /* byte offset of the message in the staged buffer (16-B aligned) */
     uint32_t msg_len;    /* 8 + size (WHOLE) or 57352 (SAMPLED)                      */
     uint32_t kind;       /* sd_kind                                                  */
 } sd_extent;

@@ -25,7 +25,7 @@ RC_NAMES = {0: "SD_OK", -1: "SD_ERR_INVALID", -2: "SD_ERR_DEVICE", -3: "SD_ERR_N
 SD_FILE_OK, SD_FILE_SKIPPED_EMPTY, SD_FILE_IO_ERROR, SD_FILE_SHORT_READ = 0, 1, 2, 3
 SD_KIND_WHOLE, SD_KIND_SAMPLED = 1, 2
 SAMPLED_MSG_LEN = 57352
-STAGE_ALIGN = 64
+STAGE_ALIGN = 128
 
 
 class SdCasError(RuntimeError):

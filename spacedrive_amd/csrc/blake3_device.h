@@ -155,16 +155,35 @@ __device__ __forceinline__ void full_chunk_cv(uint32_t (&cv)[8], const uint8_t* 
     compress(cv, m, clo, chi, BLOCK_LEN, CHUNK_END);
 }
 
+// full_chunk_cv with line-pair loads (see full_chunks_cv, PF = 2)
+__device__ __forceinline__ void full_chunk_cv_lp(uint32_t (&cv)[8], const uint8_t* __restrict__ p,
+                                                 uint64_t counter) {
+    set_iv(cv);
+    const uint32_t clo = (uint32_t)counter, chi = (uint32_t)(counter >> 32);
+    uint32_t ma[16], mb[16];
+#pragma unroll 1
+    for (uint32_t b = 0; b < 16; b += 2) {
+        load_block(ma, p + 64u * b);
+        load_block(mb, p + 64u * (b + 1));
+        compress(cv, ma, clo, chi, BLOCK_LEN, b == 0 ? CHUNK_START : 0u);
+        compress(cv, mb, clo, chi, BLOCK_LEN, b == 14 ? CHUNK_END : 0u);
+    }
+}
+
 // Merge of U consecutive, full, non-root chunks c0..c0+U-1 (an aligned group, U = 1, 2, 4):
-// the chunk CVs merged level-wise in-lane -> `out`.  The message streams through two
-// register buffers: block k+1 is loaded while block k is compressed (PF = true), so a
-// lane always has one 64-byte load in flight behind its compression.
-template <int U, bool PF>
+// the chunk CVs merged level-wise in-lane -> `out`.  Message loads (PF):
+//   0  each block loaded just before its compression (other waves hide the latency);
+//   1  two register buffers: block k+1 is loaded while block k is compressed, so a lane
+//      always has one 64-byte load in flight behind its compression;
+//   2  line pairs: blocks 2k and 2k+1 -- one 128-byte cache line -- are loaded back to
+//      back into the two buffers, then both compressed, so a line is consumed whole
+//      instead of across a compression (fewer L2 re-fetches when many lanes stream).
+template <int U, int PF>
 __device__ __forceinline__ void full_chunks_cv(uint32_t (&out)[8], const uint8_t* __restrict__ p, uint64_t c0) {
     static_assert(U == 1 || U == 2 || U == 4, "U");
     uint32_t held[2][8];  // level-wise merge stack: at most two pending nodes for U <= 4
     uint32_t ma[16], mb[16];
-    if (PF) load_block(ma, p);
+    if (PF == 1) load_block(ma, p);
 #pragma unroll
     for (int u = 0; u < U; u++) {
         uint32_t cv[8];
@@ -176,7 +195,12 @@ __device__ __forceinline__ void full_chunks_cv(uint32_t (&out)[8], const uint8_t
         for (uint32_t b = 0; b < 16; b += 2) {
             const uint32_t f0 = b == 0 ? CHUNK_START : 0u;
             const uint32_t f1 = b + 1 == 15 ? CHUNK_END : 0u;
-            if (PF) {
+            if (PF == 2) {
+                load_block(ma, q + 64u * b);
+                load_block(mb, q + 64u * (b + 1));
+                compress(cv, ma, clo, chi, BLOCK_LEN, f0);
+                compress(cv, mb, clo, chi, BLOCK_LEN, f1);
+            } else if (PF == 1) {
                 load_block(mb, q + 64u * (b + 1));
                 compress(cv, ma, clo, chi, BLOCK_LEN, f0);
                 // next block: b + 2 of this chunk, or block 0 of the next chunk (the last

@@ -83,7 +83,7 @@ struct sampled_lds {
 };
 
 // one workgroup (blockIdx-independent: `wg` is its index among sampled workgroups)
-template <int U, bool PF>
+template <int U, int PF>
 __device__ __forceinline__ void sampled_wg(uint32_t wg, const uint8_t* __restrict__ staged,
                                            const sd_extent* __restrict__ ext, const uint32_t* __restrict__ idx,
                                            uint32_t n, uint32_t* __restrict__ out, sampled_lds<U>& sh) {
@@ -146,7 +146,7 @@ __device__ __forceinline__ void sampled_wg(uint32_t wg, const uint8_t* __restric
     }
 }
 
-template <int U, bool PF>
+template <int U, int PF>
 __global__ __launch_bounds__(S_THREADS) void k_cas_sampled(const uint8_t* __restrict__ staged,
                                                            const sd_extent* __restrict__ ext,
                                                            const uint32_t* __restrict__ idx,
@@ -315,7 +315,7 @@ union mixed_lds {
     whole_lds w;
 };
 
-template <int U, bool PF, bool PAIRPF>
+template <int U, int PF, bool PAIRPF>
 __global__ __launch_bounds__(S_THREADS) void k_cas_mixed(const uint8_t* __restrict__ staged,
                                                          const sd_extent* __restrict__ ext,
                                                          const uint32_t* __restrict__ sidx, uint32_t n_sampled,
@@ -493,6 +493,7 @@ __global__ __launch_bounds__(256) void k_whole_tail(const uint8_t* __restrict__ 
 // (a workgroup-uniform branch).  The tail path hashes its chunks one after the other
 // without the prefetch buffer, so the kernel keeps the full path's register budget
 // (8 waves/SIMD), and its latency-bound lanes run while the last full-pair waves drain.
+template <int PF>  // full-pair message loads, as full_chunks_cv (1: prefetch, 2: line pairs)
 __global__ __launch_bounds__(256) void k_whole_items(const uint8_t* __restrict__ staged,
                                                      const uint4* __restrict__ full, uint32_t n_full, uint32_t wf,
                                                      const uint4* __restrict__ tail, uint32_t n_tail,
@@ -503,7 +504,7 @@ __global__ __launch_bounds__(256) void k_whole_items(const uint8_t* __restrict__
         const uint4 it = full[g];
         const uint64_t off = (uint64_t)it.x | ((uint64_t)it.y << 32);
         uint32_t cv[8];
-        full_chunks_cv<2, true>(cv, staged + off, it.w);
+        full_chunks_cv<2, PF>(cv, staged + off, it.w);
         store_cv(cvbuf + (size_t)it.z * 8, cv);
         return;
     }
@@ -566,6 +567,7 @@ __global__ __launch_bounds__(256) void k_whole_merge8(const uint4* __restrict__ 
 constexpr uint32_t CK_LANE_CHUNKS = 4;
 constexpr uint32_t CK_BLOCK_CHUNKS = 1024;
 
+template <bool LP>  // LP: full chunks with line-pair loads (checksum_variant 1)
 __global__ __launch_bounds__(256) void k_ck_leaf(const uint8_t* __restrict__ data, uint64_t shift,
                                                  const ck_file* __restrict__ files,
                                                  const uint2* __restrict__ wg_map,
@@ -588,7 +590,10 @@ __global__ __launch_bounds__(256) void k_ck_leaf(const uint8_t* __restrict__ dat
             const uint64_t ci = blk0 + c0 + j;
             const uint64_t rem = fi.len - ci * CHUNK_LEN;
             const uint32_t len = fi.len == 0 ? 0u : (rem < CHUNK_LEN ? (uint32_t)rem : CHUNK_LEN);
-            if (len == CHUNK_LEN && !(file_is_lane && nchunks == 1)) full_chunk_cv(cv, p + ci * CHUNK_LEN, ci);
+            if (len == CHUNK_LEN && !(file_is_lane && nchunks == 1)) {
+                if (LP) full_chunk_cv_lp(cv, p + ci * CHUNK_LEN, ci);
+                else full_chunk_cv(cv, p + ci * CHUNK_LEN, ci);
+            }
             else chunk_cv(cv, p + ci * CHUNK_LEN, len, ci, nchunks == 1);
             // level-wise in-lane merge of up to 4 chunks: ((0,1),(2,3)) or ((0,1),2)
             if (j == 0) {
@@ -664,7 +669,10 @@ hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const
         case 10: SD_LAUNCH_SAMPLED(1, false); break;
         case 11: SD_LAUNCH_SAMPLED(1, true); break;
         case 20: SD_LAUNCH_SAMPLED(2, false); break;
-        case 21: SD_LAUNCH_SAMPLED(2, true); break;
+        case 21: SD_LAUNCH_SAMPLED(2, 1); break;
+        case 22: SD_LAUNCH_SAMPLED(2, 2); break;
+        case 12: SD_LAUNCH_SAMPLED(1, 2); break;
+        case 42: SD_LAUNCH_SAMPLED(4, 2); break;
         case 40: SD_LAUNCH_SAMPLED(4, false); break;
         default: SD_LAUNCH_SAMPLED(4, true); break;
     }
@@ -753,12 +761,16 @@ hipError_t launch_whole(const uint8_t* staged, const sd_extent* ext, const uint3
 
 hipError_t launch_whole_items(const uint8_t* staged, const uint4* full, uint32_t n_full, const uint4* tail,
                               uint32_t n_tail, const uint4* merge_a, uint32_t n_a, const uint4* merge_b, uint32_t n_b,
-                              uint32_t* cvbuf, uint32_t* cv2, uint32_t* out, hipStream_t s, bool combined) {
+                              uint32_t* cvbuf, uint32_t* cv2, uint32_t* out, hipStream_t s, bool combined, int pf) {
     if (combined) {
         const uint32_t wf = (n_full + 255) / 256, wt = (n_tail + 255) / 256;
-        if (wf + wt)
-            hipLaunchKernelGGL(k_whole_items, dim3(wf + wt), dim3(256), (size_t)tuning_get(SD_TUNE_WHOLE_LDS_KB) << 10, s,
-                               staged, full, n_full, wf, tail, n_tail, cvbuf, out);
+        const size_t lds = (size_t)tuning_get(SD_TUNE_WHOLE_LDS_KB) << 10;
+        if (wf + wt && pf == 2)
+            hipLaunchKernelGGL(k_whole_items<2>, dim3(wf + wt), dim3(256), lds, s, staged, full, n_full, wf, tail,
+                               n_tail, cvbuf, out);
+        else if (wf + wt)
+            hipLaunchKernelGGL(k_whole_items<1>, dim3(wf + wt), dim3(256), lds, s, staged, full, n_full, wf, tail,
+                               n_tail, cvbuf, out);
     } else {
         if (n_full)
             hipLaunchKernelGGL(k_whole_full, dim3((n_full + 255) / 256), dim3(256), 0, s, staged, full, n_full, cvbuf);
@@ -778,7 +790,10 @@ hipError_t launch_whole_items(const uint8_t* staged, const uint4* full, uint32_t
 hipError_t launch_ck_leaf(const uint8_t* data, uint64_t shift, const ck_file* files, const uint2* wg_map,
                           uint32_t n_wg, uint32_t* cvbuf, uint32_t* out, hipStream_t s) {
     if (n_wg == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ck_leaf, dim3(n_wg), dim3(256), 0, s, data, shift, files, wg_map, cvbuf, out);
+    if (tuning_get(SD_TUNE_CK_VARIANT) == 1)
+        hipLaunchKernelGGL(k_ck_leaf<true>, dim3(n_wg), dim3(256), 0, s, data, shift, files, wg_map, cvbuf, out);
+    else
+        hipLaunchKernelGGL(k_ck_leaf<false>, dim3(n_wg), dim3(256), 0, s, data, shift, files, wg_map, cvbuf, out);
     return hipGetLastError();
 }
 

@@ -347,7 +347,7 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
     uint64_t end = 0;
     for (size_t i = 0; i < n; i++) {
         validate_extent(ext[i], i);
-        end = std::max<uint64_t>(end, align_up(ext[i].msg_offset + ext[i].msg_len, SD_STAGE_ALIGN));
+        end = std::max<uint64_t>(end, align_up(ext[i].msg_offset + ext[i].msg_len, SD_STAGE_PAD));
         b->msg_bytes += ext[i].msg_len;
         if (ext[i].kind == SD_KIND_SAMPLED) {
             sidx.push_back((uint32_t)i);
@@ -481,7 +481,8 @@ void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_ha
                                         wv == 4));
         return;
     }
-    if (wv == 6 || wv == 7) {  // sampled kernel; full-pair / cost-sorted tail-pair items (7: one launch); two merge8 passes
+    if (wv == 6 || wv == 7 || wv == 8) {  // sampled kernel; full-pair / cost-sorted tail-pair items (7, 8: one
+                                          // launch; 8: line-pair loads); two merge8 passes
         if (parts & SD_PART_SAMPLED)
             HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled,
                                               out, s));
@@ -489,7 +490,7 @@ void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_ha
             HIP_CHECK(sdk::launch_whole_items(d_staged, b->full_items.as<uint4>(), b->n_full, b->tail_items.as<uint4>(),
                                               b->n_tail, b->merge_a.as<uint4>(), b->n_merge_a, b->merge_b.as<uint4>(),
                                               b->n_merge_b, b->cvbuf.as<uint32_t>(), b->cv2.as<uint32_t>(), out, s,
-                                              wv == 7));
+                                              wv >= 7, wv == 8 ? 2 : 1));
         return;
     }
     if (wv == 3 || wv == 5) {  // sampled kernel; prefetching pair leaf + tree (3) / LDS forest (5) over pair nodes
@@ -665,12 +666,12 @@ int32_t pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
 }
 
 // Reads one file into its extent exactly as generate_cas_id does (cas.rs:25-58) and
-// zero-pads the message to SD_STAGE_ALIGN.  Returns an sd_file_status.
+// zero-pads the message to SD_STAGE_PAD.  Returns an sd_file_status.
 int32_t stage_one(const char* path, const sd_extent& e, uint8_t* staged) {
     uint8_t* dst = staged + e.msg_offset;
     const uint64_t size = e.size;
     for (int i = 0; i < 8; i++) dst[i] = (uint8_t)(size >> (8 * i));  // cas.rs:25 le64
-    const uint64_t padded = align_up(e.msg_len, SD_STAGE_ALIGN);
+    const uint64_t padded = align_up(e.msg_len, SD_STAGE_PAD);
     memset(dst + e.msg_len, 0, padded - e.msg_len);
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) return io_status(errno);
@@ -704,7 +705,9 @@ int32_t stage_one(const char* path, const sd_extent& e, uint8_t* staged) {
 
 // ------------------------------------------------------------------ tuning knobs
 #include <atomic>
-static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{21}, {7}, {0}, {200}, {4096}, {32}, {0}};
+// defaults: sampled U = 2 with line-pair loads (22), whole-file work lists in one launch
+// with line-pair loads (8), checksum leaf with line-pair loads (1) -- DESIGN.md §7
+static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{22}, {8}, {1}, {200}, {4096}, {32}, {0}};
 int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
 
 // ============================================================================ C ABI
@@ -925,7 +928,7 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
         while (gj < live.size()) {
             const sd_extent& e = extents[live[gj]];
             const uint64_t nlo = std::min(lo, e.msg_offset);
-            const uint64_t nhi = std::max(hi, align_up(e.msg_offset + e.msg_len, SD_STAGE_ALIGN));
+            const uint64_t nhi = std::max(hi, align_up(e.msg_offset + e.msg_len, SD_STAGE_PAD));
             if (gj > gi && nhi - nlo > WINDOW) break;
             lo = nlo;
             hi = nhi;

@@ -34,6 +34,10 @@ enum sd_tune_key {
     SD_TUNE_NKEYS = 7
 };
 int tuning_get(int key);
+// What the kernels need of a staged message: a 16-byte aligned start (validate_extent) and
+// zero padding up to the next 64-byte boundary.  The planner places messages on
+// SD_STAGE_ALIGN (128, whole cache lines) but callers' own layouts only need this.
+constexpr uint64_t SD_STAGE_PAD = 64;
 
 // latency path (coalesce.cpp)
 #include <string>
@@ -66,7 +70,7 @@ hipError_t launch_whole(const uint8_t* staged, const sd_extent* ext, const uint3
 // variant 6: full-pair items, cost-sorted tail items, two merge8 passes (cv2 = pass-A output)
 hipError_t launch_whole_items(const uint8_t* staged, const uint4* full, uint32_t n_full, const uint4* tail,
                               uint32_t n_tail, const uint4* merge_a, uint32_t n_a, const uint4* merge_b, uint32_t n_b,
-                              uint32_t* cvbuf, uint32_t* cv2, uint32_t* out, hipStream_t s, bool combined);
+                              uint32_t* cvbuf, uint32_t* cv2, uint32_t* out, hipStream_t s, bool combined, int pf);
 hipError_t launch_ck_leaf(const uint8_t* data, uint64_t shift, const ck_file* files, const uint2* wg_map,
                           uint32_t n_wg, uint32_t* cvbuf, uint32_t* out, hipStream_t s);
 hipError_t launch_ck_reduce(const uint32_t* src, uint32_t* dst, const ck_reduce_wg* wgs, uint32_t n_wg,

@@ -120,13 +120,13 @@ def test_sd_cas_ids_pipelined_windows(ctx):
             assert status[i] == 0 and raw[17 * i:17 * i + 16].decode() == h[i, :8].tobytes().hex(), i
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7],
-                ids=["fused", "split", "side-stream", "pair-leaf", "fused-pair", "pair-forest", "items", "items1"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, 8],
+                ids=["fused", "split", "side-stream", "pair-leaf", "fused-pair", "pair-forest", "items", "items1", "items1-lines"])
 def whole_variant(request):
     from spacedrive_amd._native import lib
     assert lib().sd_cas_set_tuning(b"whole_variant", request.param) == 0
     yield request.param
-    lib().sd_cas_set_tuning(b"whole_variant", 7)  # the default
+    lib().sd_cas_set_tuning(b"whole_variant", 8)  # the default
 
 
 def test_cas_exhaustive_small_sizes(ctx, oracle_native, whole_variant):
@@ -164,7 +164,7 @@ def test_cas_configs0_full_size_and_idempotent(ctx, oracle_native, whole_variant
     assert np.array_equal(h1[:, :8], ids)
 
 
-@pytest.mark.parametrize("variant", [10, 11, 20, 21, 40, 41])
+@pytest.mark.parametrize("variant", [10, 11, 12, 20, 21, 22, 40, 41, 42])
 def test_cas_sampled_variants_and_batch_shapes(ctx, oracle_native, variant):
     # every sampled-kernel variant (U chunks per lane, prefetch) is bit-exact, including
     # partial last workgroups of 8U files
@@ -177,7 +177,7 @@ def test_cas_sampled_variants_and_batch_shapes(ctx, oracle_native, variant):
             h = gpu_cas(ctx, sizes, cids, np.zeros(n, np.uint32))
             assert np.array_equal(h[:, :8], oracle_native.cas_ids_synth(sizes, cids, nthreads=NT)), n
     finally:
-        lib().sd_cas_set_tuning(b"sampled_variant", 41)
+        lib().sd_cas_set_tuning(b"sampled_variant", 22)  # the default
 
 
 def test_sample_twins_and_duplicates(ctx):
@@ -214,7 +214,15 @@ def test_checksum_goldens(ctx, golden):
         assert row.tobytes().hex() == f["checksum"], f
 
 
-def test_checksum_sizes_vs_oracle(ctx, oracle_native):
+@pytest.fixture(params=[0, 1], ids=["ck-seq", "ck-lines"])
+def checksum_variant(request):
+    from spacedrive_amd._native import lib
+    assert lib().sd_cas_set_tuning(b"checksum_variant", request.param) == 0
+    yield request.param
+    lib().sd_cas_set_tuning(b"checksum_variant", 1)  # the default
+
+
+def test_checksum_sizes_vs_oracle(ctx, oracle_native, checksum_variant):
     MiB = 1 << 20
     lens = [0, 1, 1024, 1025, 4096, 4097, 5 * 1024, MiB - 1, MiB, MiB + 1, 4 * MiB + 3, 7 * MiB,
             256 * MiB, 256 * MiB + 1, 300 * MiB + 17, 3 * 1024 + 1, 1020 * 1024 + 5]
