@@ -7,7 +7,7 @@ TAG=${TAG:-r1}
 mkdir -p gpurun_out
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o trace \
-    -- python3 bench.py --steps 5 --warmup 1 --checksum-steps 2 --no-cpu-baseline --config-files 0 --file-backed-files 0 \
+    -- python3 bench.py --steps 20 --warmup 3 --checksum-steps 5 --no-cpu-baseline --config-files 0 --file-backed-files 0 \
     > gpurun_out/prof_bench_$TAG.json 2> gpurun_out/prof_bench_$TAG.err
 rc=$?; echo "trace rc=$rc"; if fatal $rc; then exit $rc; fi
 [ "${PMC:-1}" = "1" ] || exit 0

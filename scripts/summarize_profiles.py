@@ -19,9 +19,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
 CALIB_BYTES = 4 << 30
-CMD = os.environ.get("PROF_CMD", "python3 bench.py --steps 5 --warmup 1 --checksum-steps 2 --no-cpu-baseline "
+CMD = os.environ.get("PROF_CMD", "python3 bench.py --steps 20 --warmup 3 --checksum-steps 5 --no-cpu-baseline "
                                     "--config-files 0 --file-backed-files 0")
-WARMUP = int(os.environ.get("PROF_WARMUP", "1"))
+WARMUP = int(os.environ.get("PROF_WARMUP", "3"))
 
 
 def short(name):
