@@ -218,17 +218,19 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
                            uint8_t* d_hash32, int iters, void* stream, float* ms_total);
 /* Process-wide kernel-variant knobs for A/B measurement (results are identical for
  * every value): "sampled_variant" = 10*U + prefetch with U in {1,2,4} chunks per lane
- * (default 21); "whole_variant" 0 = one fused launch (sampled workgroups + whole-file
+ * and prefetch 0/1/2 (2 = line-pair loads; default 22); "whole_variant" 0 = one fused launch (sampled workgroups + whole-file
  * groups with LDS trees), 1 = separate sampled / whole-leaf / whole-tree kernels, 2 = whole-leaf, then the sampled kernel beside the whole-tree kernel on a
  * batch-internal side stream (joined back into `stream`), 3 = sampled kernel + prefetching
  * chunk-pair leaf + tree over pair nodes, 4 = variant 0 with prefetching chunk-pair leaves,
  * 5 = variant 3 with the pair-node trees merged level-wise in LDS (k_whole_forest),
  * 6 = sampled kernel + host-built work lists: full chunk pairs (k_whole_full), cost-sorted
  * partial/short pairs (k_whole_tail), then two level-wise merge passes of <= 8 nodes per
- * lane (k_whole_merge8), 7 = variant 6 with both pair lists in one launch (k_whole_items,
- * default); "whole_lds_kb" = dynamic LDS per k_whole_items workgroup (occupancy A/B, 0);
- * "checksum_variant" (default 0); "coalesce_window_us" / "coalesce_max" (latency path);
- * "files_window_mb" (sd_cas_ids_files). */
+ * lane (k_whole_merge8), 7 = variant 6 with both pair lists in one launch (k_whole_items),
+ * 8 = variant 7 with line-pair loads (default); "whole_lds_kb" = dynamic LDS per
+ * k_whole_items workgroup (occupancy A/B, 0); "checksum_variant" 0/1 (1 = line-pair
+ * loads, default); "dedup_variant" (sd_dedup_group) 0 = rocPRIM radix sort, 1 = LDS
+ * buckets with the radix sort as overflow fallback (default); "coalesce_window_us" /
+ * "coalesce_max" (latency path); "files_window_mb" (sd_cas_ids_files). */
 int sd_cas_set_tuning(const char* key, int value);
 /* Read-only probe over d_buf[0, bytes) (bytes a multiple of 4096) for calibrating the
  * PMC byte counters on this kernel family's access patterns: pattern 0 = coalesced

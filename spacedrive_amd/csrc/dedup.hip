@@ -199,6 +199,180 @@ uint32_t grid_for(uint64_t n) {
     return (uint32_t)g;
 }
 
+// ------------------------------------------------- bucket grouping (dedup_variant 1)
+// cas_ids are uniform hash bits, so an order-preserving split of the key range into
+// nb = 2^lg buckets -- (key - kmin) >> shift -- leaves ~m/nb records per bucket, and equal
+// keys share a bucket, so every group lies inside one.  The records are bucketed by a
+// radix sort of the lg-bit bucket numbers alone (2-3 passes of u32 pairs instead of 8
+// passes of u64 pairs), then each bucket is sorted by (key, index) in LDS by one wave: a
+// rank sort that also yields each record's group minimum (the representative) and
+// whether it heads its group.  No global atomics on the data path: partial results go to
+// per-workgroup slots reduced by one small workgroup.  A bucket larger than GB_CAP (a
+// duplicate group of hundreds of files) is copied through unsorted and flags `overflow`;
+// the caller then runs the radix path over the permuted records.
+constexpr uint32_t GB_CAP = 512;
+constexpr uint32_t GB_WAVES = 4;  // buckets per workgroup, one per wave
+constexpr uint32_t GB_MM_BLOCKS = 512;
+
+struct gb_state {
+    unsigned long long ngroups, overflow, kmin, kmax, shift;
+};
+
+// per-workgroup key minimum / maximum -> part[2 * blockIdx.x + {0, 1}]
+__global__ __launch_bounds__(256) void k_gb_minmax(const uint64_t* __restrict__ rec, uint64_t m,
+                                                   uint64_t* __restrict__ part) {
+    __shared__ uint64_t slo[4], shi[4];
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = rec[2 * i];
+        lo = k < lo ? k : lo;
+        hi = k > hi ? k : hi;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { slo[w] = lo; shi[w] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t k = 1; k < blockDim.x / 64; k++) {
+            lo = slo[k] < lo ? slo[k] : lo;
+            hi = shi[k] > hi ? shi[k] : hi;
+        }
+        part[2 * blockIdx.x] = lo;
+        part[2 * blockIdx.x + 1] = hi;
+    }
+}
+
+// one workgroup of 64: reduce the partials, fix the bucket shift, clear the counters
+__global__ __launch_bounds__(64) void k_gb_final(const uint64_t* __restrict__ part, uint32_t np, uint32_t lg,
+                                                 gb_state* st) {
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint32_t i = threadIdx.x; i < np; i += 64) {
+        lo = part[2 * i] < lo ? part[2 * i] : lo;
+        hi = part[2 * i + 1] > hi ? part[2 * i + 1] : hi;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if (threadIdx.x == 0) {
+        const uint64_t span = hi - lo;
+        const uint32_t bits = span ? 64u - (uint32_t)__builtin_clzll(span) : 0u;
+        st->kmin = lo;
+        st->kmax = hi;
+        st->shift = bits > lg ? bits - lg : 0u;  // lg >= 1, so shift <= 63
+        st->ngroups = 0;
+        st->overflow = 0;
+    }
+}
+
+// a copy of the records (the output overwrites them) + the bucket number of each and its position
+__global__ __launch_bounds__(256) void k_gb_split(const uint4* __restrict__ rec, uint64_t m, const gb_state* st,
+                                                  uint4* __restrict__ copy, uint32_t* __restrict__ bk,
+                                                  uint32_t* __restrict__ pos) {
+    const uint64_t kmin = st->kmin;
+    const uint32_t sh = (uint32_t)st->shift;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 r = rec[i];
+        copy[i] = r;
+        bk[i] = (uint32_t)(((((uint64_t)r.y << 32) | r.x) - kmin) >> sh);
+        pos[i] = (uint32_t)i;
+    }
+}
+
+// bucket b occupies sorted slots [offs[b], offs[b + 1]) (offs[nb] = m)
+__global__ __launch_bounds__(256) void k_gb_bounds(const uint32_t* __restrict__ bk, uint64_t m, uint32_t nb,
+                                                   uint32_t* __restrict__ offs) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t cur = bk[i];
+        const uint32_t first = i == 0 ? 0u : bk[i - 1] + 1u;
+        for (uint32_t b = first; b <= cur; b++) offs[b] = (uint32_t)i;
+        if (i + 1 == m)
+            for (uint32_t b = cur + 1; b <= nb; b++) offs[b] = (uint32_t)m;
+    }
+}
+
+__device__ __forceinline__ uint64_t lo64(const uint4& v) { return ((uint64_t)v.y << 32) | v.x; }
+__device__ __forceinline__ uint64_t hi64(const uint4& v) { return ((uint64_t)v.w << 32) | v.z; }
+
+// One wave per bucket: rank of record e = number of records ordered before it by
+// (key, index, slot); its representative = the smallest index with an equal key; it heads
+// its group when no equal-key record precedes it.  Head counts -> heads[blockIdx.x].
+__global__ __launch_bounds__(64 * GB_WAVES) void k_gb_sort(const uint4* __restrict__ copy,
+                                                           const uint32_t* __restrict__ pos,
+                                                           const uint32_t* __restrict__ offs, uint32_t nb,
+                                                           uint4* __restrict__ rec, uint64_t* __restrict__ rep,
+                                                           uint32_t* __restrict__ heads, gb_state* st) {
+    __shared__ uint4 sr[GB_WAVES][GB_CAP];  // (key, index) per record
+    __shared__ uint32_t wh[GB_WAVES];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t b = blockIdx.x * GB_WAVES + w;
+    uint32_t h = 0;
+    if (b < nb) {
+        const uint32_t lo = offs[b], s = offs[b + 1] - lo;
+        if (s > GB_CAP) {  // copied through unsorted; the caller re-sorts everything
+            for (uint32_t e = lane; e < s; e += 64) rec[lo + e] = copy[pos[lo + e]];
+            if (lane == 0) st->overflow = 1;
+        } else {
+            uint4* r_ = sr[w];
+            for (uint32_t e = lane; e < s; e += 64) r_[e] = copy[pos[lo + e]];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t e = lane; e < s; e += 64) {
+                const uint4 me = r_[e];
+                const uint64_t k = lo64(me), id = hi64(me);
+                uint32_t rank = 0, eq_before = 0;
+                uint64_t mn = id;
+#pragma unroll 4
+                for (uint32_t j = 0; j < s; j++) {
+                    const uint4 o = r_[j];
+                    const uint64_t kj = lo64(o), ij = hi64(o);
+                    const bool eq = kj == k;
+                    const bool before = kj < k || (eq && (ij < id || (ij == id && j < e)));
+                    rank += before;
+                    eq_before += eq && before;
+                    mn = (eq && ij < mn) ? ij : mn;
+                }
+                rec[lo + rank] = me;
+                rep[lo + rank] = mn;
+                h += eq_before == 0;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+    if (lane == 0) wh[w] = h;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t k = 0; k < GB_WAVES; k++) t += wh[k];
+        heads[blockIdx.x] = t;
+    }
+}
+
+// one workgroup of 1024: group count = sum of the per-workgroup head counts
+__global__ __launch_bounds__(1024) void k_gb_sum(const uint32_t* __restrict__ heads, uint32_t n, gb_state* st) {
+    __shared__ unsigned long long ws[16];
+    unsigned long long v = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) v += heads[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int k = 0; k < 16; k++) t += ws[k];
+        st->ngroups = t;
+    }
+}
+
 }  // namespace
 
 namespace sdk {
@@ -265,6 +439,64 @@ hipError_t dedup_group(uint64_t* records, uint64_t m, int flags, uint64_t* rep, 
     e = rocprim::inclusive_scan(tmp, tb, heads, keys, (size_t)m, rocprim::maximum<uint64_t>(), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_join, dim3(grid_for(m)), dim3(256), 0, s, keys2, idx2, keys, m, records, rep);
+    return hipGetLastError();
+}
+
+static uint32_t gb_lg(uint64_t m) {  // nb = 2^lg >= m / 48: ~24-48 records per bucket; lg >= 1
+    uint32_t lg = 1;                  // keeps the bucket shift (bit length of the span - lg) < 64
+    while (lg < 24 && ((uint64_t)48 << lg) < m) lg++;
+    return lg;
+}
+
+static size_t gb_sort_bytes(uint64_t m, uint32_t lg, hipStream_t s) {
+    size_t b = 0;
+    uint32_t* nul = nullptr;
+    if (rocprim::radix_sort_pairs(nullptr, b, nul, nul, nul, nul, (size_t)m, 0, lg, s) != hipSuccess) return 0;
+    return (b + 255) & ~size_t(255);
+}
+
+// scratch: copy[m] (16-B records), bk, bk2, pos, pos2 [m] (u32), offs[nb + 1], heads[nb / 4 + 1],
+// minmax partials, then the radix sort's temporary storage
+static size_t gb_layout_bytes(uint64_t m, uint32_t nb) {
+    size_t b = 2 * m * sizeof(uint64_t) + 4 * m * sizeof(uint32_t) + (nb + 1 + nb / GB_WAVES + 1) * sizeof(uint32_t);
+    b = (b + 15) & ~size_t(15);
+    b += 2 * GB_MM_BLOCKS * sizeof(uint64_t);
+    return (b + 255) & ~size_t(255);
+}
+
+size_t dedup_group_buckets_scratch(uint64_t m) {
+    const uint32_t lg = gb_lg(m);
+    return gb_layout_bytes(m, 1u << lg) + gb_sort_bytes(m, lg, nullptr) + 256;
+}
+
+// state: 5 u64 (ngroups, overflow, kmin, kmax, shift); 0 < m < 2^31
+hipError_t dedup_group_buckets(uint64_t* records, uint64_t m, uint64_t* rep, uint64_t* state, void* scratch,
+                               size_t scratch_bytes, hipStream_t s) {
+    if (m == 0 || m >= (1ull << 31) || scratch_bytes < dedup_group_buckets_scratch(m)) return hipErrorInvalidValue;
+    const uint32_t lg = gb_lg(m), nb = 1u << lg, n_wg = (nb + GB_WAVES - 1) / GB_WAVES;
+    auto* st = reinterpret_cast<gb_state*>(state);
+    uint8_t* base = reinterpret_cast<uint8_t*>(((uintptr_t)scratch + 255) & ~uintptr_t(255));
+    uint4* copy = reinterpret_cast<uint4*>(base);
+    uint32_t* bk = reinterpret_cast<uint32_t*>(copy + m);
+    uint32_t* bk2 = bk + m;
+    uint32_t* pos = bk2 + m;
+    uint32_t* pos2 = pos + m;
+    uint32_t* offs = pos2 + m;  // nb + 1
+    uint32_t* heads = offs + nb + 1;
+    uint64_t* part = reinterpret_cast<uint64_t*>(((uintptr_t)(heads + n_wg) + 15) & ~uintptr_t(15));
+    void* tmp = base + gb_layout_bytes(m, nb);
+    size_t tb = gb_sort_bytes(m, lg, s);
+    const uint32_t g = std::min<unsigned>(grid_for(m), GB_MM_BLOCKS);
+    hipLaunchKernelGGL(k_gb_minmax, dim3(g), dim3(256), 0, s, records, m, part);
+    hipLaunchKernelGGL(k_gb_final, dim3(1), dim3(64), 0, s, part, g, lg, st);
+    hipLaunchKernelGGL(k_gb_split, dim3(grid_for(m)), dim3(256), 0, s, reinterpret_cast<const uint4*>(records), m, st,
+                       copy, bk, pos);
+    hipError_t e = rocprim::radix_sort_pairs(tmp, tb, bk, bk2, pos, pos2, (size_t)m, 0, lg, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_gb_bounds, dim3(grid_for(m)), dim3(256), 0, s, bk2, m, nb, offs);
+    hipLaunchKernelGGL(k_gb_sort, dim3(n_wg), dim3(64 * GB_WAVES), 0, s, copy, pos2, offs, nb,
+                       reinterpret_cast<uint4*>(records), rep, heads, st);
+    hipLaunchKernelGGL(k_gb_sum, dim3(1), dim3(1024), 0, s, heads, n_wg, st);
     return hipGetLastError();
 }
 

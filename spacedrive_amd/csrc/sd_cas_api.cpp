@@ -706,8 +706,9 @@ int32_t stage_one(const char* path, const sd_extent& e, uint8_t* staged) {
 // ------------------------------------------------------------------ tuning knobs
 #include <atomic>
 // defaults: sampled U = 2 with line-pair loads (22), whole-file work lists in one launch
-// with line-pair loads (8), checksum leaf with line-pair loads (1) -- DESIGN.md §7
-static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{22}, {8}, {1}, {200}, {4096}, {32}, {0}};
+// with line-pair loads (8), checksum leaf with line-pair loads (1), LDS-bucket dedup
+// grouping (1) -- DESIGN.md §7
+static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{22}, {8}, {1}, {200}, {4096}, {32}, {0}, {1}};
 int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
 
 // ============================================================================ C ABI
@@ -718,7 +719,7 @@ int sd_cas_set_tuning(const char* key, int value) {
     if (!key) throw sd_failure(SD_ERR_INVALID, "null key");
     static const char* names[SD_TUNE_NKEYS] = {"sampled_variant", "whole_variant", "checksum_variant",
                                                "coalesce_window_us", "coalesce_max", "files_window_mb",
-                                               "whole_lds_kb"};
+                                               "whole_lds_kb", "dedup_variant"};
     for (int k = 0; k < SD_TUNE_NKEYS; k++)
         if (strcmp(key, names[k]) == 0) {
             g_tune[k].store(value, std::memory_order_relaxed);
@@ -1303,10 +1304,23 @@ int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, int flags, 
         std::unique_ptr<Slot>* s;
         ~Rel() { c->release(std::move(*s)); }
     } rel{ctx, &slot};
+    const bool buckets = tuning_get(SD_TUNE_DEDUP_VARIANT) == 1 && m > 0 && m < (1ull << 31);
+    if (buckets) need = std::max(need, sdk::dedup_group_buckets_scratch(m));
     slot->staged.ensure(need);
-    slot->hashes.ensure(sizeof(uint64_t));
-    slot->host_hashes.ensure(sizeof(uint64_t));
+    slot->hashes.ensure(8 * sizeof(uint64_t));
+    slot->host_hashes.ensure(2 * sizeof(uint64_t));
     size_t have = slot->staged.bytes;
+    if (buckets) {
+        HIP_CHECK(sdk::dedup_group_buckets(d_records, m, d_rep, slot->hashes.as<uint64_t>(), slot->staged.p, have, s));
+        HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, slot->hashes.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        const uint64_t* st = reinterpret_cast<const uint64_t*>(slot->host_hashes.p);
+        if (st[1] == 0) {
+            *n_groups = st[0];
+            return SD_OK;
+        }
+        flags &= ~SD_DEDUP_INDEX_SORTED;  // a bucket overflowed: d_records is now a permutation
+    }
     HIP_CHECK(sdk::dedup_group(d_records, m, flags, d_rep, slot->hashes.as<uint64_t>(), slot->staged.p, &have, s));
     HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, slot->hashes.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));

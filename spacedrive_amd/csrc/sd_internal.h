@@ -31,7 +31,8 @@ enum sd_tune_key {
     SD_TUNE_COALESCE_MAX = 4,
     SD_TUNE_FILES_WINDOW_MB = 5,
     SD_TUNE_WHOLE_LDS_KB = 6,  // dynamic LDS per k_whole_items workgroup (occupancy A/B; 0 = none)
-    SD_TUNE_NKEYS = 7
+    SD_TUNE_DEDUP_VARIANT = 7,  // sd_dedup_group: 0 = radix sort, 1 = LDS buckets (radix on overflow)
+    SD_TUNE_NKEYS = 8
 };
 int tuning_get(int key);
 // What the kernels need of a staged message: a 16-byte aligned start (validate_extent) and
@@ -87,4 +88,11 @@ hipError_t dedup_partition(const uint8_t* hash32, const uint8_t* valid, uint64_t
 size_t dedup_partition_scratch(int nparts);
 hipError_t dedup_group(uint64_t* records, uint64_t m, int flags, uint64_t* rep, uint64_t* n_groups_dev,
                        void* scratch, size_t* scratch_bytes, hipStream_t s);
+// bucket grouping (dedup_variant 1): same outputs as dedup_group for m < 2^31 unless
+// state[1] (overflow) comes back nonzero -- then records hold a permutation of the input
+// and dedup_group (without SD_DEDUP_INDEX_SORTED) must run.  state: 5 device u64, state[0]
+// = the group count.
+size_t dedup_group_buckets_scratch(uint64_t m);
+hipError_t dedup_group_buckets(uint64_t* records, uint64_t m, uint64_t* rep, uint64_t* state, void* scratch,
+                               size_t scratch_bytes, hipStream_t s);
 }  // namespace sdk

@@ -284,7 +284,51 @@ def test_file_api_on_disk(ctx, tmp_path, golden):
 
 
 # ---------------------------------------------------------------------------- dedup
-def test_dedup_group_matches_host(ctx):
+@pytest.fixture(params=[0, 1])
+def dedup_variant(request):
+    """sd_dedup_group: 0 = rocPRIM radix sort, 1 = LDS buckets (the default)."""
+    from spacedrive_amd._native import lib
+    assert lib().sd_cas_set_tuning(b"dedup_variant", request.param) == 0
+    yield request.param
+    lib().sd_cas_set_tuning(b"dedup_variant", 1)  # the default
+
+
+def _group_check(ctx, recs: np.ndarray, index_sorted: bool = False):
+    gr, grep, gng = group_host(recs)
+    sub = torch.from_numpy(recs.copy()).cuda()
+    rep = torch.zeros(max(len(recs), 1), dtype=torch.int64, device="cuda")
+    ng = ctx.dedup_group(sub, len(recs), rep, index_sorted=index_sorted)
+    assert ng == gng
+    assert np.array_equal(sub.cpu().numpy(), gr)
+    assert np.array_equal(rep.cpu().numpy()[:len(recs)], grep)
+
+
+def test_dedup_group_edge_sizes(ctx, dedup_variant):
+    rng = np.random.default_rng(7)
+    for m in (0, 1, 2, 3, 47, 48, 49, 97, 1000, 4099):
+        keys = rng.integers(0, 2**63, m, dtype=np.int64) * 2 + rng.integers(0, 2, m)  # full 64-bit range
+        if m > 4:
+            keys[m // 2:m // 2 + 3] = keys[0]  # a group of 4
+        recs = np.stack([keys, rng.permutation(m).astype(np.int64) * 3 + 5], axis=1)
+        _group_check(ctx, recs)
+    # all keys equal (span 0), and a narrow key range (one cas_id prefix bucket of a rank)
+    _group_check(ctx, np.stack([np.full(300, 12345, np.int64), np.arange(300, dtype=np.int64)[::-1].copy()], axis=1))
+    narrow = (np.int64(0x1234) << np.int64(48)) + rng.integers(0, 2**40, 20000, dtype=np.int64)
+    _group_check(ctx, np.stack([narrow, np.arange(20000, dtype=np.int64)], axis=1), index_sorted=True)
+
+
+def test_dedup_group_bucket_overflow_falls_back(ctx, dedup_variant):
+    """A duplicate group of 3000 files exceeds one LDS bucket: the radix path takes over."""
+    rng = np.random.default_rng(8)
+    m = 100000
+    keys = rng.integers(-2**63, 2**63 - 1, m, dtype=np.int64)
+    keys[rng.choice(m, 3000, replace=False)] = keys[17]
+    recs = np.stack([keys, np.arange(m, dtype=np.int64)], axis=1)
+    _group_check(ctx, recs, index_sorted=True)
+    _group_check(ctx, recs[::-1].copy())
+
+
+def test_dedup_group_matches_host(ctx, dedup_variant):
     n = 50000
     sizes, cids, twins = synth.library(0, n, n, dup_frac=0.3)
     h = gpu_cas(ctx, sizes, cids, twins)
