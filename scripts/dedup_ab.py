@@ -22,13 +22,43 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, default=1250000)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--library", action="store_true", help="records of bench.py's library shard instead of random keys")
     a = ap.parse_args()
-    rng = np.random.default_rng(1)
-    keys = rng.integers(-2**63, 2**63 - 1, a.m, dtype=np.int64)
-    dup = rng.choice(a.m, a.m // 10, replace=False)
-    keys[dup] = keys[rng.integers(0, a.m, len(dup))]
-    src = torch.from_numpy(np.stack([keys, np.arange(a.m, dtype=np.int64)], axis=1)).cuda()
     ctx = sd.Context(0)
+    if a.library:  # the bench's shard: hash it on the device, then partition (nparts 1)
+        from spacedrive_amd import synth
+        sizes, cids, twins = synth.library(0, a.m, a.m)
+        ext, total = sd.stage_plan(sizes)
+        d_staged = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+        d_ext = torch.from_numpy(ext.view(np.uint8).copy()).cuda()
+        ctx.synth_stage_cas(torch.from_numpy(sizes.view(np.int64)).cuda(), torch.from_numpy(cids.view(np.int64)).cuda(),
+                            torch.from_numpy(twins.astype(np.int32)).cuda(), d_ext, a.m, d_staged)
+        batch = ctx.cas_batch(ext)
+        d_hash = torch.empty(a.m * 32, dtype=torch.uint8, device="cuda")
+        batch.run(d_staged, d_hash)
+        del d_staged
+        counts = torch.empty(1, dtype=torch.int64, device="cuda")
+        recs = torch.empty((a.m, 2), dtype=torch.int64, device="cuda")
+        nv = ctx.dedup_partition(d_hash.view(a.m, 32), torch.from_numpy((sizes != 0).astype(np.uint8)).cuda(), a.m, 0,
+                                 1, counts, recs)
+        src = recs[:nv].clone()
+        a.m = nv
+    else:
+        rng = np.random.default_rng(1)
+        keys = rng.integers(-2**63, 2**63 - 1, a.m, dtype=np.int64)
+        dup = rng.choice(a.m, a.m // 10, replace=False)
+        keys[dup] = keys[rng.integers(0, a.m, len(dup))]
+        src = torch.from_numpy(np.stack([keys, np.arange(a.m, dtype=np.int64)], axis=1)).cuda()
+    k = src[:, 0].cpu().numpy().view(np.uint64)
+    lg = 1
+    while lg < 24 and (48 << lg) < a.m:
+        lg += 1
+    span = int(k.max()) - int(k.min())
+    sh = max(span.bit_length() - lg, 0)
+    bsz = np.bincount(((k - k.min()) >> np.uint64(sh)).astype(np.int64), minlength=1 << lg)
+    _, gs = np.unique(k, return_counts=True)
+    print(f"records {a.m}: {1 << lg} buckets, mean {a.m / (1 << lg):.1f}, max {bsz.max()}, >128: {(bsz > 128).sum()}, "
+          f"sum s^2 {float((bsz.astype(np.float64) ** 2).sum()):.3g}; largest group {gs.max()}", flush=True)
     outs = {}
     for v in (0, 1, 0, 1):
         lib().sd_cas_set_tuning(b"dedup_variant", v)

@@ -301,9 +301,23 @@ __global__ __launch_bounds__(256) void k_gb_bounds(const uint32_t* __restrict__ 
 __device__ __forceinline__ uint64_t lo64(const uint4& v) { return ((uint64_t)v.y << 32) | v.x; }
 __device__ __forceinline__ uint64_t hi64(const uint4& v) { return ((uint64_t)v.w << 32) | v.z; }
 
-// One wave per bucket: rank of record e = number of records ordered before it by
-// (key, index, slot); its representative = the smallest index with an equal key; it heads
-// its group when no equal-key record precedes it.  Head counts -> heads[blockIdx.x].
+__device__ __forceinline__ bool rec_gt(const uint4& a, const uint4& b) {  // (key, index) order
+    const uint64_t ka = lo64(a), kb = lo64(b);
+    return ka > kb || (ka == kb && hi64(a) > hi64(b));
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave per bucket: its s records are padded to P = 2^k >= s with (~0, ~0) and
+// bitonic-sorted by (key, index) in LDS -- O(P log^2 P), so a bucket holding a large
+// duplicate group costs ~45 stages rather than the s^2 of a rank sort.  Then, in chunks
+// of 64 sorted records, a wave max-scan of head positions (a head is the first record
+// of its key) gives each record its group head, whose index is the group minimum (the
+// representative).  Head counts -> heads[blockIdx.x].
 __global__ __launch_bounds__(64 * GB_WAVES) void k_gb_sort(const uint4* __restrict__ copy,
                                                            const uint32_t* __restrict__ pos,
                                                            const uint32_t* __restrict__ offs, uint32_t nb,
@@ -319,30 +333,44 @@ __global__ __launch_bounds__(64 * GB_WAVES) void k_gb_sort(const uint4* __restri
         if (s > GB_CAP) {  // copied through unsorted; the caller re-sorts everything
             for (uint32_t e = lane; e < s; e += 64) rec[lo + e] = copy[pos[lo + e]];
             if (lane == 0) st->overflow = 1;
-        } else {
+        } else if (s > 0) {
             uint4* r_ = sr[w];
-            for (uint32_t e = lane; e < s; e += 64) r_[e] = copy[pos[lo + e]];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (uint32_t e = lane; e < s; e += 64) {
-                const uint4 me = r_[e];
-                const uint64_t k = lo64(me), id = hi64(me);
-                uint32_t rank = 0, eq_before = 0;
-                uint64_t mn = id;
-#pragma unroll 4
-                for (uint32_t j = 0; j < s; j++) {
-                    const uint4 o = r_[j];
-                    const uint64_t kj = lo64(o), ij = hi64(o);
-                    const bool eq = kj == k;
-                    const bool before = kj < k || (eq && (ij < id || (ij == id && j < e)));
-                    rank += before;
-                    eq_before += eq && before;
-                    mn = (eq && ij < mn) ? ij : mn;
+            uint32_t P = 1;
+            while (P < s) P <<= 1;
+            for (uint32_t e = lane; e < P; e += 64)
+                r_[e] = e < s ? copy[pos[lo + e]] : make_uint4(~0u, ~0u, ~0u, ~0u);
+            wave_lds_fence();
+            for (uint32_t k = 2; k <= P; k <<= 1) {
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    for (uint32_t t = lane; t < (P >> 1); t += 64) {
+                        const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), l = i + j;
+                        const uint4 x = r_[i], y = r_[l];
+                        if (rec_gt(x, y) == ((i & k) == 0)) {
+                            r_[i] = y;
+                            r_[l] = x;
+                        }
+                    }
+                    wave_lds_fence();
                 }
-                rec[lo + rank] = me;
-                rep[lo + rank] = mn;
-                h += eq_before == 0;
+            }
+            uint32_t carry = 0;  // head position of the record before this chunk
+            for (uint32_t c = 0; c < s; c += 64) {
+                const uint32_t p = c + lane;
+                const bool act = p < s;
+                const uint4 me = r_[act ? p : 0];
+                const bool head = act && (p == 0 || lo64(r_[p - 1]) != lo64(me));
+                uint32_t hp = head ? p : carry;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(hp, o);
+                    if (lane >= (uint32_t)o) hp = y > hp ? y : hp;
+                }
+                if (act) {
+                    rec[lo + p] = me;
+                    rep[lo + p] = hi64(r_[hp]);
+                }
+                h += head;
+                carry = __shfl(hp, 63);
             }
         }
     }
