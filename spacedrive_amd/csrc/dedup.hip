@@ -342,12 +342,28 @@ __global__ __launch_bounds__(64 * GB_WAVES) void k_gb_sort(const uint4* __restri
             wave_lds_fence();
             for (uint32_t k = 2; k <= P; k <<= 1) {
                 for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                    for (uint32_t t = lane; t < (P >> 1); t += 64) {
-                        const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), l = i + j;
-                        const uint4 x = r_[i], y = r_[l];
-                        if (rec_gt(x, y) == ((i & k) == 0)) {
-                            r_[i] = y;
-                            r_[l] = x;
+                    // a lane's (up to 4) pairs of a stage are disjoint: load them all, then
+                    // compare and store, so one LDS latency covers the stage
+                    constexpr uint32_t Q = GB_CAP / 128;
+                    uint4 x[Q], y[Q];
+#pragma unroll
+                    for (uint32_t q = 0; q < Q; q++) {
+                        const uint32_t t = lane + 64 * q;
+                        if (t < (P >> 1)) {
+                            const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                            x[q] = r_[i];
+                            y[q] = r_[i + j];
+                        }
+                    }
+#pragma unroll
+                    for (uint32_t q = 0; q < Q; q++) {
+                        const uint32_t t = lane + 64 * q;
+                        if (t < (P >> 1)) {
+                            const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                            if (rec_gt(x[q], y[q]) == ((i & k) == 0)) {
+                                r_[i] = y[q];
+                                r_[i + j] = x[q];
+                            }
                         }
                     }
                     wave_lds_fence();
