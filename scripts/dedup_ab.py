@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--m", type=int, default=1250000)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--library", action="store_true", help="records of bench.py's library shard instead of random keys")
+    ap.add_argument("--big", type=int, default=0,
+                    help="random keys plus this many groups of 1400 (one rank's share of the 10 M library's size-1 files at N=8)")
     a = ap.parse_args()
     ctx = sd.Context(0)
     if a.library:  # the bench's shard: hash it on the device, then partition (nparts 1)
@@ -48,6 +50,8 @@ def main():
         keys = rng.integers(-2**63, 2**63 - 1, a.m, dtype=np.int64)
         dup = rng.choice(a.m, a.m // 10, replace=False)
         keys[dup] = keys[rng.integers(0, a.m, len(dup))]
+        for g in range(a.big):
+            keys[rng.choice(a.m, 1400, replace=False)] = keys[g]
         src = torch.from_numpy(np.stack([keys, np.arange(a.m, dtype=np.int64)], axis=1)).cuda()
     k = src[:, 0].cpu().numpy().view(np.uint64)
     lg = 1

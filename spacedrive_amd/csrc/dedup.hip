@@ -208,14 +208,18 @@ uint32_t grid_for(uint64_t n) {
 // rank sort that also yields each record's group minimum (the representative) and
 // whether it heads its group.  No global atomics on the data path: partial results go to
 // per-workgroup slots reduced by one small workgroup.  A bucket larger than GB_CAP (a
+// large duplicate group) is listed for k_gb_sort_big, one 1024-lane workgroup per bucket
+// of up to GB_BIG_CAP records.  A bucket larger than that (a
 // duplicate group of hundreds of files) is copied through unsorted and flags `overflow`;
 // the caller then runs the radix path over the permuted records.
-constexpr uint32_t GB_CAP = 512;
+constexpr uint32_t GB_CAP = 128;   // wave LDS path for 64 < s <= 128; larger buckets go to k_gb_sort_big
 constexpr uint32_t GB_WAVES = 4;  // buckets per workgroup, one per wave
 constexpr uint32_t GB_MM_BLOCKS = 512;
+constexpr uint32_t GB_BIG_CAP = 4096;   // 64 KiB of LDS
+constexpr uint32_t GB_BIG_GRID = 128;   // workgroups of k_gb_sort_big (each loops over the list)
 
 struct gb_state {
-    unsigned long long ngroups, overflow, kmin, kmax, shift;
+    unsigned long long ngroups, overflow, kmin, kmax, shift, nbig;
 };
 
 // per-workgroup key minimum / maximum -> part[2 * blockIdx.x + {0, 1}]
@@ -269,6 +273,7 @@ __global__ __launch_bounds__(64) void k_gb_final(const uint64_t* __restrict__ pa
         st->shift = bits > lg ? bits - lg : 0u;  // lg >= 1, so shift <= 63
         st->ngroups = 0;
         st->overflow = 0;
+        st->nbig = 0;
     }
 }
 
@@ -322,7 +327,8 @@ __global__ __launch_bounds__(64 * GB_WAVES) void k_gb_sort(const uint4* __restri
                                                            const uint32_t* __restrict__ pos,
                                                            const uint32_t* __restrict__ offs, uint32_t nb,
                                                            uint4* __restrict__ rec, uint64_t* __restrict__ rep,
-                                                           uint32_t* __restrict__ heads, gb_state* st) {
+                                                           uint32_t* __restrict__ heads, uint32_t* __restrict__ big,
+                                                           gb_state* st) {
     __shared__ uint4 sr[GB_WAVES][GB_CAP];  // (key, index) per record
     __shared__ uint32_t wh[GB_WAVES];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -330,9 +336,46 @@ __global__ __launch_bounds__(64 * GB_WAVES) void k_gb_sort(const uint4* __restri
     uint32_t h = 0;
     if (b < nb) {
         const uint32_t lo = offs[b], s = offs[b + 1] - lo;
-        if (s > GB_CAP) {  // copied through unsorted; the caller re-sorts everything
-            for (uint32_t e = lane; e < s; e += 64) rec[lo + e] = copy[pos[lo + e]];
-            if (lane == 0) st->overflow = 1;
+        if (s > GB_CAP) {  // k_gb_sort_big takes it
+            if (lane == 0) big[atomicAdd(&st->nbig, 1ull)] = b;
+        } else if (s > 0 && s <= 64) {
+            // the common case (mean ~38): one record per lane, a bitonic network over
+            // lane shuffles, then head / representative by shuffles -- no LDS at all
+            uint32_t P = 1;
+            while (P < s) P <<= 1;
+            const bool act = lane < s;
+            uint64_t k = ~0ull, id = ~0ull;
+            if (act) {
+                const uint4 r = copy[pos[lo + lane]];
+                k = lo64(r);
+                id = hi64(r);
+            }
+            for (uint32_t kk = 2; kk <= P; kk <<= 1) {
+                for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                    const uint64_t ok = __shfl_xor(k, (int)j), oid = __shfl_xor(id, (int)j);
+                    const bool other_less = ok < k || (ok == k && oid < id);
+                    const bool me_less = k < ok || (k == ok && id < oid);
+                    const bool want_min = ((lane & j) == 0) == ((lane & kk) == 0);
+                    if (want_min ? other_less : me_less) {
+                        k = ok;
+                        id = oid;
+                    }
+                }
+            }
+            const uint64_t pk = __shfl_up(k, 1);
+            const bool head = act && (lane == 0 || pk != k);
+            uint32_t hp = head ? lane : 0u;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(hp, o);
+                if (lane >= (uint32_t)o) hp = y > hp ? y : hp;
+            }
+            const uint64_t r = __shfl(id, (int)hp);
+            if (act) {
+                rec[lo + lane] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)id, (uint32_t)(id >> 32));
+                rep[lo + lane] = r;
+            }
+            h += head;
         } else if (s > 0) {
             uint4* r_ = sr[w];
             uint32_t P = 1;
@@ -398,6 +441,99 @@ __global__ __launch_bounds__(64 * GB_WAVES) void k_gb_sort(const uint4* __restri
         uint32_t t = 0;
         for (uint32_t k = 0; k < GB_WAVES; k++) t += wh[k];
         heads[blockIdx.x] = t;
+    }
+}
+
+// Buckets of GB_CAP < s <= GB_BIG_CAP records (a duplicate group of hundreds to thousands
+// of files): one 1024-lane workgroup per listed bucket, the same bitonic sort and head
+// max-scan with workgroup barriers.  Larger buckets are copied through unsorted and flag
+// `overflow`.  Head counts -> heads[blockIdx.x] (every workgroup writes its slot).
+__global__ __launch_bounds__(1024) void k_gb_sort_big(const uint4* __restrict__ copy, const uint32_t* __restrict__ pos,
+                                                      const uint32_t* __restrict__ offs,
+                                                      const uint32_t* __restrict__ big, uint4* __restrict__ rec,
+                                                      uint64_t* __restrict__ rep, uint32_t* __restrict__ heads,
+                                                      gb_state* st) {
+    __shared__ uint4 sr[GB_BIG_CAP];
+    __shared__ uint32_t wmax[16], carry_s;
+    __shared__ uint32_t wh[16];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t nbig = (uint32_t)st->nbig;
+    uint32_t h = 0;
+    for (uint32_t q = blockIdx.x; q < nbig; q += gridDim.x) {
+        const uint32_t b = big[q];
+        const uint32_t lo = offs[b], s = offs[b + 1] - lo;
+        if (s > GB_BIG_CAP) {  // copied through unsorted; the caller re-sorts everything
+            for (uint32_t e = t; e < s; e += 1024) rec[lo + e] = copy[pos[lo + e]];
+            if (t == 0) st->overflow = 1;
+            continue;
+        }
+        uint32_t P = 1;
+        while (P < s) P <<= 1;
+        for (uint32_t e = t; e < P; e += 1024) sr[e] = e < s ? copy[pos[lo + e]] : make_uint4(~0u, ~0u, ~0u, ~0u);
+        __syncthreads();
+        for (uint32_t k = 2; k <= P; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                constexpr uint32_t Q = GB_BIG_CAP / 2048;
+                uint4 x[Q], y[Q];
+#pragma unroll
+                for (uint32_t r = 0; r < Q; r++) {
+                    const uint32_t u = t + 1024 * r;
+                    if (u < (P >> 1)) {
+                        const uint32_t i = ((u & ~(j - 1)) << 1) | (u & (j - 1));
+                        x[r] = sr[i];
+                        y[r] = sr[i + j];
+                    }
+                }
+#pragma unroll
+                for (uint32_t r = 0; r < Q; r++) {
+                    const uint32_t u = t + 1024 * r;
+                    if (u < (P >> 1)) {
+                        const uint32_t i = ((u & ~(j - 1)) << 1) | (u & (j - 1));
+                        if (rec_gt(x[r], y[r]) == ((i & k) == 0)) {
+                            sr[i] = y[r];
+                            sr[i + j] = x[r];
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        if (t == 0) carry_s = 0;
+        __syncthreads();
+        for (uint32_t c = 0; c < s; c += 1024) {
+            const uint32_t p = c + t;
+            const bool act = p < s;
+            const uint4 me = sr[act ? p : 0];
+            const bool head = act && (p == 0 || lo64(sr[p - 1]) != lo64(me));
+            uint32_t hp = head ? p : 0u;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(hp, o);
+                if (lane >= (uint32_t)o) hp = y > hp ? y : hp;
+            }
+            if (lane == 63) wmax[w] = hp;
+            __syncthreads();
+            uint32_t before = carry_s;
+            for (uint32_t k = 0; k < w; k++) before = wmax[k] > before ? wmax[k] : before;
+            hp = before > hp ? before : hp;
+            if (act) {
+                rec[lo + p] = me;
+                rep[lo + p] = hi64(sr[hp]);
+            }
+            h += head;
+            __syncthreads();
+            if (t == 1023) carry_s = hp;
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+    if (lane == 0) wh[w] = h;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < 16; k++) v += wh[k];
+        heads[blockIdx.x] = v;
     }
 }
 
@@ -499,10 +635,13 @@ static size_t gb_sort_bytes(uint64_t m, uint32_t lg, hipStream_t s) {
     return (b + 255) & ~size_t(255);
 }
 
-// scratch: copy[m] (16-B records), bk, bk2, pos, pos2 [m] (u32), offs[nb + 1], heads[nb / 4 + 1],
-// minmax partials, then the radix sort's temporary storage
+// scratch: copy[m] (16-B records), bk, bk2, pos, pos2 [m] (u32), offs[nb + 1],
+// heads[n_wg + GB_BIG_GRID], big[m / (GB_CAP + 1) + 1], minmax partials, then the radix
+// sort's temporary storage
+static uint64_t gb_big_slots(uint64_t m) { return m / (GB_CAP + 1) + 1; }
 static size_t gb_layout_bytes(uint64_t m, uint32_t nb) {
-    size_t b = 2 * m * sizeof(uint64_t) + 4 * m * sizeof(uint32_t) + (nb + 1 + nb / GB_WAVES + 1) * sizeof(uint32_t);
+    size_t b = 2 * m * sizeof(uint64_t) + 4 * m * sizeof(uint32_t) +
+               (nb + 1 + nb / GB_WAVES + 1 + GB_BIG_GRID + gb_big_slots(m)) * sizeof(uint32_t);
     b = (b + 15) & ~size_t(15);
     b += 2 * GB_MM_BLOCKS * sizeof(uint64_t);
     return (b + 255) & ~size_t(255);
@@ -513,7 +652,7 @@ size_t dedup_group_buckets_scratch(uint64_t m) {
     return gb_layout_bytes(m, 1u << lg) + gb_sort_bytes(m, lg, nullptr) + 256;
 }
 
-// state: 5 u64 (ngroups, overflow, kmin, kmax, shift); 0 < m < 2^31
+// state: 6 u64 (ngroups, overflow, kmin, kmax, shift, nbig); 0 < m < 2^31
 hipError_t dedup_group_buckets(uint64_t* records, uint64_t m, uint64_t* rep, uint64_t* state, void* scratch,
                                size_t scratch_bytes, hipStream_t s) {
     if (m == 0 || m >= (1ull << 31) || scratch_bytes < dedup_group_buckets_scratch(m)) return hipErrorInvalidValue;
@@ -526,8 +665,9 @@ hipError_t dedup_group_buckets(uint64_t* records, uint64_t m, uint64_t* rep, uin
     uint32_t* pos = bk2 + m;
     uint32_t* pos2 = pos + m;
     uint32_t* offs = pos2 + m;  // nb + 1
-    uint32_t* heads = offs + nb + 1;
-    uint64_t* part = reinterpret_cast<uint64_t*>(((uintptr_t)(heads + n_wg) + 15) & ~uintptr_t(15));
+    uint32_t* heads = offs + nb + 1;  // n_wg + GB_BIG_GRID
+    uint32_t* big = heads + n_wg + GB_BIG_GRID;
+    uint64_t* part = reinterpret_cast<uint64_t*>(((uintptr_t)(big + gb_big_slots(m)) + 15) & ~uintptr_t(15));
     void* tmp = base + gb_layout_bytes(m, nb);
     size_t tb = gb_sort_bytes(m, lg, s);
     const uint32_t g = std::min<unsigned>(grid_for(m), GB_MM_BLOCKS);
@@ -539,8 +679,10 @@ hipError_t dedup_group_buckets(uint64_t* records, uint64_t m, uint64_t* rep, uin
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_gb_bounds, dim3(grid_for(m)), dim3(256), 0, s, bk2, m, nb, offs);
     hipLaunchKernelGGL(k_gb_sort, dim3(n_wg), dim3(64 * GB_WAVES), 0, s, copy, pos2, offs, nb,
-                       reinterpret_cast<uint4*>(records), rep, heads, st);
-    hipLaunchKernelGGL(k_gb_sum, dim3(1), dim3(1024), 0, s, heads, n_wg, st);
+                       reinterpret_cast<uint4*>(records), rep, heads, big, st);
+    hipLaunchKernelGGL(k_gb_sort_big, dim3(GB_BIG_GRID), dim3(1024), 0, s, copy, pos2, offs, big,
+                       reinterpret_cast<uint4*>(records), rep, heads + n_wg, st);
+    hipLaunchKernelGGL(k_gb_sum, dim3(1), dim3(1024), 0, s, heads, n_wg + GB_BIG_GRID, st);
     return hipGetLastError();
 }
 

@@ -90,7 +90,7 @@ hipError_t dedup_group(uint64_t* records, uint64_t m, int flags, uint64_t* rep, 
                        void* scratch, size_t* scratch_bytes, hipStream_t s);
 // bucket grouping (dedup_variant 1): same outputs as dedup_group for m < 2^31 unless
 // state[1] (overflow) comes back nonzero -- then records hold a permutation of the input
-// and dedup_group (without SD_DEDUP_INDEX_SORTED) must run.  state: 5 device u64, state[0]
+// and dedup_group (without SD_DEDUP_INDEX_SORTED) must run.  state: 6 device u64, state[0]
 // = the group count.
 size_t dedup_group_buckets_scratch(uint64_t m);
 hipError_t dedup_group_buckets(uint64_t* records, uint64_t m, uint64_t* rep, uint64_t* state, void* scratch,

@@ -317,12 +317,23 @@ def test_dedup_group_edge_sizes(ctx, dedup_variant):
     _group_check(ctx, np.stack([narrow, np.arange(20000, dtype=np.int64)], axis=1), index_sorted=True)
 
 
-def test_dedup_group_bucket_overflow_falls_back(ctx, dedup_variant):
-    """A duplicate group of 3000 files exceeds one LDS bucket: the radix path takes over."""
+def test_dedup_group_large_groups(ctx, dedup_variant):
+    """Duplicate groups larger than a wave's LDS bucket (512): 3000 files and 40 groups of
+    600..1500 go to the workgroup sort (k_gb_sort_big); 5000 exceed it (radix fallback)."""
     rng = np.random.default_rng(8)
-    m = 100000
+    m = 200000
     keys = rng.integers(-2**63, 2**63 - 1, m, dtype=np.int64)
-    keys[rng.choice(m, 3000, replace=False)] = keys[17]
+    perm = rng.permutation(m)
+    keys[perm[:3000]] = keys[perm[0]]
+    at = 3000
+    for g in range(40):
+        sz = 600 + 23 * g
+        keys[perm[at:at + sz]] = keys[perm[at]]
+        at += sz
+    recs = np.stack([keys, np.arange(m, dtype=np.int64)], axis=1)
+    _group_check(ctx, recs, index_sorted=True)
+    _group_check(ctx, recs[::-1].copy())
+    keys[perm[at:at + 5000]] = keys[perm[at]]
     recs = np.stack([keys, np.arange(m, dtype=np.int64)], axis=1)
     _group_check(ctx, recs, index_sorted=True)
     _group_check(ctx, recs[::-1].copy())
