@@ -193,6 +193,13 @@ int sd_dedup_partition(sd_cas_ctx* ctx, const uint8_t* d_hash32, const uint8_t* 
 #define SD_DEDUP_INDEX_SORTED 1
 int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, int flags, uint64_t* d_rep,
                    uint64_t* n_groups, void* stream);
+/* Object owner per grouped record (d_records / d_rep as sd_dedup_group leaves them), the
+ * reference's link-or-create rule for identifier steps of `chunk_size` files
+ * (file_identifier/mod.rs:36,136-333): d_owner[i] = index if index / chunk_size ==
+ * rep / chunk_size (the group's first step creates an Object per file), else rep (a later
+ * step links to it).  Asynchronous on `stream`; no host sync. */
+int sd_dedup_owners(sd_cas_ctx* ctx, const uint64_t* d_records, uint64_t m, const uint64_t* d_rep,
+                    uint64_t chunk_size, uint64_t* d_owner, void* stream);
 
 /* ---------------------------------------------------------------- synthetic data */
 /* Device generator of SURVEY.md §8(d) (seed 0x5D5DCA51D, splitmix64 counter stream),

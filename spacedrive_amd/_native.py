@@ -76,6 +76,7 @@ SIGNATURES = [
     ("sd_coalescer_stats", I32, [P, P]),
     ("sd_dedup_partition", I32, [P, P, P, U64, U64, I32, P, P, PU64, P]),
     ("sd_dedup_group", I32, [P, P, U64, I32, P, PU64, P]),
+    ("sd_dedup_owners", I32, [P, P, U64, P, U64, P, P]),
     ("sd_synth_stage_cas", I32, [P, P, P, P, P, SZ, P, P]),
     ("sd_synth_fill", I32, [P, U64, U32, U64, P, P]),
     ("sd_device_malloc", I32, [P, U64, ctypes.POINTER(P)]),

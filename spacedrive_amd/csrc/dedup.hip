@@ -553,6 +553,18 @@ __global__ __launch_bounds__(1024) void k_gb_sum(const uint32_t* __restrict__ he
     }
 }
 
+// Object owner per record under the reference's chunk-of-100 rule (file_identifier/
+// mod.rs:136-333; spacedrive_amd/identifier.py): a file links to its group's first Object
+// when that was created in an earlier identifier step, else it creates its own.
+__global__ __launch_bounds__(256) void k_owners(const uint64_t* __restrict__ rec, uint64_t m,
+                                                const uint64_t* __restrict__ rep, uint64_t chunk,
+                                                uint64_t* __restrict__ owner) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t idx = rec[2 * i + 1], r = rep[i];
+        owner[i] = idx / chunk == r / chunk ? idx : r;
+    }
+}
+
 }  // namespace
 
 namespace sdk {
@@ -683,6 +695,13 @@ hipError_t dedup_group_buckets(uint64_t* records, uint64_t m, uint64_t* rep, uin
     hipLaunchKernelGGL(k_gb_sort_big, dim3(GB_BIG_GRID), dim3(1024), 0, s, copy, pos2, offs, big,
                        reinterpret_cast<uint4*>(records), rep, heads + n_wg, st);
     hipLaunchKernelGGL(k_gb_sum, dim3(1), dim3(1024), 0, s, heads, n_wg + GB_BIG_GRID, st);
+    return hipGetLastError();
+}
+
+hipError_t dedup_owners(const uint64_t* records, uint64_t m, const uint64_t* rep, uint64_t chunk, uint64_t* owner,
+                        hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_owners, dim3(grid_for(m)), dim3(256), 0, s, records, m, rep, chunk, owner);
     return hipGetLastError();
 }
 

@@ -1329,6 +1329,17 @@ int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, int flags, 
     SD_GUARD_END
 }
 
+int sd_dedup_owners(sd_cas_ctx* ctx, const uint64_t* d_records, uint64_t m, const uint64_t* d_rep,
+                    uint64_t chunk_size, uint64_t* d_owner, void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || (m && (!d_records || !d_rep || !d_owner))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (chunk_size == 0) throw sd_failure(SD_ERR_INVALID, "chunk_size must be positive");
+    ctx->bind();
+    HIP_CHECK(sdk::dedup_owners(d_records, m, d_rep, chunk_size, d_owner, ctx->pick(stream)));
+    return SD_OK;
+    SD_GUARD_END
+}
+
 // ----------------------------------------------------------------- synthetic data
 int sd_synth_stage_cas(sd_cas_ctx* ctx, const uint64_t* d_sizes, const uint64_t* d_cids, const uint32_t* d_twins,
                        const sd_extent* d_extents, size_t n, uint8_t* d_staged, void* stream) {

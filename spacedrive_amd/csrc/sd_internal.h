@@ -95,4 +95,6 @@ hipError_t dedup_group(uint64_t* records, uint64_t m, int flags, uint64_t* rep, 
 size_t dedup_group_buckets_scratch(uint64_t m);
 hipError_t dedup_group_buckets(uint64_t* records, uint64_t m, uint64_t* rep, uint64_t* state, void* scratch,
                                size_t scratch_bytes, hipStream_t s);
+hipError_t dedup_owners(const uint64_t* records, uint64_t m, const uint64_t* rep, uint64_t chunk, uint64_t* owner,
+                        hipStream_t s);
 }  // namespace sdk

@@ -84,8 +84,10 @@ def dedup_shard(ctx, d_hash32: torch.Tensor, d_valid: Optional[torch.Tensor], n_
     # the partition is stable and shard r holds indices [r*n, (r+1)*n): the received
     # records are in ascending index order, so one stable cas_id sort suffices
     records, rep, ng = group_device(ctx, recv, index_sorted=True)
-    from .identifier import object_owners
-    return records, rep, ng, object_owners(records[:, 1], rep)
+    # identifier.object_owners is the torch statement of the same rule (tests compare them)
+    owners = torch.empty(max(records.shape[0], 1), dtype=torch.int64, device=dev)
+    ctx.dedup_owners(records, records.shape[0], rep, owners)
+    return records, rep, ng, owners[:records.shape[0]]
 
 
 # ------------------------------------------------------------------ host reference

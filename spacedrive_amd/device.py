@@ -100,6 +100,10 @@ class Context:
                                    ctypes.byref(ng), _stream(stream)))
         return int(ng.value)
 
+    def dedup_owners(self, d_records, m: int, d_rep, d_owner, chunk_size: int = 100, stream=None) -> None:
+        check(lib().sd_dedup_owners(self.handle, _ptr(d_records), m, _ptr(d_rep), chunk_size, _ptr(d_owner),
+                                    _stream(stream)))
+
 
 class CasBatch:
     """Prepared cas_id batch (sd_cas_batch): run over device-resident staged messages."""

@@ -580,3 +580,19 @@ def test_file_api_past_4gib_sparse(ctx, tmp_path, oracle_native):
     data = np.memmap(paths[0], dtype=np.uint8, mode="r")
     want = oracle_native.checksums_simd(data, [0], [sizes[0]], nthreads=1)[0].tobytes().hex()
     assert sums[0] == want
+
+
+def test_dedup_owners_matches_torch_rule(ctx):
+    """sd_dedup_owners (one kernel) == identifier.object_owners (the torch statement)."""
+    from spacedrive_amd.identifier import object_owners
+    rng = np.random.default_rng(11)
+    for m, chunk in ((0, 100), (1, 100), (100000, 100), (4099, 7)):
+        idx = np.sort(rng.choice(10 * max(m, 1), m, replace=False)).astype(np.int64)
+        rep = np.minimum(idx, idx[rng.integers(0, max(m, 1), m)] if m else idx)
+        recs = torch.from_numpy(np.stack([rng.integers(0, 2**62, m), idx], axis=1).astype(np.int64)).cuda()
+        d_rep = torch.from_numpy(rep).cuda()
+        out = torch.full((max(m, 1),), -1, dtype=torch.int64, device="cuda")
+        ctx.dedup_owners(recs, m, d_rep, out, chunk_size=chunk)
+        torch.cuda.synchronize()
+        want = object_owners(torch.from_numpy(idx), torch.from_numpy(rep), chunk_size=chunk).numpy()
+        assert np.array_equal(out.cpu().numpy()[:m], want)
