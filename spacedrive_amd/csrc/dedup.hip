@@ -201,17 +201,19 @@ uint32_t grid_for(uint64_t n) {
 
 // ------------------------------------------------- bucket grouping (dedup_variant 1)
 // cas_ids are uniform hash bits, so an order-preserving split of the key range into
-// nb = 2^lg buckets -- (key - kmin) >> shift -- leaves ~m/nb records per bucket, and equal
-// keys share a bucket, so every group lies inside one.  The records are bucketed by a
-// radix sort of the lg-bit bucket numbers alone (2-3 passes of u32 pairs instead of 8
-// passes of u64 pairs), then each bucket is sorted by (key, index) in LDS by one wave: a
-// rank sort that also yields each record's group minimum (the representative) and
-// whether it heads its group.  No global atomics on the data path: partial results go to
-// per-workgroup slots reduced by one small workgroup.  A bucket larger than GB_CAP (a
-// large duplicate group) is listed for k_gb_sort_big, one 1024-lane workgroup per bucket
-// of up to GB_BIG_CAP records.  A bucket larger than that (a
-// duplicate group of hundreds of files) is copied through unsorted and flags `overflow`;
-// the caller then runs the radix path over the permuted records.
+// nb = 2^lg buckets -- (key - kmin) >> shift -- leaves ~m/nb (24-48) records per bucket,
+// and equal keys share a bucket, so every group lies inside one.  The records are bucketed
+// by a radix sort of the lg-bit bucket numbers alone (2-3 passes of u32 pairs instead of
+// 8 passes of u64 pairs).  Each bucket is then sorted by (key, index) with a bitonic
+// network and a max-scan of head positions gives every record its group head, whose
+// index is the group minimum (the representative):
+//   s <= 64        one wave, one record per lane, in registers (lane shuffles);
+//   s <= GB_CAP    one wave, in LDS;
+//   s <= GB_BIG_CAP  one 1024-lane workgroup (k_gb_sort_big; a large duplicate group);
+//   larger         copied through unsorted, flagging `overflow`: the caller then runs the
+//                  radix path over the permuted records.
+// No global atomics on the data path (only the rare big-bucket listing): partial results
+// go to per-workgroup slots reduced by one small workgroup.
 constexpr uint32_t GB_CAP = 128;   // wave LDS path for 64 < s <= 128; larger buckets go to k_gb_sort_big
 constexpr uint32_t GB_WAVES = 4;  // buckets per workgroup, one per wave
 constexpr uint32_t GB_MM_BLOCKS = 512;
