@@ -52,10 +52,6 @@ def parse():
     p.add_argument("--checksum-steps", type=int, default=5)
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target seconds per CPU-baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--whole-variant", type=int, default=8,
-                   help="0/4 = fused launch; 1 = separate sampled / whole-leaf / whole-tree kernels; 3 = separate "
-                        "sampled / prefetching pair-leaf / pair-tree kernels; 7 = sampled kernel + one full/tail "
-                        "pair-item launch + two merge8 passes; 8 = 7 with line-pair loads (default); see DESIGN.md")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (rehearsal)")
     p.add_argument("--share-gpu", action="store_true", help="map every rank onto the visible GPUs (rehearsal)")
     p.add_argument("--config-files", type=int, default=1_000_000,
@@ -333,9 +329,7 @@ def main():
 
     stream = torch.cuda.current_stream()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    from spacedrive_amd._native import lib
-    lib().sd_cas_set_tuning(b"whole_variant", args.whole_variant)
-    split = args.whole_variant in (1, 3, 5, 6, 7, 8)  # separate launches: the dominant kernel is timed on its own
+    split = True  # separate launches: the dominant kernel is timed on its own
 
     def step(k=None):
         if k is not None:
@@ -397,19 +391,14 @@ def main():
         dom_kernel, dom_ms = "k_cas_sampled", sampled_ms
         dom_comp = 953 * batch.n_sampled
         dom_bytes = batch.n_sampled * (SAMPLED_MSG + 32)
-    else:  # fused / side-stream variants: the whole hashing phase
-        dom_kernel, dom_ms = ("k_cas_mixed" if args.whole_variant == 0 else "hash phase"), hash_ms
+    else:
+        dom_kernel, dom_ms = "hash phase", hash_ms
         dom_comp, dom_bytes = batch.compressions, batch.msg_bytes + 32 * n
     dom_valu = dom_comp * 672 / (dom_ms * 1e-3)
     dom_gbps = dom_bytes / (dom_ms * 1e-3) / 1e9
     hash_bytes = batch.msg_bytes + 32 * n
     hash_valu = batch.compressions * 672 / (hash_ms * 1e-3)
-    phase = {0: ["k_cas_mixed"], 4: ["k_cas_mixed"], 1: ["k_cas_sampled", "k_whole_leaf", "k_whole_tree"],
-             5: ["k_cas_sampled", "k_whole_pair_leaf", "k_whole_forest"],
-             6: ["k_cas_sampled", "k_whole_full", "k_whole_tail", "k_whole_merge8"],
-             7: ["k_cas_sampled", "k_whole_items", "k_whole_merge8"],
-             8: ["k_cas_sampled", "k_whole_items", "k_whole_merge8"]}.get(
-        args.whole_variant, ["k_cas_sampled", "k_whole_pair_leaf", "k_whole_tree"])
+    phase = ["k_cas_sampled", "k_whole_items", "k_whole_merge8"]
     traffic = pmc_traffic(dom_kernel) if split else pmc_traffic(phase)
 
     out = {

@@ -22,8 +22,19 @@
  *   - `stream` arguments are hipStream_t passed as void*; NULL is HIP's null (default)
  *     stream, as everywhere in HIP.  Device-pointer entry points only enqueue work on it
  *     and do not synchronise (the dedup calls return host counts and so do sync it);
- *   - the library has no CPU fallback: without a usable gfx950 device every compute entry
- *     point fails with SD_ERR_DEVICE.
+ *   - the GPU entry points need a gfx950 device (sd_cas_ctx_create fails with SD_ERR_DEVICE
+ *     otherwise); the sd_cpu_* entry points are the library's CPU path:
+ *     the same results from the host cores, for a node without the device and for the
+ *     latency path's single-file callers.  No GPU entry point falls back to them silently;
+ *     sd_cas_id_path / sd_file_checksum_path route a call to the CPU by a documented,
+ *     tunable policy ("latency_cpu_max") and count it in sd_coalescer_stats.
+ *
+ * File-read semantics (the reference's, whatever the file's length): a whole-kind cas
+ * message is le64(size) || every byte fs::read returns (cas.rs:25,29) -- the file may be
+ * shorter or longer than `size`; a sampled message reads head and samples with read_exact
+ * at their traced offsets and the tail at seek(End(-8192)), the file's real end (cas.rs:
+ * 31-58); a checksum hashes what 1 MiB read calls return until one returns fewer
+ * (hash.rs:14-20).
  */
 #ifndef SD_CAS_H
 #define SD_CAS_H
@@ -35,7 +46,7 @@
 extern "C" {
 #endif
 
-#define SD_CAS_ABI_VERSION 1
+#define SD_CAS_ABI_VERSION 2
 
 /* cas.rs:10-15 */
 #define SD_SAMPLE_COUNT 4u
@@ -63,7 +74,11 @@ typedef enum sd_file_status {
     SD_FILE_OK = 0,
     SD_FILE_SKIPPED_EMPTY = 1, /* FileMetadata::new skips len 0 (file_identifier/mod.rs:80-88) */
     SD_FILE_IO_ERROR = 2,      /* open/read failed: errno in the high 16 bits */
-    SD_FILE_SHORT_READ = 3     /* read_exact hit EOF: io::ErrorKind::UnexpectedEof (cas.rs:36,43,56) */
+    SD_FILE_SHORT_READ = 3,    /* read_exact hit EOF: io::ErrorKind::UnexpectedEof (cas.rs:36,43,56) */
+    SD_FILE_CHANGED = 4        /* staging only (sd_cas_stage_file/_files): the whole-kind file holds
+                                  more bytes than its extent's room (it grew since the caller's
+                                  stat); the reference hashes them all -- re-stage it with a larger
+                                  extent, or use sd_cas_ids_files / sd_cas_id_path, which do */
 } sd_file_status;
 
 typedef enum sd_kind {
@@ -75,7 +90,7 @@ typedef enum sd_kind {
 typedef struct sd_extent {
     uint64_t size;       /* file size as passed to generate_cas_id (hashed as le64)  */
     uint64_t msg_offset; /* byte offset of the message in the staged buffer (16-B aligned) */
-    uint32_t msg_len;    /* 8 + size (WHOLE) or 57352 (SAMPLED)                      */
+    uint32_t msg_len;    /* SAMPLED: 57352; WHOLE: 8 + the bytes staged (planned 8 + size) */
     uint32_t kind;       /* sd_kind                                                  */
 } sd_extent;
 
@@ -98,19 +113,25 @@ void sd_cas_host_free(sd_cas_ctx* ctx, void* p);
  * staged-buffer size.  Pure host arithmetic; no device needed. */
 int sd_cas_stage_plan(const uint64_t* sizes, size_t n, sd_extent* extents_out,
                       uint64_t* total_bytes_out);
-/* Reads one file into its extent exactly as generate_cas_id does (le64 header, whole
- * file or head/samples/tail via pread), zero-padding to SD_STAGE_ALIGN.  Sets *status
- * to an sd_file_status; returns SD_OK unless arguments are invalid. */
-int sd_cas_stage_file(const char* path, const sd_extent* ext, uint8_t* staged, int32_t* status);
+/* Reads one file into its extent exactly as generate_cas_id does (le64 header, then the
+ * whole file until EOF, or head/samples by read_exact and the tail at the file's real end),
+ * zero-padding to the next 64-byte boundary.  The extent is in/out: for a whole-kind file
+ * msg_len becomes 8 + the bytes read, which may be fewer than planned (the file is shorter
+ * than `size`; room = the planned msg_len - 8).  Sets *status to an sd_file_status
+ * (SD_FILE_CHANGED when the file holds more than the room); returns SD_OK unless
+ * arguments are invalid. */
+int sd_cas_stage_file(const char* path, sd_extent* ext, uint8_t* staged, int32_t* status);
 /* The same for n files on nthreads threads (the reference does these reads one tokio
  * blocking-pool hop at a time: cas.rs:29-58).  status[n] receives each file's outcome. */
-int sd_cas_stage_files(const char* const* paths, const sd_extent* extents, size_t n, uint8_t* staged,
+int sd_cas_stage_files(const char* const* paths, sd_extent* extents, size_t n, uint8_t* staged,
                        int32_t* status, int nthreads);
 
 /* ---------------------------------------------------------------- cas ids */
 /* Drop-in batch: staged messages in host memory (pinned or pageable) -> n cas_ids as
  * 16 lowercase hex chars + NUL (cas.rs:61), 17 bytes per file.  status may be NULL;
- * entries whose status[i] != SD_FILE_OK on input are skipped and left untouched. */
+ * entries whose status[i] != SD_FILE_OK on input are skipped and left untouched.  Whole-
+ * kind messages of any length are accepted (longer than 8 + 102400 B: hashed by the
+ * chunk-parallel checksum kernels). */
 int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes,
                const sd_extent* extents, size_t n, char* out_hex17, int32_t* status);
 
@@ -154,9 +175,10 @@ int sd_checksum_batch_run(sd_cas_ctx* ctx, const sd_checksum_batch* batch, const
 /* [0] files, [1] total bytes, [2] BLAKE3 compressions, [3] 1 MiB leaf blocks */
 int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
 /* Drop-in: checksums of n files on disk -> 65-byte lowercase hex each (hash.rs:21-23);
- * status[n] required.  Files up to 256 MiB are packed many per pinned window, larger
- * ones are streamed window by window; two windows alternate so host reads overlap the
- * H2D copies and the kernels.  The length hashed is the file's length at stat time. */
+ * status[n] required.  Each file is read as hash.rs reads it (1 MiB read calls until a
+ * short one); small files are packed many per pinned window, large ones (or ones that
+ * outgrow their room) streamed window by window, whatever their final length; two
+ * windows alternate so host reads overlap the H2D copies and the kernels. */
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65,
                       int32_t* status);
 
@@ -164,14 +186,38 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
 /* Single-file generate_cas_id (cas.rs:23) / file_checksum (hash.rs:10) for the
  * reference's per-file callers -- the location watcher (core/src/location/manager/
  * watcher/utils.rs:235,393,438-446) and non_indexed::walk (core/src/location/
- * non_indexed.rs:164-187).  Blocking and thread-safe: concurrent calls on one context
- * are coalesced by a dispatcher thread into one staged GPU batch per window (tuning
- * "coalesce_window_us", default 200, or "coalesce_max" requests, default 4096).  Return
- * SD_OK with *status = sd_file_status (the hex is written only for SD_FILE_OK). */
+ * non_indexed.rs:164-187).  Blocking and thread-safe.  Policy: while fewer than
+ * "latency_cpu_max" (default 16; 0 = never) single-file calls are in flight on the
+ * context, a call is hashed on the calling thread by the CPU path -- one GPU round trip
+ * per file costs more than hashing it; beyond that, concurrent calls are coalesced by a
+ * dispatcher thread into one staged GPU batch per window (tuning "coalesce_window_us",
+ * default 200, or "coalesce_max" requests, default 4096).  Return SD_OK with *status =
+ * sd_file_status (the hex is written only for SD_FILE_OK). */
 int sd_cas_id_path(sd_cas_ctx* ctx, const char* path, uint64_t size, char* out_hex17, int32_t* status);
 int sd_file_checksum_path(sd_cas_ctx* ctx, const char* path, char* out_hex65, int32_t* status);
-/* [0] single-file requests, [1] batches they were coalesced into, [2] largest batch */
-int sd_coalescer_stats(sd_cas_ctx* ctx, uint64_t out[3]);
+/* [0] single-file requests, [1] GPU batches they were coalesced into, [2] largest batch,
+ * [3] requests hashed on the CPU path */
+int sd_coalescer_stats(sd_cas_ctx* ctx, uint64_t out[4]);
+
+/* ---------------------------------------------------------------- CPU path (no device) */
+/* The library's own host BLAKE3 (AVX-512 16-lane / AVX2 8-lane / SSE2 4-lane chunk
+ * hashing, picked at run time) with the same file-read semantics as the GPU path.  No
+ * context needed; nthreads host threads (the caller's included). */
+int sd_cpu_simd_lanes(void);
+/* sd_cas_ids on the host: staged messages -> 17-byte hex cas_ids (status as sd_cas_ids) */
+int sd_cpu_cas_ids(const uint8_t* staged, uint64_t staged_bytes, const sd_extent* extents, size_t n,
+                   char* out_hex17, int32_t* status, int nthreads);
+/* sd_cas_ids_files on the host: (path, size) pairs -> cas_ids; status[n] required */
+int sd_cpu_cas_ids_files(const char* const* paths, const uint64_t* sizes, size_t n, char* out_hex17,
+                         int32_t* status, int nthreads);
+/* full BLAKE3 of n byte ranges of one host buffer -> 32 raw bytes each */
+int sd_cpu_checksums(const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
+                     uint8_t* out_hash32, int nthreads);
+/* sd_file_checksums on the host: paths -> 65-byte hex; status[n] required */
+int sd_cpu_file_checksums(const char* const* paths, size_t n, char* out_hex65, int32_t* status, int nthreads);
+/* one file on the calling thread (the latency path's CPU route) */
+int sd_cpu_cas_id_path(const char* path, uint64_t size, char* out_hex17, int32_t* status);
+int sd_cpu_file_checksum_path(const char* path, char* out_hex65, int32_t* status);
 
 /* ---------------------------------------------------------------- dedup (post-hash) */
 /* Bucket records (cas_id as big-endian u64 of the first 8 hash bytes, global file
@@ -223,21 +269,11 @@ int sd_cas_batch_time(sd_cas_ctx* ctx, const sd_cas_batch* batch, const uint8_t*
                       uint8_t* d_hash32, int iters, void* stream, float* ms_total);
 int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, const uint8_t* d_data,
                            uint8_t* d_hash32, int iters, void* stream, float* ms_total);
-/* Process-wide kernel-variant knobs for A/B measurement (results are identical for
- * every value): "sampled_variant" = 10*U + prefetch with U in {1,2,4} chunks per lane
- * and prefetch 0/1/2 (2 = line-pair loads; default 22); "whole_variant" 0 = one fused launch (sampled workgroups + whole-file
- * groups with LDS trees), 1 = separate sampled / whole-leaf / whole-tree kernels, 2 = whole-leaf, then the sampled kernel beside the whole-tree kernel on a
- * batch-internal side stream (joined back into `stream`), 3 = sampled kernel + prefetching
- * chunk-pair leaf + tree over pair nodes, 4 = variant 0 with prefetching chunk-pair leaves,
- * 5 = variant 3 with the pair-node trees merged level-wise in LDS (k_whole_forest),
- * 6 = sampled kernel + host-built work lists: full chunk pairs (k_whole_full), cost-sorted
- * partial/short pairs (k_whole_tail), then two level-wise merge passes of <= 8 nodes per
- * lane (k_whole_merge8), 7 = variant 6 with both pair lists in one launch (k_whole_items),
- * 8 = variant 7 with line-pair loads (default); "whole_lds_kb" = dynamic LDS per
- * k_whole_items workgroup (occupancy A/B, 0); "checksum_variant" 0/1 (1 = line-pair
- * loads, default); "dedup_variant" (sd_dedup_group) 0 = rocPRIM radix sort, 1 = LDS
- * buckets with the radix sort as overflow fallback (default); "coalesce_window_us" /
- * "coalesce_max" (latency path); "files_window_mb" (sd_cas_ids_files). */
+/* Process-wide knobs (results are identical for every value): "coalesce_window_us"
+ * (200), "coalesce_max" (4096) and "latency_cpu_max" (16) of the latency path;
+ * "files_window_mb" (32) of sd_cas_ids_files; "dedup_variant" (sd_dedup_group) 0 =
+ * rocPRIM radix sort, 1 = LDS buckets with the radix sort as overflow fallback (default).
+ * Unknown keys fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);
 /* Read-only probe over d_buf[0, bytes) (bytes a multiple of 4096) for calibrating the
  * PMC byte counters on this kernel family's access patterns: pattern 0 = coalesced

@@ -62,11 +62,52 @@ def sample_windows(size: int) -> list:
 
 
 def cas_message(read_at, size: int) -> bytes:
-    """Exact hashed stream of generate_cas_id; ``read_at(off, n)`` returns file bytes."""
+    """Exact hashed stream of generate_cas_id for a file whose length is ``size``;
+    ``read_at(off, n)`` returns file bytes.  (``cas_message_file`` covers a file whose
+    length differs from ``size``.)"""
     head = struct.pack("<Q", size)  # cas.rs:25 (little-endian u64)
     if size <= MINIMUM_FILE_SIZE:  # cas.rs:27 -- note <=, 102400 is hashed whole
         return head + read_at(0, size)
     return head + b"".join(read_at(o, n) for o, n in sample_windows(size))
+
+
+class UnexpectedEof(EOFError):
+    """read_exact hit the end of the file: io::ErrorKind::UnexpectedEof (cas.rs:36,43,56)."""
+
+
+def cas_message_file(content: bytes, size: int) -> bytes:
+    """generate_cas_id's hashed stream for a file holding ``content`` when the caller passes
+    ``size`` (metadata that may be stale: the two lengths may differ).
+
+    * ``size <= 102400`` (cas.rs:27-29): ``fs::read`` hashes every byte the file holds,
+      however many there are -- ``le64(size) || content``.
+    * else (cas.rs:31-58): each ``read_exact`` at the traced position raises
+      UnexpectedEof when the file ends inside its window; the seeks never fail forward
+      (a seek past EOF is legal, the read after it fails); the footer is read at
+      ``SeekFrom::End(-8192)`` -- the file's real end -- which fails with EINVAL
+      (OSError) when the file is shorter than 8192 bytes.
+    """
+    import errno
+
+    head = struct.pack("<Q", size)
+    if size <= MINIMUM_FILE_SIZE:
+        return head + content
+    wins = sample_windows(size)[:-1]
+    out = [head]
+    for off, n in wins:  # header (:35-38) and the samples (:42-51)
+        if off + n > len(content):
+            raise UnexpectedEof(f"read_exact of {n} bytes at {off} past EOF {len(content)}")
+        out.append(content[off:off + n])
+    end = len(content) - HEADER_OR_FOOTER_SIZE  # :54 seek(End(-8192))
+    if end < 0:
+        raise OSError(errno.EINVAL, "invalid seek to a negative position")
+    out.append(content[end:end + HEADER_OR_FOOTER_SIZE])  # :56-58 (always whole here)
+    return b"".join(out)
+
+
+def generate_cas_id_file(content: bytes, size: int) -> str:
+    """cas.rs:23-62 on a file holding ``content``, called with ``size`` (see cas_message_file)."""
+    return Hasher().update(cas_message_file(content, size)).finalize().hex()[:16]
 
 
 def generate_cas_id(read_at, size: int) -> str:
@@ -85,12 +126,26 @@ def file_checksum(content: bytes) -> str:
     BLAKE3 output is independent of update split points, so the read loop reduces to
     one hash of the whole content; the loop is kept to mirror the reference.
     """
-    h = Hasher()
     pos = 0
-    while True:
-        buf = content[pos:pos + CHECKSUM_READ_LEN]
-        h.update(buf)
+
+    def read(n):
+        nonlocal pos
+        buf = content[pos:pos + n]
         pos += len(buf)
+        return buf
+
+    return file_checksum_reads(read)
+
+
+def file_checksum_reads(read) -> str:
+    """hash.rs:14-20 over a reader: ``read(n)`` is one read call returning up to n bytes
+    (tokio's ``File::read`` issues one ``read`` per call).  Every returned byte is hashed;
+    the loop ends at the first call that returns fewer than BLOCK_LEN bytes -- the end of
+    a regular file, or simply a short read of a pipe."""
+    h = Hasher()
+    while True:
+        buf = read(CHECKSUM_READ_LEN)
+        h.update(buf)
         if len(buf) != CHECKSUM_READ_LEN:
             break
     return h.finalize().hex()

@@ -48,6 +48,8 @@ def lib():
         L.sdo_checksums_simd.restype = I
         L.sdo_cas_ids_files.argtypes = [P, P, U64, P, P, I, I]
         L.sdo_cas_ids_files.restype = I
+        L.sdo_file_checksums.argtypes = [P, U64, P, P, I, I]
+        L.sdo_file_checksums.restype = I
         L.sdo_checksum_synth_mt.argtypes = [U64, U64, ctypes.c_uint32, I, I, P]
         L.sdo_checksum_synth_mt.restype = I
         L.sdo_simd_level.argtypes = [I]
@@ -115,6 +117,17 @@ def cas_ids_files(paths, sizes, nthreads: int = 1, simd: int = -1):
     out = np.zeros((n, 8), np.uint8)
     status = np.zeros(n, np.int32)
     lib().sdo_cas_ids_files(arr, _p(sizes), n, _p(out), _p(status), nthreads, simd)
+    return out, status
+
+
+def file_checksums(paths, nthreads: int = 1, simd: int = -1):
+    """file_checksum over files on disk with the reference's read schedule (hash.rs:10-24:
+    1 MiB read calls until a short one) -> (32-byte hashes [n, 32], sd_file_status [n])."""
+    n = len(paths)
+    arr = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
+    out = np.zeros((n, 32), np.uint8)
+    status = np.zeros(n, np.int32)
+    lib().sdo_file_checksums(arr, n, _p(out), _p(status), nthreads, simd)
     return out, status
 
 

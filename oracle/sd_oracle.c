@@ -185,7 +185,10 @@ uint64_t sdo_cas_message_len(uint64_t size) {
     return size <= MINIMUM_FILE_SIZE ? 8 + size : SAMPLED_MSG_LEN;
 }
 
-/* sample window offsets, cas.rs:35-58 traced literally (see oracle/cas_spec.py) */
+/* sample window offsets, cas.rs:35-58 traced literally (see oracle/cas_spec.py), for a
+ * file whose length is `size`: the footer window is at (file length - 8192), cas.rs:54
+ * seeks SeekFrom::End(-8192).  read_cas_message takes the footer from the real end of
+ * the file instead (the two agree when the file length equals `size`). */
 static int cas_windows(uint64_t size, uint64_t off[6], uint64_t len[6]) {
     int k = 0;
     off[k] = 0; len[k++] = HEADER_OR_FOOTER_SIZE;
@@ -263,7 +266,8 @@ typedef struct {
     atomic_ullong cursor;
 } job_t;
 
-enum { MODE_CAS_STAGED = 0, MODE_CAS_SYNTH = 1, MODE_CHECKSUM = 2, MODE_CHECKSUM_SYNTH = 3, MODE_CAS_FILES = 4 };
+enum { MODE_CAS_STAGED = 0, MODE_CAS_SYNTH = 1, MODE_CHECKSUM = 2, MODE_CHECKSUM_SYNTH = 3, MODE_CAS_FILES = 4,
+       MODE_FILE_CHECKSUM = 5 };
 
 /* read exactly n bytes at the current position (read_exact); 0 ok, -1 EOF, else errno */
 static int read_exact_fd(int fd, uint8_t* p, uint64_t n) {
@@ -276,57 +280,135 @@ static int read_exact_fd(int fd, uint8_t* p, uint64_t n) {
     return 0;
 }
 
-/* generate_cas_id (cas.rs:23-62) with the reference's own read schedule: fs::read of
- * the whole file (size <= 102400, :27-29), else open + read_exact(head) + 4 x
- * (seek, read_exact sample) + seek(End(-8192)) + read_exact(tail) (:31-58).  The
- * message is assembled in `msg` (the le64 header first, :25); returns its length, or
- * -1 with *st = 2 | errno << 16 (I/O error) or 3 (UnexpectedEof), as sd_file_status. */
-static int64_t read_cas_message(const char* path, uint64_t size, uint8_t* msg, int32_t* st) {
-    for (int i = 0; i < 8; i++) msg[i] = (uint8_t)(size >> (8 * i));
+/* generate_cas_id (cas.rs:23-62) with the reference's own read schedule:
+ *   size <= 102400 (:27-29): fs::read -- the file's actual bytes, read until read()
+ *     returns 0, whatever their count (the file may be shorter or longer than `size`,
+ *     which is only hashed as the le64 header, :25);
+ *   else (:31-58): open, read_exact(head) at 0, then per sample read_exact at current_pos
+ *     and seek(Start(current_pos + seek_jump)), then seek(End(-8192)) -- relative to the
+ *     file's real end, failing with EINVAL when the file is shorter than 8192 bytes --
+ *     and read_exact(tail).
+ * The message is assembled in *msg (realloc'd to *cap as needed; the le64 header first,
+ * :25); returns its length, or -1 with *st = 2 | errno << 16 (I/O error) or 3
+ * (read_exact's UnexpectedEof), as sd_file_status. */
+static int64_t read_cas_message(const char* path, uint64_t size, uint8_t** msg, uint64_t* cap, int32_t* st) {
+    if (*cap < 8 + SAMPLED_MSG_LEN + 64) {
+        *cap = 8 + MINIMUM_FILE_SIZE + 64;
+        *msg = (uint8_t*)realloc(*msg, *cap);
+    }
+    for (int i = 0; i < 8; i++) (*msg)[i] = (uint8_t)(size >> (8 * i));
     int fd = open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) { *st = 2 | (errno << 16); return -1; }
-    int64_t len = 8;
+    uint64_t len = 8;
     int rc = 0;
-    if (size <= MINIMUM_FILE_SIZE) { /* fs::read: the file's actual bytes, up to EOF */
+    if (size <= MINIMUM_FILE_SIZE) { /* fs::read: read_to_end */
         for (;;) {
-            ssize_t r = read(fd, msg + len, 8 + MINIMUM_FILE_SIZE + 1 - (uint64_t)len);
+            if (*cap - len < 4096) { *cap *= 2; *msg = (uint8_t*)realloc(*msg, *cap); }
+            ssize_t r = read(fd, *msg + len, *cap - len);
             if (r < 0) { if (errno == EINTR) continue; rc = errno; break; }
             if (r == 0) break;
-            len += r;
-            if ((uint64_t)len > 8 + MINIMUM_FILE_SIZE) { rc = EFBIG; break; }
+            len += (uint64_t)r;
         }
     } else {
         uint64_t off[6], wl[6];
         int k = cas_windows(size, off, wl);
         for (int i = 0; i < k && !rc; i++) {
-            if (lseek(fd, (off_t)off[i], SEEK_SET) < 0) { rc = errno; break; }
-            rc = read_exact_fd(fd, msg + len, wl[i]);
-            len += (int64_t)wl[i];
+            off_t at;
+            if (i == k - 1) at = lseek(fd, -(off_t)HEADER_OR_FOOTER_SIZE, SEEK_END); /* :54 */
+            else at = lseek(fd, (off_t)off[i], SEEK_SET);
+            if (at < 0) { rc = errno; break; }
+            rc = read_exact_fd(fd, *msg + len, wl[i]);
+            len += wl[i];
         }
     }
     close(fd);
     if (rc == -1) { *st = 3; return -1; }
     if (rc) { *st = 2 | (rc << 16); return -1; }
     *st = 0;
-    return len;
+    return (int64_t)len;
+}
+
+/* subtree CV / whole-message hash with the SIMD hasher (sd_oracle_simd.c) */
+void sdo_subtree_simd(const uint8_t* data, uint64_t len, uint64_t chunk0, int root, uint8_t out[32], int lvl,
+                      uint8_t* scratch);
+
+/* file_checksum (hash.rs:10-24) with the reference's read schedule: one read() of up to
+ * BLOCK_LEN = 1 MiB per iteration (:15, tokio's File::read is one read call), every
+ * returned byte hashed (:16), stop at the first read that returns fewer than 1 MiB
+ * (:17-19).  The hasher is the crate's structure at 1 MiB granularity: each full 1 MiB
+ * piece is a complete 1024-chunk subtree (hashed with hash_many when simd > 0), pushed
+ * on a CV stack only once more input is known to follow (the crate's lazy merge), and
+ * the final piece is merged down the stack with ROOT on the last parent.  Returns 0, or
+ * an sd_file_status (2 | errno << 16). */
+static int32_t file_checksum_fd(int fd, uint8_t out[32], int simd, uint8_t* buf, uint8_t* scratch) {
+    const uint64_t BL = 1u << 20;
+    uint32_t stack[64][8];
+    int sp = 0;
+    uint64_t blocks = 0, have = 0; /* `have`: bytes of the pending (last read) piece */
+    int pending = 0;
+    for (;;) {
+        ssize_t r;
+        for (;;) {
+            r = read(fd, buf + (pending ? BL : 0), BL);
+            if (r < 0 && errno == EINTR) continue;
+            break;
+        }
+        if (r < 0) return 2 | (errno << 16);
+        if (pending && r > 0) { /* the pending full piece is not the last: push its CV */
+            uint8_t cv[32];
+            sdo_subtree_simd(buf, BL, blocks * 1024, 0, cv, simd, scratch);
+            blocks++;
+            memcpy(stack[sp++], cv, 32);
+            for (uint64_t t = blocks; (t & 1) == 0; t >>= 1) {
+                sp--;
+                parent_cv(stack[sp - 1], stack[sp], 0, stack[sp - 1]);
+            }
+            memmove(buf, buf + BL, (size_t)r);
+        }
+        if (!pending || r > 0) have = (uint64_t)r;
+        pending = 1;
+        if ((uint64_t)r != BL) break; /* :17-19 */
+    }
+    /* the last piece: buf[0, have) at chunk blocks * 1024 */
+    if (sp == 0) {
+        if (simd && have > 1024) sdo_subtree_simd(buf, have, 0, 1, out, simd, scratch);
+        else sdo_blake3(buf, have, out);
+        return 0;
+    }
+    uint32_t cur[8];
+    sdo_subtree_simd(buf, have, blocks * 1024, 0, (uint8_t*)cur, simd, scratch);
+    for (int i = sp - 1; i >= 1; i--) parent_cv(stack[i], cur, 0, cur);
+    parent_cv(stack[0], cur, F_ROOT, cur);
+    memcpy(out, cur, 32);
+    return 0;
 }
 
 
 static void* worker(void* arg) {
     job_t* j = (job_t*)arg;
     uint8_t* scratch = NULL;
+    uint64_t scratch_cap = 0;
     if (j->mode == MODE_CAS_SYNTH) scratch = (uint8_t*)malloc(8 + MINIMUM_FILE_SIZE);
     if (j->mode == MODE_CHECKSUM_SYNTH) scratch = (uint8_t*)malloc(1u << 20);
-    if (j->mode == MODE_CAS_FILES) scratch = (uint8_t*)malloc(8 + MINIMUM_FILE_SIZE + 64);
+    if (j->mode == MODE_FILE_CHECKSUM) scratch = (uint8_t*)malloc((2u << 20) + 64);
     uint8_t* cvs = NULL;
     uint64_t cvs_cap = 0;
     for (;;) {
         uint64_t i = atomic_fetch_add(&j->cursor, 1);
         if (i >= j->n) break;
         uint8_t h[32];
-        if (j->mode == MODE_CAS_FILES) {
+        if (j->mode == MODE_FILE_CHECKSUM) {
+            if (!cvs) { cvs_cap = 32 * 1025; cvs = (uint8_t*)malloc(cvs_cap); }
+            memset(h, 0, 32);
+            int fd = open(j->paths[i], O_RDONLY | O_CLOEXEC);
+            if (fd < 0) j->status[i] = 2 | (errno << 16);
+            else {
+                j->status[i] = file_checksum_fd(fd, h, j->simd, scratch, cvs);
+                close(fd);
+            }
+        } else if (j->mode == MODE_CAS_FILES) {
             int32_t st = 0;
-            int64_t m = read_cas_message(j->paths[i], j->sizes[i], scratch, &st);
+            int64_t m = read_cas_message(j->paths[i], j->sizes[i], &scratch, &scratch_cap, &st);
             j->status[i] = st;
             if (m < 0) { memset(h, 0, 32); }
             else if (j->simd) {
@@ -464,6 +546,17 @@ int sdo_cas_ids_files(const char* const* paths, const uint64_t* sizes, uint64_t 
     job_t j = {0};
     j.mode = MODE_CAS_FILES; j.n = n; j.paths = paths; j.sizes = sizes; j.status = status;
     j.out = out8; j.out_stride = 8;
+    j.simd = simd == 0 ? 0 : sdo_simd_level(simd);
+    run_job(&j, nthreads);
+    return j.simd;
+}
+
+/* full checksums of files on disk through the reference's read schedule
+ * (file_checksum_fd, hash.rs:10-24); status[n] as sd_file_status.  Returns the level. */
+int sdo_file_checksums(const char* const* paths, uint64_t n, uint8_t* out32, int32_t* status, int nthreads, int simd) {
+    job_t j = {0};
+    j.mode = MODE_FILE_CHECKSUM; j.n = n; j.paths = paths; j.status = status;
+    j.out = out32; j.out_stride = 32;
     j.simd = simd == 0 ? 0 : sdo_simd_level(simd);
     run_job(&j, nthreads);
     return j.simd;

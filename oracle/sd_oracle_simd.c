@@ -320,6 +320,50 @@ void sdo_blake3_simd(const uint8_t* data, uint64_t len, uint8_t out[32], int lvl
     memcpy(out, o, 32);
 }
 
+/* CV of the subtree over data[0, len) whose first chunk has index chunk0 -- an aligned
+ * power-of-two group of chunks, or the final group of a message -- merged level-wise
+ * (the odd node carried up), non-root; or, with root (chunk0 = 0), the whole message's
+ * hash.  lvl 0 = scalar compressions, 1/2 = hash_many.  scratch: 32 * ceil(len/1024). */
+void sdo_subtree_simd(const uint8_t* data, uint64_t len, uint64_t chunk0, int root, uint8_t out[32], int lvl,
+                      uint8_t* scratch) {
+    const uint64_t C = len == 0 ? 1 : (len + 1023) / 1024;
+    uint32_t cv[8], m[16], o[16];
+    if (C == 1) {
+        scalar_chunk(data, (uint32_t)len, chunk0, root, cv);
+        memcpy(out, cv, 32);
+        return;
+    }
+    const uint8_t* ptrs[64];
+    for (uint64_t c0 = 0; c0 < C - 1; c0 += 64) {
+        int k = (int)((C - 1 - c0) < 64 ? (C - 1 - c0) : 64);
+        if (lvl) {
+            for (int i = 0; i < k; i++) ptrs[i] = data + 1024 * (c0 + i);
+            hash_many(lvl, ptrs, k, 16, chunk0 + c0, 1, 0, FS_CHUNK_START, FS_CHUNK_END, scratch + 32 * c0);
+        } else {
+            for (int i = 0; i < k; i++) {
+                scalar_chunk(data + 1024 * (c0 + i), 1024, chunk0 + c0 + i, 0, cv);
+                memcpy(scratch + 32 * (c0 + i), cv, 32);
+            }
+        }
+    }
+    scalar_chunk(data + 1024 * (C - 1), (uint32_t)(len - 1024 * (C - 1)), chunk0 + C - 1, 0, cv);
+    memcpy(scratch + 32 * (C - 1), cv, 32);
+    uint64_t nodes = C;
+    while (nodes > 2) {
+        uint64_t P = nodes / 2;
+        for (uint64_t p = 0; p < P; p++) {
+            memcpy(m, scratch + 64 * p, 64);
+            sdo_compress_words(IV_, m, 0, 64, FS_PARENT, o);
+            memcpy(scratch + 32 * p, o, 32);
+        }
+        if (nodes & 1) memmove(scratch + 32 * P, scratch + 32 * (nodes - 1), 32);
+        nodes = P + (nodes & 1);
+    }
+    memcpy(m, scratch, 64);
+    sdo_compress_words(IV_, m, 0, 64, FS_PARENT | (root ? FS_ROOT : 0), o);
+    memcpy(out, o, 32);
+}
+
 /* ----------------------------------------------- multi-threaded checksum of one file */
 /* Full BLAKE3 (hash.rs:10-24) of one synthetic file of `size` bytes (content cid/twin of
  * sdo_synth_fill) on nthreads threads: the threads generate 1 MiB windows and hash their

@@ -1,8 +1,8 @@
 """Loader for the in-tree HIP library ``spacedrive_amd/libsdcas.so`` (C ABI: include/sd_cas.h).
 
-There is no CPU fallback: importing the product path without the built library raises,
-and every compute entry point of the library fails with SD_ERR_DEVICE when no gfx950
-device is present.
+Importing the product path without the built library raises (there is no Python
+fallback).  The library's GPU entry points fail with SD_ERR_DEVICE without a gfx950
+device; its sd_cpu_* entry points are the explicit CPU path (include/sd_cas.h).
 
 torch is imported first on purpose: the torch wheel ships its own ``libamdhip64.so.7``
 and the library's ``NEEDED libamdhip64.so.7`` must bind to that same copy, so that one
@@ -22,7 +22,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "sd_cas.h")
 SD_OK = 0
 RC_NAMES = {0: "SD_OK", -1: "SD_ERR_INVALID", -2: "SD_ERR_DEVICE", -3: "SD_ERR_NOMEM",
             -4: "SD_ERR_INTERNAL", -5: "SD_ERR_COMM"}
-SD_FILE_OK, SD_FILE_SKIPPED_EMPTY, SD_FILE_IO_ERROR, SD_FILE_SHORT_READ = 0, 1, 2, 3
+SD_FILE_OK, SD_FILE_SKIPPED_EMPTY, SD_FILE_IO_ERROR, SD_FILE_SHORT_READ, SD_FILE_CHANGED = 0, 1, 2, 3, 4
 SD_KIND_WHOLE, SD_KIND_SAMPLED = 1, 2
 SAMPLED_MSG_LEN = 57352
 STAGE_ALIGN = 128
@@ -74,6 +74,13 @@ SIGNATURES = [
     ("sd_cas_id_path", I32, [P, ctypes.c_char_p, U64, P, ctypes.POINTER(ctypes.c_int32)]),
     ("sd_file_checksum_path", I32, [P, ctypes.c_char_p, P, ctypes.POINTER(ctypes.c_int32)]),
     ("sd_coalescer_stats", I32, [P, P]),
+    ("sd_cpu_simd_lanes", I32, []),
+    ("sd_cpu_cas_ids", I32, [P, U64, P, SZ, P, P, I32]),
+    ("sd_cpu_cas_ids_files", I32, [P, P, SZ, P, P, I32]),
+    ("sd_cpu_checksums", I32, [P, P, P, SZ, P, I32]),
+    ("sd_cpu_file_checksums", I32, [P, SZ, P, P, I32]),
+    ("sd_cpu_cas_id_path", I32, [ctypes.c_char_p, U64, P, ctypes.POINTER(ctypes.c_int32)]),
+    ("sd_cpu_file_checksum_path", I32, [ctypes.c_char_p, P, ctypes.POINTER(ctypes.c_int32)]),
     ("sd_dedup_partition", I32, [P, P, P, U64, U64, I32, P, P, PU64, P]),
     ("sd_dedup_group", I32, [P, P, U64, I32, P, PU64, P]),
     ("sd_dedup_owners", I32, [P, P, U64, P, U64, P, P]),

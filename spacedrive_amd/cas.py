@@ -10,14 +10,22 @@ Same names, argument meaning and error behaviour as the Rust functions they repl
 * ``FileMetadata.new(path)``              -- core/src/object/file_identifier/mod.rs:59-97
   (``cas_id`` is ``None`` for an empty file; directories are rejected).
 
-I/O errors surface as ``OSError`` (the reference's ``io::Error``); a file shorter than
-the ``size`` it was planned with raises ``UnexpectedEofError`` (``read_exact``'s
-``io::ErrorKind::UnexpectedEof``, cas.rs:36,43,56).  The batched variants return one
-result or exception per input, which lets callers keep the reference's per-caller
-policy (identifier: log and drop, file_identifier/mod.rs:127-128; validator: abort the
-step, validator_job.rs:147-149).
+Files are read with the reference's semantics whatever their length: ``size`` is only
+hashed (le64) and picks the branch; a whole-kind file contributes every byte it holds
+(``fs::read``, cas.rs:29), a sampled one its head and samples by ``read_exact`` and its
+tail at ``SeekFrom::End(-8192)`` (cas.rs:31-58); a checksum hashes 1 MiB reads until a
+short one (hash.rs:14-20).  I/O errors surface as ``OSError`` (the reference's
+``io::Error``); a sample or header past the end of the file raises
+``UnexpectedEofError`` (``read_exact``'s ``io::ErrorKind::UnexpectedEof``, cas.rs:36,43,
+56).  The batched variants return one result or exception per input, which lets callers
+keep the reference's per-caller policy (identifier: log and drop,
+file_identifier/mod.rs:127-128; validator: abort the step, validator_job.rs:147-149).
 
-Hashing always runs in libsdcas.so on the GPU; there is no CPU path here.
+Batches hash on the GPU (libsdcas.so's HIP kernels).  The single-file calls follow the
+library's latency policy (include/sd_cas.h, sd_cas_id_path): hashed on the calling
+thread by the library's CPU path while few calls are in flight, coalesced into GPU
+batches beyond that.  ``spacedrive_amd.cpu`` exposes the CPU path explicitly (a node
+without the device).
 """
 from __future__ import annotations
 
@@ -120,10 +128,17 @@ def file_checksum(path: Union[str, os.PathLike], device: Optional[int] = None) -
 
 
 def coalescer_stats(device: Optional[int] = None) -> dict:
-    """Latency-path counters of the device's default context."""
-    v = np.zeros(3, np.uint64)
+    """Latency-path counters of the device's default context: single-file requests, the
+    GPU batches they were coalesced into, the largest batch, and requests hashed on the
+    CPU path."""
+    v = np.zeros(4, np.uint64)
     check(lib().sd_coalescer_stats(default_context(device).handle, _ptr(v)))
-    return {"requests": int(v[0]), "batches": int(v[1]), "max_batch": int(v[2])}
+    return {"requests": int(v[0]), "batches": int(v[1]), "max_batch": int(v[2]), "cpu": int(v[3])}
+
+
+def set_tuning(key: str, value: int) -> None:
+    """sd_cas_set_tuning (process-wide knobs, include/sd_cas.h)."""
+    check(lib().sd_cas_set_tuning(key.encode(), int(value)))
 
 
 @dataclass

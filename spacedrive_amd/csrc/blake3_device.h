@@ -138,24 +138,7 @@ __device__ __forceinline__ void chunk_cv(uint32_t (&cv)[8], const uint8_t* __res
     compress(cv, m, clo, chi, tail, (last == 0 ? CHUNK_START : 0u) | CHUNK_END | (is_root ? ROOT : 0u));
 }
 
-// Full 1 KiB non-root chunk: 16 blocks, no bounds logic.
-__device__ __forceinline__ void full_chunk_cv(uint32_t (&cv)[8], const uint8_t* __restrict__ p,
-                                              uint64_t counter) {
-    set_iv(cv);
-    const uint32_t clo = (uint32_t)counter, chi = (uint32_t)(counter >> 32);
-    uint32_t m[16];
-    load_block(m, p);
-    compress(cv, m, clo, chi, BLOCK_LEN, CHUNK_START);
-#pragma unroll 1
-    for (uint32_t b = 1; b < 15; b++) {
-        load_block(m, p + 64u * b);
-        compress(cv, m, clo, chi, BLOCK_LEN, 0u);
-    }
-    load_block(m, p + 64u * 15);
-    compress(cv, m, clo, chi, BLOCK_LEN, CHUNK_END);
-}
-
-// full_chunk_cv with line-pair loads (see full_chunks_cv, PF = 2)
+// Full 1 KiB non-root chunk with line-pair loads (see full_chunks_cv)
 __device__ __forceinline__ void full_chunk_cv_lp(uint32_t (&cv)[8], const uint8_t* __restrict__ p,
                                                  uint64_t counter) {
     set_iv(cv);
@@ -171,19 +154,16 @@ __device__ __forceinline__ void full_chunk_cv_lp(uint32_t (&cv)[8], const uint8_
 }
 
 // Merge of U consecutive, full, non-root chunks c0..c0+U-1 (an aligned group, U = 1, 2, 4):
-// the chunk CVs merged level-wise in-lane -> `out`.  Message loads (PF):
-//   0  each block loaded just before its compression (other waves hide the latency);
-//   1  two register buffers: block k+1 is loaded while block k is compressed, so a lane
-//      always has one 64-byte load in flight behind its compression;
-//   2  line pairs: blocks 2k and 2k+1 -- one 128-byte cache line -- are loaded back to
-//      back into the two buffers, then both compressed, so a line is consumed whole
-//      instead of across a compression (fewer L2 re-fetches when many lanes stream).
-template <int U, int PF>
+// the chunk CVs merged level-wise in-lane -> `out`.  Line-pair loads: blocks 2k and 2k+1 --
+// one 128-byte cache line -- are loaded back to back into two register buffers, then both
+// compressed, so a line is consumed whole instead of across a compression (with ~7 MB of
+// lines in flight per XCD against a 4 MB L2, half-consumed lines were evicted and fetched
+// again: 1.10x the algorithmic HBM bytes before, 1.00x after).
+template <int U>
 __device__ __forceinline__ void full_chunks_cv(uint32_t (&out)[8], const uint8_t* __restrict__ p, uint64_t c0) {
     static_assert(U == 1 || U == 2 || U == 4, "U");
     uint32_t held[2][8];  // level-wise merge stack: at most two pending nodes for U <= 4
     uint32_t ma[16], mb[16];
-    if (PF == 1) load_block(ma, p);
 #pragma unroll
     for (int u = 0; u < U; u++) {
         uint32_t cv[8];
@@ -193,27 +173,10 @@ __device__ __forceinline__ void full_chunks_cv(uint32_t (&out)[8], const uint8_t
         const uint8_t* q = p + (size_t)u * CHUNK_LEN;
 #pragma unroll 1
         for (uint32_t b = 0; b < 16; b += 2) {
-            const uint32_t f0 = b == 0 ? CHUNK_START : 0u;
-            const uint32_t f1 = b + 1 == 15 ? CHUNK_END : 0u;
-            if (PF == 2) {
-                load_block(ma, q + 64u * b);
-                load_block(mb, q + 64u * (b + 1));
-                compress(cv, ma, clo, chi, BLOCK_LEN, f0);
-                compress(cv, mb, clo, chi, BLOCK_LEN, f1);
-            } else if (PF == 1) {
-                load_block(mb, q + 64u * (b + 1));
-                compress(cv, ma, clo, chi, BLOCK_LEN, f0);
-                // next block: b + 2 of this chunk, or block 0 of the next chunk (the last
-                // lane block re-reads itself rather than run past the group)
-                const uint32_t nb = (uint32_t)u * 16 + b + 2;
-                load_block(ma, p + 64u * (nb < 16u * U ? nb : 16u * U - 1));
-                compress(cv, mb, clo, chi, BLOCK_LEN, f1);
-            } else {
-                load_block(ma, q + 64u * b);
-                compress(cv, ma, clo, chi, BLOCK_LEN, f0);
-                load_block(ma, q + 64u * (b + 1));
-                compress(cv, ma, clo, chi, BLOCK_LEN, f1);
-            }
+            load_block(ma, q + 64u * b);
+            load_block(mb, q + 64u * (b + 1));
+            compress(cv, ma, clo, chi, BLOCK_LEN, b == 0 ? CHUNK_START : 0u);
+            compress(cv, mb, clo, chi, BLOCK_LEN, b + 1 == 15 ? CHUNK_END : 0u);
         }
         if (U == 1) {
 #pragma unroll
@@ -232,55 +195,6 @@ __device__ __forceinline__ void full_chunks_cv(uint32_t (&out)[8], const uint8_t
             parent(p23, held[1], cv, 0u);
             parent(out, held[0], p23, 0u);
         }
-    }
-}
-
-// 64-byte block q of a message group whose last block (lastq) holds `tail` bytes (1..64)
-__device__ __forceinline__ void load_block_q(uint32_t (&m)[16], const uint8_t* __restrict__ p, uint32_t q,
-                                             uint32_t lastq, uint32_t tail) {
-    if (q == lastq && tail < 64u) load_block_partial(m, p + 64u * q, tail);
-    else load_block(m, p + 64u * q);
-}
-
-// Chaining value of an aligned chunk PAIR (c0, c0 + 1) of a message: `glen` (1..2048)
-// bytes at p, i.e. chunk c0 is full when glen > 1024.  The pair's blocks are consecutive,
-// so the message streams through two register buffers with block q+1 loading while q
-// compresses (as full_chunks_cv does for full chunks).  root: the pair is the whole
-// message -- ROOT goes on the last block of a single chunk, or on the pair's parent.
-__device__ __forceinline__ void pair_cv(uint32_t (&out)[8], const uint8_t* __restrict__ p, uint32_t glen,
-                                        uint64_t c0, bool root) {
-    const uint32_t nq = (glen + 63u) >> 6;
-    const uint32_t lastq = nq - 1u, tail = glen - 64u * lastq;
-    const bool two = glen > CHUNK_LEN;
-    uint32_t cv[8], held[8], ma[16], mb[16];
-    set_iv(cv);
-    load_block_q(ma, p, 0u, lastq, tail);
-#define SD_PAIR_STEP(Q, M)                                                                               \
-    do {                                                                                                 \
-        const uint32_t b_ = (Q) & 15u, u_ = (Q) >> 4;                                                    \
-        const bool endc_ = b_ == 15u || (Q) == lastq;                                                    \
-        const uint32_t fl_ = (b_ == 0u ? CHUNK_START : 0u) | (endc_ ? CHUNK_END : 0u) |                  \
-                             (((Q) == lastq && root && !two) ? ROOT : 0u);                                \
-        const uint64_t ctr_ = c0 + u_;                                                                   \
-        compress(cv, M, (uint32_t)ctr_, (uint32_t)(ctr_ >> 32), (Q) == lastq ? tail : BLOCK_LEN, fl_);   \
-        if (b_ == 15u && u_ == 0u && two) {                                                              \
-            _Pragma("unroll") for (int i_ = 0; i_ < 8; i_++) held[i_] = cv[i_];                          \
-            set_iv(cv);                                                                                  \
-        }                                                                                                \
-    } while (0)
-#pragma unroll 1
-    for (uint32_t q = 0; q < nq; q += 2) {
-        if (q + 1u < nq) load_block_q(mb, p, q + 1u, lastq, tail);
-        SD_PAIR_STEP(q, ma);
-        if (q + 1u >= nq) break;
-        if (q + 2u < nq) load_block_q(ma, p, q + 2u, lastq, tail);
-        SD_PAIR_STEP(q + 1u, mb);
-    }
-#undef SD_PAIR_STEP
-    if (two) parent(out, held, cv, root ? ROOT : 0u);
-    else {
-#pragma unroll
-        for (int i = 0; i < 8; i++) out[i] = cv[i];
     }
 }
 

@@ -4,17 +4,20 @@
 // (core/src/location/manager/watcher/utils.rs:235 on create, :393 on update, checksum
 // recompute :438-446) and non_indexed::walk (core/src/location/non_indexed.rs:164-187),
 // each an independent tokio task calling generate_cas_id(path, size) / file_checksum.
-// A GPU round trip per file would waste the device, and libsdcas has no CPU path, so
-// concurrent single-file calls meet here: a dispatcher thread per context waits for the
-// first request, keeps collecting for a short window (tuning "coalesce_window_us",
-// default 200) or until "coalesce_max" requests (default 4096) are queued, then stages
-// the whole batch with the pread pool (sd_cas_stage_files) into pinned memory and hashes
-// it with one sd_cas_ids / sd_file_checksums call.  Requests that arrive meanwhile form
-// the next batch, so a busy watcher is served at batch throughput and an idle one at
-// window + one small batch of latency.  Each caller blocks only on its own request.
+// Policy: one GPU round trip per file costs more than hashing
+// the file on the host, so while fewer than "latency_cpu_max" (default 16) single-file
+// calls are in flight on the context, a call is hashed on its own thread by the CPU path
+// (cpu_blake3.cpp).  Beyond that, concurrent calls meet here: a dispatcher thread per
+// context waits for the first request, keeps collecting for a short window (tuning
+// "coalesce_window_us", default 200) or until "coalesce_max" requests (default 4096) are
+// queued, then hashes the whole batch with one sd_cas_ids_files / sd_file_checksums
+// call.  Requests that arrive meanwhile form the next batch, so a busy watcher is served
+// at batch throughput and an idle one at CPU latency.  Each caller blocks only on its own
+// request.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -42,9 +45,8 @@ struct sd_coalescer {
     std::deque<Req*> q;
     bool stop = false;
     std::thread th;
-    uint64_t n_requests = 0, n_batches = 0, max_batch = 0;
-    void* pinned = nullptr;
-    uint64_t pinned_bytes = 0;
+    uint64_t n_requests = 0, n_batches = 0, max_batch = 0, n_cpu = 0;
+    uint64_t inflight = 0;  // single-file calls inside submit(), either route
 
     explicit sd_coalescer(sd_cas_ctx* c) : ctx(c) { th = std::thread([this] { loop(); }); }
     ~sd_coalescer() {
@@ -54,16 +56,27 @@ struct sd_coalescer {
         }
         work.notify_all();
         if (th.joinable()) th.join();
-        if (pinned) sd_cas_host_free(ctx, pinned);
     }
 
     int submit(Req& r) {
         std::unique_lock<std::mutex> g(mu);
         if (stop) return SD_ERR_INVALID;
-        q.push_back(&r);
         n_requests++;
+        const int cpu_max = tuning_get(SD_TUNE_LATENCY_CPU_MAX);
+        if (cpu_max > 0 && inflight < (uint64_t)cpu_max) {  // few callers: hash on this thread
+            inflight++;
+            n_cpu++;
+            g.unlock();
+            *r.status = r.kind == 0 ? cpu_cas_id_file(r.path, r.size, r.out) : cpu_checksum_file(r.path, r.out);
+            g.lock();
+            inflight--;
+            return SD_OK;
+        }
+        inflight++;
+        q.push_back(&r);
         work.notify_one();
         done.wait(g, [&] { return r.done; });
+        inflight--;
         return r.rc;
     }
 
@@ -83,22 +96,10 @@ struct sd_coalescer {
             sizes[i] = batch[i]->size;
             paths[i] = batch[i]->path;
         }
-        std::vector<sd_extent> ext(n);
-        uint64_t total = 0;
-        int rc = sd_cas_stage_plan(sizes.data(), n, ext.data(), &total);
-        if (rc == SD_OK && total > pinned_bytes) {
-            if (pinned) sd_cas_host_free(ctx, pinned);
-            pinned = nullptr;
-            pinned_bytes = 0;
-            rc = sd_cas_host_alloc(ctx, total * 2, &pinned);
-            if (rc == SD_OK) pinned_bytes = total * 2;
-        }
         std::vector<int32_t> st(n, SD_FILE_OK);
         std::vector<char> hex(17 * n, 0);
-        const int threads = (int)std::min<size_t>(16, n);
-        if (rc == SD_OK)
-            rc = sd_cas_stage_files(paths.data(), ext.data(), n, (uint8_t*)pinned, st.data(), threads);
-        if (rc == SD_OK) rc = sd_cas_ids(ctx, (const uint8_t*)pinned, total, ext.data(), n, hex.data(), st.data());
+        const int rc = sd_cas_ids_files(ctx, paths.data(), sizes.data(), n, hex.data(), st.data(),
+                                        (int)std::min<size_t>(16, n));
         if (rc != SD_OK) return fail(batch, rc);
         for (size_t i = 0; i < n; i++) {
             *batch[i]->status = st[i];
@@ -165,9 +166,10 @@ int coalescer_submit(sd_coalescer* c, int kind, const char* path, uint64_t size,
     return rc;
 }
 
-void coalescer_stats(sd_coalescer* c, uint64_t out[3]) {
+void coalescer_stats(sd_coalescer* c, uint64_t out[4]) {
     std::lock_guard<std::mutex> g(c->mu);
     out[0] = c->n_requests;
     out[1] = c->n_batches;
     out[2] = c->max_batch;
+    out[3] = c->n_cpu;
 }

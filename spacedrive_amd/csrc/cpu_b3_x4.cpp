@@ -1,0 +1,4 @@
+// 4-lane instantiation of cpu_b3_lanes.inc (see the Makefile for its ISA flags)
+#define SD_LANES 4
+#define SD_CHUNKS_FN cpu_hash_chunks_x4
+#include "cpu_b3_lanes.inc"

@@ -1,0 +1,4 @@
+// 8-lane instantiation of cpu_b3_lanes.inc (see the Makefile for its ISA flags)
+#define SD_LANES 8
+#define SD_CHUNKS_FN cpu_hash_chunks_x8
+#include "cpu_b3_lanes.inc"

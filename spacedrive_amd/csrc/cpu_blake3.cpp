@@ -1,0 +1,329 @@
+// cpu_blake3.cpp -- the library's CPU path: BLAKE3 on the host and the sd_cpu_* entry points.
+//
+// SURVEY.md §8(b) asks for a CPU variant of each export -- for a node without a gfx950
+// device, and for the latency path's single-file callers (the location watcher,
+// core/src/location/manager/watcher/utils.rs:235,393,438-446, and non_indexed::walk,
+// core/src/location/non_indexed.rs:164-187), where one GPU round trip per file costs more
+// than hashing the file on the calling thread.  It reads files with the same semantics as
+// the GPU path (sd_host.cpp: stage_one, MsgSource) and hashes with:
+//   * whole 1 KiB chunks many at a time, one chunk per SIMD lane (cpu_b3_lanes.inc:
+//     AVX-512 16 lanes, AVX2 8, SSE2 4 -- chosen at run time);
+//   * the BLAKE3 spec's incremental structure: the last chunk of the input stays buffered
+//     until more input arrives, complete chunks push their CV on a stack that merges
+//     every completed subtree, finalize merges the stack into the root (ROOT on the
+//     final compression).
+#include <errno.h>
+#include <fcntl.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <memory>
+#include <thread>
+#include <vector>
+
+#include "sd_host.h"
+
+void cpu_hash_chunks_x16(const uint8_t* const* in, int n, uint64_t ctr0, uint32_t (*cv)[8]);
+void cpu_hash_chunks_x8(const uint8_t* const* in, int n, uint64_t ctr0, uint32_t (*cv)[8]);
+void cpu_hash_chunks_x4(const uint8_t* const* in, int n, uint64_t ctr0, uint32_t (*cv)[8]);
+
+namespace {
+
+constexpr uint32_t CHUNK_START = 1, CHUNK_END = 2, PARENT = 4, ROOT = 8;
+constexpr uint32_t IV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,
+                            0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u};
+constexpr uint8_t PERM[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+
+inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+// one compression: cv <- first 8 words of compress(cv, m, counter, len, flags)
+void compress1(uint32_t cv[8], const uint32_t m_in[16], uint64_t counter, uint32_t len, uint32_t flags) {
+    uint32_t m[16], s[16];
+    memcpy(m, m_in, 64);
+    for (int i = 0; i < 8; i++) s[i] = cv[i];
+    for (int i = 0; i < 4; i++) s[8 + i] = IV[i];
+    s[12] = (uint32_t)counter;
+    s[13] = (uint32_t)(counter >> 32);
+    s[14] = len;
+    s[15] = flags;
+    auto g = [&](int a, int b, int c, int d, uint32_t x, uint32_t y) {
+        s[a] = s[a] + s[b] + x; s[d] = rotr(s[d] ^ s[a], 16);
+        s[c] = s[c] + s[d];     s[b] = rotr(s[b] ^ s[c], 12);
+        s[a] = s[a] + s[b] + y; s[d] = rotr(s[d] ^ s[a], 8);
+        s[c] = s[c] + s[d];     s[b] = rotr(s[b] ^ s[c], 7);
+    };
+    for (int r = 0; r < 7; r++) {
+        g(0, 4, 8, 12, m[0], m[1]);
+        g(1, 5, 9, 13, m[2], m[3]);
+        g(2, 6, 10, 14, m[4], m[5]);
+        g(3, 7, 11, 15, m[6], m[7]);
+        g(0, 5, 10, 15, m[8], m[9]);
+        g(1, 6, 11, 12, m[10], m[11]);
+        g(2, 7, 8, 13, m[12], m[13]);
+        g(3, 4, 9, 14, m[14], m[15]);
+        uint32_t t[16];
+        for (int i = 0; i < 16; i++) t[i] = m[PERM[i]];
+        memcpy(m, t, 64);
+    }
+    for (int i = 0; i < 8; i++) cv[i] = s[i] ^ s[i + 8];
+}
+
+void parent_cv(const uint32_t l[8], const uint32_t r[8], uint32_t extra, uint32_t out[8]) {
+    uint32_t m[16];
+    memcpy(m, l, 32);
+    memcpy(m + 8, r, 32);
+    memcpy(out, IV, 32);
+    compress1(out, m, 0, 64, PARENT | extra);
+}
+
+// CV of one chunk of len (0..1024) bytes, chunk index counter; ROOT on its last block
+void chunk_cv(const uint8_t* p, uint32_t len, uint64_t counter, bool root, uint32_t cv[8]) {
+    memcpy(cv, IV, 32);
+    const uint32_t nb = len == 0 ? 1 : (len + 63) / 64;
+    for (uint32_t b = 0; b < nb; b++) {
+        const uint32_t bl = b + 1 < nb ? 64 : len - 64 * b;
+        uint8_t blk[64] = {0};
+        memcpy(blk, p + 64 * b, bl);
+        uint32_t m[16];
+        memcpy(m, blk, 64);  // little-endian host
+        const uint32_t fl = (b == 0 ? CHUNK_START : 0) | (b + 1 == nb ? CHUNK_END : 0) | (root && b + 1 == nb ? ROOT : 0);
+        compress1(cv, m, counter, bl, fl);
+    }
+}
+
+using chunks_fn = void (*)(const uint8_t* const*, int, uint64_t, uint32_t (*)[8]);
+struct Simd {
+    chunks_fn fn;
+    int lanes;
+};
+Simd pick_simd() {
+    __builtin_cpu_init();
+    // SD_CPU_LANES=4/8 caps the width (tests run every width the CPU has)
+    const char* cap = getenv("SD_CPU_LANES");
+    const int lim = cap ? atoi(cap) : 16;
+    if (lim >= 16 && __builtin_cpu_supports("avx512f")) return {cpu_hash_chunks_x16, 16};
+    if (lim >= 8 && __builtin_cpu_supports("avx2")) return {cpu_hash_chunks_x8, 8};
+    return {cpu_hash_chunks_x4, 4};
+}
+const Simd& simd() {
+    static const Simd s = pick_simd();
+    return s;
+}
+
+}  // namespace
+
+int cpu_lanes() { return simd().lanes; }
+
+CpuHasher::CpuHasher() {}
+
+void CpuHasher::push_chunk_cv(const uint32_t cv[8]) {
+    uint32_t cur[8];
+    memcpy(cur, cv, 32);
+    uint64_t total = ++chunks_;
+    while ((total & 1) == 0) {  // this chunk completes a subtree: merge it with its left half
+        parent_cv(stack_[--sp_], cur, 0, cur);
+        total >>= 1;
+    }
+    memcpy(stack_[sp_++], cur, 32);
+}
+
+void CpuHasher::update(const uint8_t* p, size_t n) {
+    const Simd& s = simd();
+    while (n) {
+        if (buf_len_ == 1024) {  // the buffered chunk is not the last one: push it
+            uint32_t cv[8];
+            chunk_cv(buf_, 1024, chunks_, false, cv);
+            push_chunk_cv(cv);
+            buf_len_ = 0;
+        }
+        if (buf_len_ == 0 && n > 1024) {  // whole chunks straight from the input, keeping >= 1 byte back
+            size_t k = (n - 1) / 1024;
+            const uint8_t* ptrs[16];
+            uint32_t cvs[16][8];
+            while (k) {
+                const int g = (int)std::min<size_t>(k, (size_t)s.lanes);
+                for (int i = 0; i < g; i++) ptrs[i] = p + 1024 * (size_t)i;
+                s.fn(ptrs, g, chunks_, cvs);
+                for (int i = 0; i < g; i++) push_chunk_cv(cvs[i]);
+                p += 1024 * (size_t)g;
+                n -= 1024 * (size_t)g;
+                k -= (size_t)g;
+            }
+            continue;
+        }
+        const size_t take = std::min<size_t>(1024 - buf_len_, n);
+        memcpy(buf_ + buf_len_, p, take);
+        buf_len_ += (uint32_t)take;
+        p += take;
+        n -= take;
+    }
+}
+
+void CpuHasher::finalize(uint8_t out[32]) const {
+    uint32_t cur[8];
+    if (sp_ == 0) {
+        chunk_cv(buf_, buf_len_, chunks_, true, cur);
+    } else {
+        chunk_cv(buf_, buf_len_, chunks_, false, cur);
+        for (int i = sp_ - 1; i >= 1; i--) parent_cv(stack_[i], cur, 0, cur);
+        parent_cv(stack_[0], cur, ROOT, cur);
+    }
+    memcpy(out, cur, 32);  // little-endian words = the hash bytes
+}
+
+void cpu_blake3(const uint8_t* p, size_t n, uint8_t out[32]) {
+    CpuHasher h;
+    h.update(p, n);
+    h.finalize(out);
+}
+
+void hex_lower(const uint8_t* h, int nbytes, char* out) {
+    static const char HEX[] = "0123456789abcdef";
+    for (int i = 0; i < nbytes; i++) {
+        out[2 * i] = HEX[h[i] >> 4];
+        out[2 * i + 1] = HEX[h[i] & 15];
+    }
+    out[2 * nbytes] = 0;
+}
+
+namespace {
+struct Fd {
+    int fd;
+    ~Fd() {
+        if (fd >= 0) close(fd);
+    }
+};
+
+// hashes a MsgSource to its end; SD_FILE_OK or io_status
+int32_t hash_source(MsgSource& src, uint8_t* buf, uint64_t bufsz, uint8_t out[32]) {
+    CpuHasher h;
+    for (;;) {
+        const uint64_t got = src.read(buf, bufsz);
+        if (src.err) return io_status(src.err);
+        h.update(buf, got);
+        if (src.done) break;
+    }
+    h.finalize(out);
+    return SD_FILE_OK;
+}
+}  // namespace
+
+int32_t cpu_cas_id_file(const char* path, uint64_t size, char out_hex17[17]) {
+    uint8_t h[32];
+    if (size > SD_MINIMUM_FILE_SIZE) {  // cas.rs:30-58: the 57 352 B sampled message
+        std::vector<uint8_t> msg(sd_align_up(SD_SAMPLED_MSG_LEN, SD_STAGE_PAD));
+        sd_extent e = plan_extent(size, 0);
+        const int32_t st = stage_one(path, e, msg.data());
+        if (st != SD_FILE_OK) return st;
+        cpu_blake3(msg.data(), e.msg_len, h);
+    } else {  // cas.rs:25-29: le64(size) || fs::read
+        Fd f{open(path, O_RDONLY | O_CLOEXEC)};
+        if (f.fd < 0) return io_status(errno);
+        MsgSource src(f.fd, MsgSource::READ_TO_EOF);
+        src.set_prefix_le64(size);
+        std::vector<uint8_t> buf(128 << 10);
+        const int32_t st = hash_source(src, buf.data(), buf.size(), h);
+        if (st != SD_FILE_OK) return st;
+    }
+    hex_lower(h, 8, out_hex17);  // cas.rs:61 to_hex()[..16]
+    return SD_FILE_OK;
+}
+
+int32_t cpu_checksum_file(const char* path, char out_hex65[65]) {
+    Fd f{open(path, O_RDONLY | O_CLOEXEC)};  // hash.rs:11
+    if (f.fd < 0) return io_status(errno);
+    MsgSource src(f.fd, MsgSource::CHECKSUM_READS);
+    std::unique_ptr<uint8_t[]> buf(new uint8_t[SD_CK_BLOCK]);
+    uint8_t h[32];
+    const int32_t st = hash_source(src, buf.get(), SD_CK_BLOCK, h);
+    if (st != SD_FILE_OK) return st;
+    hex_lower(h, 32, out_hex65);  // hash.rs:21-23
+    return SD_FILE_OK;
+}
+
+namespace {
+// fn(i) for i in [0, n) on up to nthreads threads (the caller's included)
+template <class F>
+void parallel_for(size_t n, int nthreads, F fn) {
+    nthreads = std::max(1, std::min<int>(nthreads, (int)std::min<size_t>(n, 256)));
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) fn(i);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; t++) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+}
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" {
+
+int sd_cpu_simd_lanes(void) { return cpu_lanes(); }
+
+int sd_cpu_cas_ids(const uint8_t* staged, uint64_t staged_bytes, const sd_extent* extents, size_t n, char* out_hex17,
+                   int32_t* status, int nthreads) {
+    SD_GUARD_BEGIN
+    if (n && (!staged || !extents || !out_hex17)) throw sd_failure(SD_ERR_INVALID, "null argument");
+    for (size_t i = 0; i < n; i++) {
+        validate_extent(extents[i], i);
+        if (extents[i].msg_offset + extents[i].msg_len > staged_bytes)
+            throw sd_failure(SD_ERR_INVALID, "extent beyond staged_bytes");
+    }
+    parallel_for(n, nthreads, [&](size_t i) {
+        if (status && status[i] != SD_FILE_OK) return;
+        uint8_t h[32];
+        cpu_blake3(staged + extents[i].msg_offset, extents[i].msg_len, h);
+        hex_lower(h, 8, out_hex17 + 17 * i);
+    });
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cpu_cas_ids_files(const char* const* paths, const uint64_t* sizes, size_t n, char* out_hex17, int32_t* status,
+                         int nthreads) {
+    SD_GUARD_BEGIN
+    if (n && (!paths || !sizes || !out_hex17 || !status)) throw sd_failure(SD_ERR_INVALID, "null argument");
+    parallel_for(n, nthreads, [&](size_t i) { status[i] = cpu_cas_id_file(paths[i], sizes[i], out_hex17 + 17 * i); });
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cpu_checksums(const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n, uint8_t* out_hash32,
+                     int nthreads) {
+    SD_GUARD_BEGIN
+    if (n && (!data || !offsets || !lens || !out_hash32)) throw sd_failure(SD_ERR_INVALID, "null argument");
+    parallel_for(n, nthreads, [&](size_t i) { cpu_blake3(data + offsets[i], lens[i], out_hash32 + 32 * i); });
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cpu_file_checksums(const char* const* paths, size_t n, char* out_hex65, int32_t* status, int nthreads) {
+    SD_GUARD_BEGIN
+    if (n && (!paths || !out_hex65 || !status)) throw sd_failure(SD_ERR_INVALID, "null argument");
+    parallel_for(n, nthreads, [&](size_t i) { status[i] = cpu_checksum_file(paths[i], out_hex65 + 65 * i); });
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cpu_cas_id_path(const char* path, uint64_t size, char* out_hex17, int32_t* status) {
+    SD_GUARD_BEGIN
+    if (!path || !out_hex17 || !status) throw sd_failure(SD_ERR_INVALID, "null argument");
+    *status = cpu_cas_id_file(path, size, out_hex17);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cpu_file_checksum_path(const char* path, char* out_hex65, int32_t* status) {
+    SD_GUARD_BEGIN
+    if (!path || !out_hex65 || !status) throw sd_failure(SD_ERR_INVALID, "null argument");
+    *status = cpu_checksum_file(path, out_hex65);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+}  // extern "C"

@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <functional>
@@ -27,14 +28,15 @@
 #include <thread>
 #include <vector>
 
+#include "sd_host.h"
 #include "sd_internal.h"
 #include "stage_pool.h"
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-void set_err(const char* fmt, ...) {
+void sd_set_err(const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -43,10 +45,7 @@ void set_err(const char* fmt, ...) {
     g_err = buf;
 }
 
-struct sd_failure : std::runtime_error {
-    int rc;
-    sd_failure(int r, const std::string& m) : std::runtime_error(m), rc(r) {}
-};
+namespace {
 
 #define HIP_CHECK(expr)                                                                              \
     do {                                                                                             \
@@ -55,26 +54,6 @@ struct sd_failure : std::runtime_error {
             throw sd_failure(e_ == hipErrorOutOfMemory ? SD_ERR_NOMEM : SD_ERR_DEVICE,              \
                              std::string(#expr) + ": " + hipGetErrorString(e_));                    \
     } while (0)
-
-#define SD_GUARD_BEGIN try {
-#define SD_GUARD_END                                   \
-    }                                                  \
-    catch (const sd_failure& f) {                      \
-        set_err("%s", f.what());                       \
-        return f.rc;                                   \
-    }                                                  \
-    catch (const std::bad_alloc&) {                    \
-        set_err("host allocation failed");             \
-        return SD_ERR_NOMEM;                           \
-    }                                                  \
-    catch (const std::exception& ex) {                 \
-        set_err("internal error: %s", ex.what());      \
-        return SD_ERR_INTERNAL;                        \
-    }                                                  \
-    catch (...) {                                      \
-        set_err("internal error");                     \
-        return SD_ERR_INTERNAL;                        \
-    }
 
 inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
@@ -97,12 +76,28 @@ struct DevBuf {
         HIP_CHECK(hipMalloc(&p, n));
         bytes = n;
     }
+    // grow-only (never frees a buffer that is large enough: hipFree synchronises the device)
     void ensure(size_t n) {
         if (n > bytes) alloc(n);
     }
+    // grow keeping the contents (the caller has synchronised every stream writing it)
+    void grow_preserve(size_t n) {
+        if (n <= bytes) return;
+        void* q = nullptr;
+        HIP_CHECK(hipMalloc(&q, n));
+        if (p) {
+            const hipError_t e = hipMemcpy(q, p, bytes, hipMemcpyDeviceToDevice);
+            if (e != hipSuccess) {
+                (void)hipFree(q);
+                HIP_CHECK(e);
+            }
+            (void)hipFree(p);
+        }
+        p = q;
+        bytes = n;
+    }
     template <class T>
     T* as() const { return reinterpret_cast<T*>(p); }
-    // grow-only (never frees a buffer that is large enough: hipFree synchronises the device)
     template <class T>
     void upload(const std::vector<T>& v, hipStream_t s = nullptr) {
         ensure(v.size() * sizeof(T));
@@ -127,6 +122,7 @@ struct PinnedBuf {
         HIP_CHECK(hipHostMalloc(&p, n, hipHostMallocDefault));
         bytes = n;
     }
+    uint8_t* u8() const { return reinterpret_cast<uint8_t*>(p); }
 };
 
 // per-call working set of the host drop-in entry points
@@ -145,11 +141,14 @@ struct sd_cas_ctx {
     std::mutex coal_mu;
     sd_coalescer* coal = nullptr;  // latency path, created on the first single-file call
     std::mutex pool_mu;
-    std::unique_ptr<StagePool> pool;  // file stager threads (sd_cas_ids_files)
-    StagePool& stage_pool(int nthreads) {
+    // File stager threads (sd_cas_ids_files).  One pool per context, grown to the largest
+    // thread count any call asked for; a caller holds its shared_ptr while it runs, so a
+    // concurrent call that grows the pool never destroys one in use.
+    std::shared_ptr<StagePool> pool;
+    std::shared_ptr<StagePool> stage_pool(int nthreads) {
         std::lock_guard<std::mutex> g(pool_mu);
-        if (!pool || pool->threads() != nthreads) pool = std::make_unique<StagePool>(nthreads);
-        return *pool;
+        if (!pool || pool->threads() < nthreads) pool = std::make_shared<StagePool>(nthreads);
+        return pool;
     }
     sd_coalescer* coalescer() {
         std::lock_guard<std::mutex> g(coal_mu);
@@ -179,536 +178,274 @@ struct sd_cas_ctx {
     static hipStream_t pick(void* s) { return reinterpret_cast<hipStream_t>(s); }  // NULL = null stream
 };
 
-struct sd_cas_batch {
-    size_t n = 0;
-    uint32_t n_sampled = 0, n_whole = 0, n_multi = 0;
-    uint32_t total_chunks = 0;
-    uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0;
-    uint32_t n_groups = 0;  // whole-file groups of the fused kernel
-    uint32_t total_pairs = 0, n_multi2 = 0;  // pair leaf: chunk pairs; files with >= 3 chunks
-    uint32_t n_groups2 = 0;                  // forest groups over the multi-pair files
-    // variant 6 item lists (kernel formats in cas_kernels.hip, k_whole_full / _tail / _merge8)
-    uint32_t n_full = 0, n_tail = 0, n_merge_a = 0, n_merge_b = 0, n_cv2 = 0;
-    DevBuf ext, sidx, order, prefix, hint, cvbuf, groups, prefix2, hint2, groups2;
-    DevBuf full_items, tail_items, merge_a, merge_b, cv2;
-    std::vector<uint4> h_full, h_tail, h_merge_a, h_merge_b;
-    // variant 2: the whole-file tree kernel runs on a side stream beside the sampled kernel
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-    ~sd_cas_batch() {
-        if (side) (void)hipStreamDestroy(side);
-        if (fork) (void)hipEventDestroy(fork);
-        if (join) (void)hipEventDestroy(join);
+namespace {
+
+// Two slots held for one call; released (after their streams drain) on scope exit.
+struct SlotPair {
+    sd_cas_ctx* c;
+    std::unique_ptr<Slot> s[2];
+    explicit SlotPair(sd_cas_ctx* ctx) : c(ctx) {
+        s[0] = c->acquire();
+        s[1] = c->acquire();
     }
-    std::vector<sd_extent> h_ext;  // host copies backing async uploads
-    std::vector<uint32_t> h_sidx, h_order, h_prefix, h_hint, h_prefix2, h_hint2;
-    std::vector<uint2> h_groups, h_groups2;
+    ~SlotPair() {
+        for (auto& x : s)
+            if (x) {
+                (void)hipStreamSynchronize(x->stream);
+                c->release(std::move(x));
+            }
+    }
+    Slot& operator[](int k) { return *s[k]; }
+    void sync_all() {
+        HIP_CHECK(hipStreamSynchronize(s[0]->stream));
+        HIP_CHECK(hipStreamSynchronize(s[1]->stream));
+    }
 };
 
-struct ck_pass {
-    DevBuf wgs;
-    std::vector<ck_reduce_wg> h_wgs;  // host copy backing the async upload
-    uint32_t n_wg = 0;
-    int src = 0, dst = 1;  // which CV level buffer
-};
+}  // namespace
 
 struct sd_checksum_batch {
     size_t n = 0;
-    uint64_t total_bytes = 0, compressions = 0, blocks = 0;
-    std::vector<ck_file> files_h;
-    std::vector<uint2> wg_map_h;
+    CkPlan plan;
     DevBuf files, wg_map;
     DevBuf lvl[2];
-    std::vector<std::unique_ptr<ck_pass>> passes;  // capacity reused across replans
-    size_t n_passes = 0;
+    std::vector<std::unique_ptr<DevBuf>> pass_wgs;  // capacity reused across replans
+};
+
+struct sd_cas_batch {
+    size_t n = 0;
+    uint32_t n_sampled = 0, n_whole = 0, n_long = 0;
+    uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0, whole_chunks = 0;
+    WholePlan whole;  // work lists (kernel formats in cas_kernels.hip, k_whole_items / _merge8)
+    DevBuf ext, sidx, full_items, tail_items, merge_a, merge_b, cvbuf, cv2;
+    // whole-file messages longer than SD_WHOLE_ITEMS_MAX: a checksum sub-batch over their
+    // byte ranges, its hashes scattered to out[long_idx[i]]
+    sd_checksum_batch lng;
+    DevBuf long_idx, long_out;
+    // host copies backing async uploads
+    std::vector<sd_extent> h_ext;
+    std::vector<uint32_t> h_sidx, h_long_idx;
 };
 
 namespace {
 
-// ----------------------------------------------------------------- cas batch planning
-uint32_t msg_chunks(uint32_t msg_len) { return msg_len == 0 ? 1u : (msg_len + 1023u) / 1024u; }
-
-uint64_t msg_compressions(uint64_t msg_len) {  // blocks in all chunks + parents
-    const uint64_t C = msg_len == 0 ? 1 : (msg_len + 1023) / 1024;
-    uint64_t blocks = 0;
-    for (uint64_t c = 0; c < C; c++) {
-        const uint64_t len = std::min<uint64_t>(1024, msg_len - c * 1024);
-        blocks += len == 0 ? 1 : (len + 63) / 64;
-    }
-    return blocks + (C - 1);
-}
-
-uint64_t file_compressions(uint64_t len) {  // same, closed form for large inputs
-    const uint64_t C = len == 0 ? 1 : (len + 1023) / 1024;
-    const uint64_t last = len - (C - 1) * 1024;
-    return (C - 1) * 16 + (last == 0 ? 1 : (last + 63) / 64) + (C - 1);
-}
-
-void validate_extent(const sd_extent& e, size_t i) {
-    const bool whole = e.size <= SD_MINIMUM_FILE_SIZE;
-    const uint64_t want = whole ? 8 + e.size : SD_SAMPLED_MSG_LEN;
-    if (e.kind != (whole ? SD_KIND_WHOLE : SD_KIND_SAMPLED) || e.msg_len != want)
-        throw sd_failure(SD_ERR_INVALID, "extent " + std::to_string(i) + ": kind/msg_len do not match size");
-    if (e.msg_offset % 16)
-        throw sd_failure(SD_ERR_INVALID, "extent " + std::to_string(i) + ": msg_offset not 16-byte aligned");
-}
-
-// compressions of aligned chunk pair (c0, c0 + 1) holding glen (1..2048) message bytes
-uint32_t pair_compressions(uint32_t glen) {
-    const uint32_t l0 = std::min<uint32_t>(glen, 1024), l1 = glen - l0;
-    return (l0 + 63) / 64 + (l1 ? (l1 + 63) / 64 + 1 : 0);
-}
-
-// Variant-6 work lists over the length-sorted whole files (b->h_order, pair prefix
-// b->h_prefix2): full-pair items in (file, pair) order; tail items counting-sorted by
-// compressions, descending; merge8 items -- pass A over aligned groups of <= 8 pair nodes
-// (the whole tree when a file has <= 8 nodes), pass B over the pass-A nodes of files with
-// more than 8.
-void plan_whole_items(sd_cas_batch* b, const sd_extent* ext) {
-    auto& full = b->h_full;
-    auto& tail = b->h_tail;
-    auto& ma = b->h_merge_a;
-    auto& mb = b->h_merge_b;
-    full.clear();
-    tail.clear();
-    ma.clear();
-    mb.clear();
-    std::vector<uint32_t> tail_cost;
-    const auto& p2 = b->h_prefix2;
-    // items are emitted in file (= staged address) order, so the full-pair waves sweep the
-    // staged buffer front to back as the sampled kernel does, instead of hopping between
-    // the length-sorted files' scattered messages; the cv slot still follows the sorted order
-    std::vector<uint32_t> rank(b->n, 0);
-    for (uint32_t k = 0; k < b->n_whole; k++) rank[b->h_order[k]] = k;
-    for (uint32_t file = 0; file < b->n; file++) {
-        const sd_extent& e = ext[file];
-        if (e.kind != SD_KIND_WHOLE) continue;
-        const uint32_t k = rank[file];
-        const uint32_t C = msg_chunks(e.msg_len), P = (C + 1) / 2;
-        const bool multi = C >= 3;
-        for (uint32_t j = 0; j < P; j++) {
-            const uint64_t off = e.msg_offset + 2048ull * j;
-            const uint32_t glen = std::min<uint32_t>(2048, e.msg_len - 2048 * j);
-            const uint32_t lo = (uint32_t)off, hi = (uint32_t)(off >> 32);
-            if (multi && glen == 2048) {
-                full.push_back(make_uint4(lo, hi, p2[k] + j, 2 * j));
-            } else {
-                const uint32_t w = glen | ((2 * j) << 12) | (multi ? 0u : 0x80000000u);
-                tail.push_back(make_uint4(lo, hi, multi ? p2[k] + j : file, w));
-                tail_cost.push_back(pair_compressions(glen));
-            }
-        }
-    }
-    // stable counting sort of the tail items by cost, descending (cost 1..33)
-    {
-        std::vector<uint32_t> start(35, 0);
-        for (uint32_t c : tail_cost) start[34 - c]++;
-        uint32_t acc = 0;
-        for (auto& s : start) {
-            const uint32_t t = s;
-            s = acc;
-            acc += t;
-        }
-        std::vector<uint4> sorted(tail.size());
-        for (size_t i = 0; i < tail.size(); i++) sorted[start[34 - tail_cost[i]]++] = tail[i];
-        tail.swap(sorted);
-    }
-    uint32_t cv2 = 0;
-    for (uint32_t k = 0; k < b->n_multi2; k++) {
-        const uint32_t P = p2[k + 1] - p2[k], file = b->h_order[k];
-        if (P <= 8) {
-            ma.push_back(make_uint4(p2[k], P | 0x80000000u, file, 0));
-            continue;
-        }
-        const uint32_t G = (P + 7) / 8;
-        for (uint32_t a = 0; a < G; a++) ma.push_back(make_uint4(p2[k] + 8 * a, std::min<uint32_t>(8, P - 8 * a), cv2 + a, 0));
-        if (G > 8) throw sd_failure(SD_ERR_INTERNAL, "whole-file message with more than 64 pair nodes");
-        mb.push_back(make_uint4(cv2, G | 0x80000000u, file, 0));
-        cv2 += G;
-    }
-    b->n_full = (uint32_t)full.size();
-    b->n_tail = (uint32_t)tail.size();
-    b->n_merge_a = (uint32_t)ma.size();
-    b->n_merge_b = (uint32_t)mb.size();
-    b->n_cv2 = cv2;
-}
-
-// (Re)plans `b` for these extents, reusing its device buffers.  With a stream, the small
-// metadata uploads are async on it and read from b's host copies, which stay valid until
-// the next rebuild of `b` (the caller syncs the stream before that).
-void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t stream) {
-    if (n >= (1ull << 31)) throw sd_failure(SD_ERR_INVALID, "batch too large");
-    b->n = n;
-    b->n_sampled = b->n_whole = b->n_multi = 0;
-    b->compressions = b->msg_bytes = 0;
-    std::vector<uint32_t>& sidx = b->h_sidx;
-    sidx.clear();
-    std::vector<uint32_t> count(SD_MINIMUM_FILE_SIZE + 9 + 1, 0);
-    uint64_t end = 0;
-    for (size_t i = 0; i < n; i++) {
-        validate_extent(ext[i], i);
-        end = std::max<uint64_t>(end, align_up(ext[i].msg_offset + ext[i].msg_len, SD_STAGE_PAD));
-        b->msg_bytes += ext[i].msg_len;
-        if (ext[i].kind == SD_KIND_SAMPLED) {
-            sidx.push_back((uint32_t)i);
-            b->compressions += 953;  // 56 x 16 + 1 blocks, 56 parents
-        } else {
-            count[ext[i].msg_len]++;
-            b->compressions += msg_compressions(ext[i].msg_len);
-        }
-    }
-    b->staged_bytes = end;
-    b->n_sampled = (uint32_t)sidx.size();
-    b->n_whole = (uint32_t)(n - sidx.size());
-    // counting sort of whole files by msg_len, descending (uniform lanes in both kernels)
-    std::vector<uint32_t> start(count.size() + 1, 0);
-    for (size_t L = count.size(); L-- > 0;) start[L] = start[L + 1] + count[L];
-    std::vector<uint32_t>& order = b->h_order;
-    order.assign(b->n_whole, 0);
-    for (size_t i = 0; i < n; i++)
-        if (ext[i].kind == SD_KIND_WHOLE) order[start[ext[i].msg_len + 1]++] = (uint32_t)i;
-    std::vector<uint32_t>& prefix = b->h_prefix;
-    prefix.assign(b->n_whole + 1, 0);
-    uint64_t total = 0;
-    for (uint32_t k = 0; k < b->n_whole; k++) {
-        prefix[k] = (uint32_t)total;
-        const uint32_t C = msg_chunks(ext[order[k]].msg_len);
-        total += C;
-        if (C >= 2) b->n_multi = k + 1;
-    }
-    if (total >= (1ull << 32)) throw sd_failure(SD_ERR_INVALID, "too many chunks in one batch");
-    prefix[b->n_whole] = (uint32_t)total;
-    b->total_chunks = (uint32_t)total;
-    const uint32_t W = (b->total_chunks + 63) / 64;
-    std::vector<uint32_t>& hint = b->h_hint;
-    hint.assign(W + 1, 0);
-    {
-        uint32_t k = 0;
-        for (uint32_t w = 0; w <= W; w++) {
-            const uint64_t c = std::min<uint64_t>((uint64_t)w * 64, total ? total - 1 : 0);
-            while (k + 1 < b->n_whole && prefix[k + 1] <= c) k++;
-            hint[w] = k;
-        }
-    }
-    // the same in units of aligned chunk pairs (pair leaf kernel)
-    {
-        std::vector<uint32_t>& p2 = b->h_prefix2;
-        p2.assign(b->n_whole + 1, 0);
-        uint32_t tp = 0;
-        b->n_multi2 = 0;
-        for (uint32_t k = 0; k < b->n_whole; k++) {
-            p2[k] = tp;
-            const uint32_t C = msg_chunks(ext[order[k]].msg_len);
-            tp += (C + 1) / 2;
-            if (C >= 3) b->n_multi2 = k + 1;
-        }
-        p2[b->n_whole] = tp;
-        b->total_pairs = tp;
-        // forest groups: consecutive multi-pair files whose pair nodes fit 448 lanes
-        b->h_groups2.clear();
-        uint32_t first = 0, lanes = 0;
-        for (uint32_t k = 0; k < b->n_multi2; k++) {
-            const uint32_t L = p2[k + 1] - p2[k];
-            if (lanes + L > 448) {
-                b->h_groups2.push_back(make_uint2(first, k - first));
-                first = k;
-                lanes = 0;
-            }
-            lanes += L;
-        }
-        if (b->n_multi2) b->h_groups2.push_back(make_uint2(first, b->n_multi2 - first));
-        b->n_groups2 = (uint32_t)b->h_groups2.size();
-        const uint32_t W2 = (tp + 63) / 64;
-        std::vector<uint32_t>& h2 = b->h_hint2;
-        h2.assign(W2 + 1, 0);
-        uint32_t k = 0;
-        for (uint32_t w = 0; w <= W2; w++) {
-            const uint64_t c = std::min<uint64_t>((uint64_t)w * 64, tp ? tp - 1 : 0);
-            while (k + 1 < b->n_whole && p2[k + 1] <= c) k++;
-            h2[w] = k;
-        }
-    }
-    plan_whole_items(b, ext);
-    // whole-file groups for the fused kernel: consecutive (length-sorted) files whose
-    // chunk pairs fit one 448-lane workgroup
-    b->h_groups.clear();
-    {
-        uint32_t first = 0, lanes = 0;
-        for (uint32_t k = 0; k < b->n_whole; k++) {
-            const uint32_t L = (msg_chunks(ext[order[k]].msg_len) + 1) / 2;
-            if (lanes + L > 448) {
-                b->h_groups.push_back(make_uint2(first, k - first));
-                first = k;
-                lanes = 0;
-            }
-            lanes += L;
-        }
-        if (b->n_whole) b->h_groups.push_back(make_uint2(first, b->n_whole - first));
-    }
-    b->n_groups = (uint32_t)b->h_groups.size();
-    b->groups.upload(b->h_groups, stream);
-    b->h_ext.assign(ext, ext + n);
-    b->ext.upload(b->h_ext, stream);
-    b->sidx.upload(sidx, stream);
-    b->order.upload(order, stream);
-    b->prefix.upload(prefix, stream);
-    b->hint.upload(hint, stream);
-    b->prefix2.upload(b->h_prefix2, stream);
-    b->hint2.upload(b->h_hint2, stream);
-    b->groups2.upload(b->h_groups2, stream);
-    b->full_items.upload(b->h_full, stream);
-    b->tail_items.upload(b->h_tail, stream);
-    b->merge_a.upload(b->h_merge_a, stream);
-    b->merge_b.upload(b->h_merge_b, stream);
-    b->cv2.ensure((size_t)b->n_cv2 * 32);
-    b->cvbuf.ensure((size_t)b->total_chunks * 32);
-}
-
-sd_cas_batch* build_cas_batch(const sd_extent* ext, size_t n) {
-    auto b = std::make_unique<sd_cas_batch>();
-    plan_cas_batch(b.get(), ext, n, nullptr);
-    return b.release();
-}
-
-void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_hash32, hipStream_t s,
-                   int parts = SD_PART_SAMPLED | SD_PART_WHOLE) {
-    uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
-    const int wv = tuning_get(SD_TUNE_WHOLE_VARIANT);
-    if (wv == 0 || wv == 4) {  // one fused launch (4: prefetching pair leaves)
-        HIP_CHECK(sdk::launch_cas_mixed(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(),
-                                        (parts & SD_PART_SAMPLED) ? b->n_sampled : 0, b->order.as<uint32_t>(),
-                                        b->groups.as<uint2>(), (parts & SD_PART_WHOLE) ? b->n_groups : 0, out, s,
-                                        wv == 4));
-        return;
-    }
-    if (wv == 6 || wv == 7 || wv == 8) {  // sampled kernel; full-pair / cost-sorted tail-pair items (7, 8: one
-                                          // launch; 8: line-pair loads); two merge8 passes
-        if (parts & SD_PART_SAMPLED)
-            HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled,
-                                              out, s));
-        if (parts & SD_PART_WHOLE)
-            HIP_CHECK(sdk::launch_whole_items(d_staged, b->full_items.as<uint4>(), b->n_full, b->tail_items.as<uint4>(),
-                                              b->n_tail, b->merge_a.as<uint4>(), b->n_merge_a, b->merge_b.as<uint4>(),
-                                              b->n_merge_b, b->cvbuf.as<uint32_t>(), b->cv2.as<uint32_t>(), out, s,
-                                              wv >= 7, wv == 8 ? 2 : 1));
-        return;
-    }
-    if (wv == 3 || wv == 5) {  // sampled kernel; prefetching pair leaf + tree (3) / LDS forest (5) over pair nodes
-        if (parts & SD_PART_SAMPLED)
-            HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled,
-                                              out, s));
-        if (parts & SD_PART_WHOLE) {
-            HIP_CHECK(sdk::launch_whole_pair_leaf(d_staged, b->ext.as<sd_extent>(), b->order.as<uint32_t>(),
-                                                  b->prefix2.as<uint32_t>(), b->hint2.as<uint32_t>(), b->n_whole,
-                                                  b->total_pairs, b->cvbuf.as<uint32_t>(), out, s));
-            if (wv == 3)
-                HIP_CHECK(sdk::launch_whole_tree(b->order.as<uint32_t>(), b->prefix2.as<uint32_t>(), b->n_multi2,
-                                                 b->cvbuf.as<uint32_t>(), out, s));
-            else
-                HIP_CHECK(sdk::launch_whole_forest(b->order.as<uint32_t>(), b->prefix2.as<uint32_t>(),
-                                                   b->groups2.as<uint2>(), b->n_groups2, b->cvbuf.as<uint32_t>(), out,
-                                                   s));
-        }
-        return;
-    }
-    if (tuning_get(SD_TUNE_WHOLE_VARIANT) == 2 && (parts & SD_PART_WHOLE) && (parts & SD_PART_SAMPLED) && b->n_multi) {
-        // whole-file leaf, then the sampled kernel on `s` beside the whole-file tree on a
-        // side stream (the tree's long single-lane chains leave most issue slots idle)
-        auto* mb = const_cast<sd_cas_batch*>(b);
-        if (!mb->side) {
-            HIP_CHECK(hipStreamCreateWithFlags(&mb->side, hipStreamNonBlocking));
-            HIP_CHECK(hipEventCreateWithFlags(&mb->fork, hipEventDisableTiming));
-            HIP_CHECK(hipEventCreateWithFlags(&mb->join, hipEventDisableTiming));
-        }
-        HIP_CHECK(sdk::launch_whole_leaf(d_staged, b->ext.as<sd_extent>(), b->order.as<uint32_t>(),
-                                         b->prefix.as<uint32_t>(), b->hint.as<uint32_t>(), b->n_whole,
-                                         b->total_chunks, b->cvbuf.as<uint32_t>(), out, s));
-        HIP_CHECK(hipEventRecord(mb->fork, s));
-        HIP_CHECK(hipStreamWaitEvent(mb->side, mb->fork, 0));
-        HIP_CHECK(sdk::launch_whole_tree(b->order.as<uint32_t>(), b->prefix.as<uint32_t>(), b->n_multi,
-                                         b->cvbuf.as<uint32_t>(), out, mb->side));
-        HIP_CHECK(hipEventRecord(mb->join, mb->side));
-        HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled, out,
-                                          s));
-        HIP_CHECK(hipStreamWaitEvent(s, mb->join, 0));
-        return;
-    }
-    // variant 1 (default): separate sampled kernel, whole-file leaf kernel, whole-file tree
-    // kernel -- 1.5% faster than the fused launch in a same-process A/B
-    if (parts & SD_PART_SAMPLED)
-        HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled, out,
-                                          s));
-    if (parts & SD_PART_WHOLE)
-        HIP_CHECK(sdk::launch_whole(d_staged, b->ext.as<sd_extent>(), b->order.as<uint32_t>(), b->prefix.as<uint32_t>(),
-                                    b->hint.as<uint32_t>(), b->n_whole, b->total_chunks, b->n_multi,
-                                    b->cvbuf.as<uint32_t>(), out, s));
-}
-
-// -------------------------------------------------------------- checksum planning
-constexpr uint64_t CK_BLOCK_BYTES = 1024ull * 1024ull;  // 1024 chunks per leaf workgroup
-
-// (Re)plans `b` for these byte ranges reusing its device buffers (grow-only; see
-// plan_cas_batch for the stream / host-copy lifetime rule).
+// ----------------------------------------------------------- checksum batches (device)
+// (Re)plans `b` for these byte ranges reusing its device buffers (grow-only).  With a
+// stream, the small uploads are async on it and read from b's host copies, which stay
+// valid until the next rebuild of `b` (the caller syncs the stream before that).
 void plan_checksum_batch(sd_checksum_batch* b, const uint64_t* offsets, const uint64_t* lens, size_t n,
                          hipStream_t stream) {
-    if (n >= (1ull << 31)) throw sd_failure(SD_ERR_INVALID, "batch too large");
+    plan_checksum(b->plan, offsets, lens, n);
     b->n = n;
-    b->total_bytes = b->compressions = b->blocks = 0;
-    b->files_h.resize(n);
-    b->wg_map_h.clear();
-    std::vector<uint64_t> level_n(n);  // current level size per file
-    uint64_t cv0 = 0;
-    for (size_t i = 0; i < n; i++) {
-        if (offsets[i] % 16) throw sd_failure(SD_ERR_INVALID, "checksum range " + std::to_string(i) + " not 16-byte aligned");
-        const uint64_t nb = lens[i] == 0 ? 1 : (lens[i] + CK_BLOCK_BYTES - 1) / CK_BLOCK_BYTES;
-        if (nb >= (1ull << 32)) throw sd_failure(SD_ERR_INVALID, "file too large");
-        b->files_h[i] = ck_file{offsets[i], lens[i], nb > 1 ? cv0 : 0};
-        for (uint64_t k = 0; k < nb; k++) b->wg_map_h.push_back(make_uint2((uint32_t)i, (uint32_t)k));
-        if (nb > 1) cv0 += nb;
-        level_n[i] = nb;
-        b->total_bytes += lens[i];
-        b->compressions += file_compressions(lens[i]);
-        b->blocks += nb;
-    }
-    b->files.upload(b->files_h, stream);
-    b->wg_map.upload(b->wg_map_h, stream);
-    // reduce passes: groups of 256 CVs per workgroup until every file has its root
-    std::vector<uint64_t> base(n, 0);
-    for (size_t i = 0; i < n; i++) base[i] = b->files_h[i].cv_base;
-    size_t lvl_cap[2] = {cv0, 0};
-    int src = 0;
-    b->n_passes = 0;
-    for (;;) {
-        if (b->n_passes == b->passes.size()) b->passes.push_back(std::make_unique<ck_pass>());
-        ck_pass& p = *b->passes[b->n_passes];
-        p.h_wgs.clear();
-        uint64_t dst_total = 0;
-        std::vector<uint64_t> nbase(n, 0);
-        for (size_t i = 0; i < n; i++) {
-            const uint64_t cnt = level_n[i];
-            if (cnt <= 1) continue;
-            const uint64_t groups = (cnt + 255) / 256;
-            nbase[i] = dst_total;
-            for (uint64_t g = 0; g < groups; g++) {
-                ck_reduce_wg w{};
-                w.src_base = base[i] + g * 256;
-                w.dst_index = dst_total + g;
-                w.count = (uint32_t)std::min<uint64_t>(256, cnt - g * 256);
-                w.file = (uint32_t)i;
-                w.is_root = groups == 1;
-                p.h_wgs.push_back(w);
-            }
-            dst_total += groups == 1 ? 0 : groups;
-            level_n[i] = groups == 1 ? 1 : groups;
-        }
-        if (p.h_wgs.empty()) break;
-        p.wgs.upload(p.h_wgs, stream);
-        p.n_wg = (uint32_t)p.h_wgs.size();
-        p.src = src;
-        p.dst = 1 - src;
-        lvl_cap[1 - src] = std::max<size_t>(lvl_cap[1 - src], dst_total);
-        b->n_passes++;
-        base = nbase;
-        src = 1 - src;
-    }
-    b->lvl[0].ensure(lvl_cap[0] * 32);
-    b->lvl[1].ensure(lvl_cap[1] * 32);
+    b->files.upload(b->plan.files, stream);
+    b->wg_map.upload(b->plan.wg_map, stream);
+    while (b->pass_wgs.size() < b->plan.passes.size()) b->pass_wgs.push_back(std::make_unique<DevBuf>());
+    for (size_t k = 0; k < b->plan.passes.size(); k++) b->pass_wgs[k]->upload(b->plan.passes[k], stream);
+    b->lvl[0].ensure(b->plan.lvl_cap[0] * 32);
+    b->lvl[1].ensure(b->plan.lvl_cap[1] * 32);
 }
-
-sd_checksum_batch* build_checksum_batch(const uint64_t* offsets, const uint64_t* lens, size_t n) {
-    auto b = std::make_unique<sd_checksum_batch>();
-    plan_checksum_batch(b.get(), offsets, lens, n, nullptr);
-    return b.release();
-}
-
-void run_checksum_leaf(const sd_checksum_batch* b, const uint8_t* d_data, uint64_t shift, uint32_t wg0, uint32_t wg1,
-                       uint32_t* out, hipStream_t s);
 
 void run_checksum_reduce(const sd_checksum_batch* b, uint32_t* out, hipStream_t s) {
-    for (size_t k = 0; k < b->n_passes; k++) {
-        const ck_pass& p = *b->passes[k];
-        HIP_CHECK(sdk::launch_ck_reduce(b->lvl[p.src].as<uint32_t>(), b->lvl[p.dst].as<uint32_t>(),
-                                        p.wgs.as<ck_reduce_wg>(), p.n_wg, out, s));
+    for (size_t k = 0; k < b->plan.passes.size(); k++) {
+        const int src = (int)(k & 1);  // level 0 -> 1 -> 0 ...
+        HIP_CHECK(sdk::launch_ck_reduce(b->lvl[src].as<uint32_t>(), b->lvl[1 - src].as<uint32_t>(),
+                                        b->pass_wgs[k]->as<ck_reduce_wg>(), (uint32_t)b->plan.passes[k].size(), out,
+                                        s));
     }
 }
 
 void run_checksum_batch(const sd_checksum_batch* b, const uint8_t* d_data, uint8_t* d_hash32, hipStream_t s) {
     uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
-    run_checksum_leaf(b, d_data, 0, 0, (uint32_t)b->wg_map_h.size(), out, s);
+    HIP_CHECK(sdk::launch_ck_leaf(d_data, 0, 0, b->files.as<ck_file>(), b->wg_map.as<uint2>(),
+                                  (uint32_t)b->plan.wg_map.size(), b->lvl[0].as<uint32_t>(), out, s));
     run_checksum_reduce(b, out, s);
 }
 
-const char HEX[] = "0123456789abcdef";
-void to_hex(const uint8_t* h, int nbytes, char* out) {
-    for (int i = 0; i < nbytes; i++) {
-        out[2 * i] = HEX[h[i] >> 4];
-        out[2 * i + 1] = HEX[h[i] & 15];
-    }
-    out[2 * nbytes] = 0;
-}
-
-int32_t io_status(int err) { return (int32_t)(SD_FILE_IO_ERROR | ((uint32_t)(err & 0xFFFF) << 16)); }
-
-// read exactly n bytes at off; returns 0, or an sd_file_status code
-int32_t pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
-    while (n) {
-        const ssize_t r = pread(fd, dst, n, (off_t)off);
-        if (r < 0) {
-            if (errno == EINTR) continue;
-            return io_status(errno);
+// ---------------------------------------------------------------- cas batches (device)
+// (Re)plans `b` for these extents, reusing its device buffers (see plan_checksum_batch for
+// the stream / host-copy lifetime rule).
+void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t stream) {
+    if (n >= (1ull << 31)) throw sd_failure(SD_ERR_INVALID, "batch too large");
+    b->n = n;
+    b->n_whole = 0;
+    b->compressions = b->msg_bytes = b->whole_chunks = 0;
+    b->h_sidx.clear();
+    b->h_long_idx.clear();
+    std::vector<uint64_t> loff, llen;
+    uint64_t end = 0;
+    for (size_t i = 0; i < n; i++) {
+        const sd_extent& e = ext[i];
+        validate_extent(e, i);
+        end = std::max<uint64_t>(end, align_up(e.msg_offset + e.msg_len, SD_STAGE_PAD));
+        b->msg_bytes += e.msg_len;
+        if (e.kind == SD_KIND_SAMPLED) {
+            b->h_sidx.push_back((uint32_t)i);
+            b->compressions += 953;  // 56 x 16 + 1 blocks, 56 parents
+        } else if (e.msg_len <= SD_WHOLE_ITEMS_MAX) {
+            b->n_whole++;
+            b->whole_chunks += msg_chunks(e.msg_len);
+            b->compressions += msg_compressions(e.msg_len);
+        } else {
+            b->h_long_idx.push_back((uint32_t)i);
+            loff.push_back(e.msg_offset);
+            llen.push_back(e.msg_len);
         }
-        if (r == 0) return SD_FILE_SHORT_READ;
-        dst += r;
-        n -= (uint64_t)r;
-        off += (uint64_t)r;
     }
-    return SD_FILE_OK;
+    b->staged_bytes = end;
+    b->n_sampled = (uint32_t)b->h_sidx.size();
+    b->n_long = (uint32_t)b->h_long_idx.size();
+    plan_whole_items(b->whole, ext, n);
+    b->h_ext.assign(ext, ext + n);
+    b->ext.upload(b->h_ext, stream);
+    b->sidx.upload(b->h_sidx, stream);
+    b->full_items.upload(b->whole.full, stream);
+    b->tail_items.upload(b->whole.tail, stream);
+    b->merge_a.upload(b->whole.merge_a, stream);
+    b->merge_b.upload(b->whole.merge_b, stream);
+    b->cvbuf.ensure((size_t)b->whole.n_cv * 32);
+    b->cv2.ensure((size_t)b->whole.n_cv2 * 32);
+    if (b->n_long) {
+        plan_checksum_batch(&b->lng, loff.data(), llen.data(), b->n_long, stream);
+        b->compressions += b->lng.plan.compressions;
+        b->long_idx.upload(b->h_long_idx, stream);
+        b->long_out.ensure((size_t)b->n_long * 32);
+    }
 }
 
-// Reads one file into its extent exactly as generate_cas_id does (cas.rs:25-58) and
-// zero-pads the message to SD_STAGE_PAD.  Returns an sd_file_status.
-int32_t stage_one(const char* path, const sd_extent& e, uint8_t* staged) {
-    uint8_t* dst = staged + e.msg_offset;
-    const uint64_t size = e.size;
-    for (int i = 0; i < 8; i++) dst[i] = (uint8_t)(size >> (8 * i));  // cas.rs:25 le64
-    const uint64_t padded = align_up(e.msg_len, SD_STAGE_PAD);
-    memset(dst + e.msg_len, 0, padded - e.msg_len);
+void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_hash32, hipStream_t s,
+                   int parts = SD_PART_SAMPLED | SD_PART_WHOLE) {
+    uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
+    if (parts & SD_PART_SAMPLED)
+        HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled, out,
+                                          s));
+    if (parts & SD_PART_WHOLE) {
+        const WholePlan& w = b->whole;
+        HIP_CHECK(sdk::launch_whole_items(d_staged, b->full_items.as<uint4>(), (uint32_t)w.full.size(),
+                                          b->tail_items.as<uint4>(), (uint32_t)w.tail.size(), b->merge_a.as<uint4>(),
+                                          (uint32_t)w.merge_a.size(), b->merge_b.as<uint4>(),
+                                          (uint32_t)w.merge_b.size(), b->cvbuf.as<uint32_t>(),
+                                          b->cv2.as<uint32_t>(), out, s));
+        if (b->n_long) {
+            run_checksum_batch(&b->lng, d_staged, b->long_out.as<uint8_t>(), s);
+            HIP_CHECK(sdk::launch_scatter_hash(b->long_out.as<uint32_t>(), b->long_idx.as<uint32_t>(), b->n_long, out,
+                                               s));
+        }
+    }
+}
+
+// ------------------------------------------------------- streaming (unknown length)
+// Hashes one message read front to back from a MsgSource through 256 MiB windows on two
+// alternating slots.  The message's length is only known when the source ends, which is
+// all the 1 MiB-block tree needs: a full window (more than 1 MiB) holds 256 complete,
+// non-final blocks whose subtree CVs do not depend on the total, so they are hashed as the
+// windows arrive (a provisional one-message table of unbounded length); the final window
+// then runs with the message's real length, and the reduce passes merge all block CVs.
+struct Streamer {
+    static constexpr uint64_t W = 256ull << 20;  // a multiple of the 1 MiB leaf block
+    static constexpr uint32_t BPW = (uint32_t)(W / SD_CK_BLOCK);
+    sd_checksum_batch fin;        // the final plan: one message of the final length
+    DevBuf prov_files, prov_map;  // full windows: {0, 2^62, 0} and (0, b) for b < BPW
+    bool prov_ready = false;
+
+    static void prepare(SlotPair& sl) {
+        for (int k = 0; k < 2; k++) {
+            sl[k].window.ensure(W + 128);
+            sl[k].staged.ensure(W + 128);
+            sl[k].hashes.ensure(32);
+            sl[k].host_hashes.ensure(32);
+        }
+    }
+
+    // Returns SD_FILE_OK with the 32-byte hash in out32, or the source's I/O status.
+    int32_t hash(SlotPair& sl, int& cur, MsgSource& src, uint64_t size_hint, uint8_t out32[32]) {
+        prepare(sl);
+        if (!prov_ready) {
+            std::vector<ck_file> f{ck_file{0, 1ull << 62, 0}};
+            std::vector<sd_u32x2> m(BPW);
+            for (uint32_t b = 0; b < BPW; b++) m[b] = sd_u32x2{0, b};
+            prov_files.upload(f);
+            prov_map.upload(m);
+            prov_ready = true;
+        }
+        sl.sync_all();
+        fin.lvl[0].grow_preserve((size_t)std::max<uint64_t>(size_hint / SD_CK_BLOCK + 2, 2 * BPW) * 32);
+        uint64_t pos = 0;
+        for (;;) {
+            const int k = cur;
+            cur ^= 1;
+            HIP_CHECK(hipStreamSynchronize(sl[k].stream));  // its window is free again
+            uint8_t* win = sl[k].window.u8();
+            const uint64_t got = src.read(win, W);
+            if (src.err) {
+                sl.sync_all();
+                return io_status(src.err);
+            }
+            if (got == W && !src.done) {  // a full window with more to come
+                const uint32_t blk0 = (uint32_t)(pos / SD_CK_BLOCK);
+                if ((uint64_t)(blk0 + BPW) * 32 > fin.lvl[0].bytes) {
+                    sl.sync_all();
+                    fin.lvl[0].grow_preserve((size_t)(blk0 + BPW) * 64);
+                }
+                HIP_CHECK(hipMemcpyAsync(sl[k].staged.p, win, W, hipMemcpyHostToDevice, sl[k].stream));
+                HIP_CHECK(sdk::launch_ck_leaf(sl[k].staged.as<uint8_t>(), pos, blk0, prov_files.as<ck_file>(),
+                                              prov_map.as<uint2>(), BPW, fin.lvl[0].as<uint32_t>(),
+                                              sl[k].hashes.as<uint32_t>(), sl[k].stream));
+                pos += W;
+                continue;
+            }
+            const uint64_t L = pos + got;
+            const uint64_t nb = L == 0 ? 1 : (L + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
+            sl.sync_all();
+            fin.lvl[0].grow_preserve((size_t)nb * 32);  // plan_checksum_batch must not reallocate it
+            const uint64_t off0 = 0;
+            plan_checksum_batch(&fin, &off0, &L, 1, nullptr);
+            uint32_t* out = sl[k].hashes.as<uint32_t>();
+            if (got > 0 || L == 0) {
+                memset(win + got, 0, 64);
+                HIP_CHECK(hipMemcpyAsync(sl[k].staged.p, win, align_up(got, 64) + 64, hipMemcpyHostToDevice,
+                                         sl[k].stream));
+                const uint32_t wg0 = (uint32_t)(pos / SD_CK_BLOCK);
+                HIP_CHECK(sdk::launch_ck_leaf(sl[k].staged.as<uint8_t>(), pos, 0, fin.files.as<ck_file>(),
+                                              fin.wg_map.as<uint2>() + wg0, (uint32_t)(nb - wg0),
+                                              fin.lvl[0].as<uint32_t>(), out, sl[k].stream));
+            }
+            run_checksum_reduce(&fin, out, sl[k].stream);
+            HIP_CHECK(hipMemcpyAsync(sl[k].host_hashes.p, out, 32, hipMemcpyDeviceToHost, sl[k].stream));
+            HIP_CHECK(hipStreamSynchronize(sl[k].stream));
+            memcpy(out32, sl[k].host_hashes.p, 32);
+            return SD_FILE_OK;
+        }
+    }
+};
+
+inline void to_hex(const uint8_t* h, int nbytes, char* out) { hex_lower(h, nbytes, out); }
+
+// Hashes (GPU, streaming) the whole-file cas message of a file that held more bytes than
+// its staged extent could take: le64(size) || every byte fs::read returns (cas.rs:25,29).
+int32_t cas_overflow(SlotPair& sl, int& cur, Streamer& st, const char* path, uint64_t size, char* out_hex17) {
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) return io_status(errno);
-    int32_t st = SD_FILE_OK;
-    if (e.kind == SD_KIND_WHOLE) {  // cas.rs:29 fs::read -- requires len == size
-        st = pread_exact(fd, dst + 8, size, 0);
-        if (st == SD_FILE_OK) {
-            uint8_t extra;
-            if (pread(fd, &extra, 1, (off_t)size) == 1) st = SD_FILE_SHORT_READ;  // file grew since stat
-        }
-    } else {  // cas.rs:31-58: header, 4 samples at 8192 + k*seek_jump, footer
-        const uint64_t H = SD_HEADER_OR_FOOTER_SIZE, S = SD_SAMPLE_SIZE;
-        const uint64_t jump = (size - 2 * H) / SD_SAMPLE_COUNT;
-        uint8_t* p = dst + 8;
-        st = pread_exact(fd, p, H, 0);
-        p += H;
-        uint64_t current_pos = H;
-        while (st == SD_FILE_OK) {
-            st = pread_exact(fd, p, S, current_pos);
-            p += S;
-            if (current_pos >= H + jump * (SD_SAMPLE_COUNT - 1)) break;
-            current_pos += jump;
-        }
-        if (st == SD_FILE_OK) st = pread_exact(fd, p, H, size - H);
+    MsgSource src(fd, MsgSource::READ_TO_EOF);
+    src.set_prefix_le64(size);
+    uint8_t h[32];
+    int32_t rc;
+    try {
+        rc = st.hash(sl, cur, src, size + 8, h);
+    } catch (...) {
+        close(fd);
+        throw;
     }
     close(fd);
-    return st;
+    if (rc == SD_FILE_OK) to_hex(h, 8, out_hex17);  // cas.rs:61 to_hex()[..16]
+    return rc;
 }
 
 }  // namespace
 
 // ------------------------------------------------------------------ tuning knobs
-#include <atomic>
-// defaults: sampled U = 2 with line-pair loads (22), whole-file work lists in one launch
-// with line-pair loads (8), checksum leaf with line-pair loads (1), LDS-bucket dedup
-// grouping (1) -- DESIGN.md §7
-static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{22}, {8}, {1}, {200}, {4096}, {32}, {0}, {1}};
+// defaults: 200 us coalescing window, 4096-request batches, 32 MiB file windows, LDS-bucket
+// dedup grouping, single-file calls on the CPU while fewer than 16 are in flight
+static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}};
 int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
 
 // ============================================================================ C ABI
@@ -717,9 +454,8 @@ extern "C" {
 int sd_cas_set_tuning(const char* key, int value) {
     SD_GUARD_BEGIN
     if (!key) throw sd_failure(SD_ERR_INVALID, "null key");
-    static const char* names[SD_TUNE_NKEYS] = {"sampled_variant", "whole_variant", "checksum_variant",
-                                               "coalesce_window_us", "coalesce_max", "files_window_mb",
-                                               "whole_lds_kb", "dedup_variant"};
+    static const char* names[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max", "files_window_mb",
+                                               "dedup_variant", "latency_cpu_max"};
     for (int k = 0; k < SD_TUNE_NKEYS; k++)
         if (strcmp(key, names[k]) == 0) {
             g_tune[k].store(value, std::memory_order_relaxed);
@@ -739,7 +475,7 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
     *out = nullptr;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
-        throw sd_failure(SD_ERR_DEVICE, "no HIP device available (libsdcas has no CPU fallback)");
+        throw sd_failure(SD_ERR_DEVICE, "no HIP device available (the sd_cpu_* entry points need none)");
     if (device < 0 || device >= count) throw sd_failure(SD_ERR_INVALID, "device index out of range");
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
@@ -789,20 +525,15 @@ int sd_cas_stage_plan(const uint64_t* sizes, size_t n, sd_extent* extents_out, u
     if (!total_bytes_out) throw sd_failure(SD_ERR_INVALID, "total_bytes_out is null");
     uint64_t off = 0;
     for (size_t i = 0; i < n; i++) {
-        sd_extent& e = extents_out[i];
-        e.size = sizes[i];
-        const bool whole = sizes[i] <= SD_MINIMUM_FILE_SIZE;  // cas.rs:27 (<=)
-        e.kind = whole ? SD_KIND_WHOLE : SD_KIND_SAMPLED;
-        e.msg_len = whole ? (uint32_t)(8 + sizes[i]) : SD_SAMPLED_MSG_LEN;
-        e.msg_offset = off;
-        off = align_up(off + e.msg_len, SD_STAGE_ALIGN);
+        extents_out[i] = plan_extent(sizes[i], off);
+        off = align_up(off + extents_out[i].msg_len, SD_STAGE_ALIGN);
     }
     *total_bytes_out = off;
     return SD_OK;
     SD_GUARD_END
 }
 
-int sd_cas_stage_file(const char* path, const sd_extent* ext, uint8_t* staged, int32_t* status) {
+int sd_cas_stage_file(const char* path, sd_extent* ext, uint8_t* staged, int32_t* status) {
     SD_GUARD_BEGIN
     if (!path || !ext || !staged || !status) throw sd_failure(SD_ERR_INVALID, "null argument");
     validate_extent(*ext, 0);
@@ -811,8 +542,8 @@ int sd_cas_stage_file(const char* path, const sd_extent* ext, uint8_t* staged, i
     SD_GUARD_END
 }
 
-int sd_cas_stage_files(const char* const* paths, const sd_extent* extents, size_t n, uint8_t* staged,
-                       int32_t* status, int nthreads) {
+int sd_cas_stage_files(const char* const* paths, sd_extent* extents, size_t n, uint8_t* staged, int32_t* status,
+                       int nthreads) {
     SD_GUARD_BEGIN
     if (n && (!paths || !extents || !staged || !status)) throw sd_failure(SD_ERR_INVALID, "null argument");
     for (size_t i = 0; i < n; i++) validate_extent(extents[i], i);
@@ -838,7 +569,9 @@ int sd_cas_batch_create(sd_cas_ctx* ctx, const sd_extent* extents, size_t n, sd_
     SD_GUARD_BEGIN
     if (!ctx || !out || (!extents && n)) throw sd_failure(SD_ERR_INVALID, "null argument");
     ctx->bind();
-    *out = build_cas_batch(extents, n);
+    auto b = std::make_unique<sd_cas_batch>();
+    plan_cas_batch(b.get(), extents, n, nullptr);
+    *out = b.release();
     return SD_OK;
     SD_GUARD_END
 }
@@ -873,7 +606,7 @@ int sd_cas_batch_run_part(sd_cas_ctx* ctx, const sd_cas_batch* batch, int parts,
 int sd_cas_batch_stats(const sd_cas_batch* b, uint64_t out[6]) {
     SD_GUARD_BEGIN
     if (!b || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
-    out[0] = b->n; out[1] = b->n_sampled; out[2] = b->n_whole; out[3] = b->total_chunks;
+    out[0] = b->n; out[1] = b->n_sampled; out[2] = b->n_whole + b->n_long; out[3] = b->whole_chunks;
     out[4] = b->compressions; out[5] = b->msg_bytes;
     return SD_OK;
     SD_GUARD_END
@@ -896,24 +629,13 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
         size_t gi = 0, gj = 0;
         bool busy = false;
     };
-    std::unique_ptr<Slot> slots[2] = {ctx->acquire(), ctx->acquire()};
-    struct Rel {
-        sd_cas_ctx* c;
-        std::unique_ptr<Slot>* s;
-        ~Rel() {
-            for (int k = 0; k < 2; k++)
-                if (s[k]) {
-                    (void)hipStreamSynchronize(s[k]->stream);
-                    c->release(std::move(s[k]));
-                }
-        }
-    } rel{ctx, slots};
+    SlotPair slots(ctx);
     sd_cas_batch batches[2];
     Win wins[2];
     auto harvest = [&](int k) {
         if (!wins[k].busy) return;
-        HIP_CHECK(hipStreamSynchronize(slots[k]->stream));
-        const uint8_t* h = reinterpret_cast<const uint8_t*>(slots[k]->host_hashes.p);
+        HIP_CHECK(hipStreamSynchronize(slots[k].stream));
+        const uint8_t* h = slots[k].host_hashes.u8();
         for (size_t q = wins[k].gi; q < wins[k].gj; q++) {
             to_hex(h + (q - wins[k].gi) * 32, 8, out_hex17 + live[q] * 17);  // cas.rs:61 to_hex()[..16]
             if (status) status[live[q]] = SD_FILE_OK;
@@ -942,7 +664,7 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
             e.msg_offset -= lo;
             ext.push_back(e);
         }
-        Slot& sl = *slots[w];
+        Slot& sl = slots[w];
         plan_cas_batch(&batches[w], ext.data(), ext.size(), sl.stream);
         sl.staged.ensure(hi - lo);
         sl.hashes.ensure(ext.size() * 32);
@@ -962,8 +684,10 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
 // Path-based drop-in batch: generate_cas_id (cas.rs:23-62) for n (path, size) pairs,
 // the sizes being the ones the caller's metadata reported (FileMetadata::new,
 // file_identifier/mod.rs:65-97).  Files are planned into windows of consecutive files;
-// the stager pool preads window k+1 into one pinned slot while window k's H2D copy,
-// kernels and D2H run on the other slot's stream.
+// the stager pool reads window k+1 into one pinned slot while window k's H2D copy,
+// kernels and D2H run on the other slot's stream.  A whole-kind file that turns out
+// longer than its planned extent (it grew since the caller's stat) is hashed afterwards
+// from the file itself, streamed (fs::read hashes every byte, cas.rs:29).
 int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n, char* out_hex17,
                      int32_t* status, int nthreads) {
     SD_GUARD_BEGIN
@@ -971,20 +695,9 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
     ctx->bind();
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 64) nthreads = 64;
-    StagePool& pool = ctx->stage_pool(nthreads);
+    std::shared_ptr<StagePool> pool = ctx->stage_pool(nthreads);
     const uint64_t WINDOW = (uint64_t)std::max(1, tuning_get(SD_TUNE_FILES_WINDOW_MB)) << 20;
-    std::unique_ptr<Slot> slots[2] = {ctx->acquire(), ctx->acquire()};
-    struct Rel {
-        sd_cas_ctx* c;
-        std::unique_ptr<Slot>* s;
-        ~Rel() {
-            for (int k = 0; k < 2; k++)
-                if (s[k]) {
-                    (void)hipStreamSynchronize(s[k]->stream);
-                    c->release(std::move(s[k]));
-                }
-        }
-    } rel{ctx, slots};
+    SlotPair slots(ctx);
     sd_cas_batch batches[2];
     struct Win {
         std::vector<size_t> files;  // hashed files of the window, in extent order
@@ -992,14 +705,14 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
     } wins[2];
     auto harvest = [&](int k) {
         if (!wins[k].busy) return;
-        HIP_CHECK(hipStreamSynchronize(slots[k]->stream));
-        const uint8_t* h = reinterpret_cast<const uint8_t*>(slots[k]->host_hashes.p);
+        HIP_CHECK(hipStreamSynchronize(slots[k].stream));
+        const uint8_t* h = slots[k].host_hashes.u8();
         for (size_t q = 0; q < wins[k].files.size(); q++)
             to_hex(h + q * 32, 8, out_hex17 + wins[k].files[q] * 17);  // cas.rs:61 to_hex()[..16]
         wins[k].busy = false;
     };
     std::vector<sd_extent> ext;
-    std::vector<size_t> idx;
+    std::vector<size_t> idx, overflow;
     size_t i = 0;
     for (int w = 0; i < n; w ^= 1) {
         // the next window: consecutive files whose messages fit WINDOW bytes
@@ -1007,27 +720,30 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
         idx.clear();
         uint64_t off = 0;
         while (i < n) {
-            const bool whole = sizes[i] <= SD_MINIMUM_FILE_SIZE;  // cas.rs:27
-            const uint32_t len = whole ? (uint32_t)(8 + sizes[i]) : SD_SAMPLED_MSG_LEN;
-            const uint64_t next = align_up(off + len, SD_STAGE_ALIGN);
+            const sd_extent e = plan_extent(sizes[i], off);
+            const uint64_t next = align_up(off + e.msg_len, SD_STAGE_ALIGN);
             if (!ext.empty() && next > WINDOW) break;
-            ext.push_back(sd_extent{sizes[i], off, len, whole ? (uint32_t)SD_KIND_WHOLE : (uint32_t)SD_KIND_SAMPLED});
+            ext.push_back(e);
             idx.push_back(i);
             off = next;
             i++;
         }
         harvest(w);  // slot w's previous window is done: its pinned buffer is free
-        Slot& sl = *slots[w];
+        Slot& sl = slots[w];
         sl.window.ensure(off + 64);
-        uint8_t* win = reinterpret_cast<uint8_t*>(sl.window.p);
-        pool.run(ext.size(), [&](size_t q) { status[idx[q]] = stage_one(paths[idx[q]], ext[q], win); });
-        // failed files (I/O error, short read) keep their status and leave the window
+        uint8_t* win = sl.window.u8();
+        pool->run(ext.size(), [&](size_t q) { status[idx[q]] = stage_one(paths[idx[q]], ext[q], win); });
+        // failed files (I/O error, short read) keep their status and leave the window;
+        // files longer than their extent are hashed from disk after the windows
         size_t m = 0;
-        for (size_t q = 0; q < ext.size(); q++)
+        for (size_t q = 0; q < ext.size(); q++) {
             if (status[idx[q]] == SD_FILE_OK) {
                 ext[m] = ext[q];
                 idx[m++] = idx[q];
+            } else if (status[idx[q]] == SD_FILE_CHANGED) {
+                overflow.push_back(idx[q]);
             }
+        }
         ext.resize(m);
         idx.resize(m);
         if (m == 0) continue;
@@ -1043,6 +759,11 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
     }
     harvest(0);
     harvest(1);
+    if (!overflow.empty()) {
+        Streamer st;
+        int cur = 0;
+        for (size_t f : overflow) status[f] = cas_overflow(slots, cur, st, paths[f], sizes[f], out_hex17 + f * 17);
+    }
     return SD_OK;
     SD_GUARD_END
 }
@@ -1053,7 +774,7 @@ int sd_cas_id_path(sd_cas_ctx* ctx, const char* path, uint64_t size, char* out_h
     if (!ctx || !path || !out_hex17 || !status) throw sd_failure(SD_ERR_INVALID, "null argument");
     std::string err;
     const int rc = coalescer_submit(ctx->coalescer(), 0, path, size, out_hex17, status, &err);
-    if (rc != SD_OK) set_err("%s", err.c_str());
+    if (rc != SD_OK) sd_set_err("%s", err.c_str());
     return rc;
     SD_GUARD_END
 }
@@ -1063,12 +784,12 @@ int sd_file_checksum_path(sd_cas_ctx* ctx, const char* path, char* out_hex65, in
     if (!ctx || !path || !out_hex65 || !status) throw sd_failure(SD_ERR_INVALID, "null argument");
     std::string err;
     const int rc = coalescer_submit(ctx->coalescer(), 1, path, 0, out_hex65, status, &err);
-    if (rc != SD_OK) set_err("%s", err.c_str());
+    if (rc != SD_OK) sd_set_err("%s", err.c_str());
     return rc;
     SD_GUARD_END
 }
 
-int sd_coalescer_stats(sd_cas_ctx* ctx, uint64_t out[3]) {
+int sd_coalescer_stats(sd_cas_ctx* ctx, uint64_t out[4]) {
     SD_GUARD_BEGIN
     if (!ctx || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
     coalescer_stats(ctx->coalescer(), out);
@@ -1082,7 +803,9 @@ int sd_checksum_batch_create(sd_cas_ctx* ctx, const uint64_t* offsets, const uin
     SD_GUARD_BEGIN
     if (!ctx || !out || (n && (!offsets || !lens))) throw sd_failure(SD_ERR_INVALID, "null argument");
     ctx->bind();
-    *out = build_checksum_batch(offsets, lens, n);
+    auto b = std::make_unique<sd_checksum_batch>();
+    plan_checksum_batch(b.get(), offsets, lens, n, nullptr);
+    *out = b.release();
     return SD_OK;
     SD_GUARD_END
 }
@@ -1107,152 +830,133 @@ int sd_checksum_batch_run(sd_cas_ctx* ctx, const sd_checksum_batch* b, const uin
 int sd_checksum_batch_stats(const sd_checksum_batch* b, uint64_t out[4]) {
     SD_GUARD_BEGIN
     if (!b || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
-    out[0] = b->n; out[1] = b->total_bytes; out[2] = b->compressions; out[3] = b->blocks;
+    out[0] = b->n; out[1] = b->plan.total_bytes; out[2] = b->plan.compressions; out[3] = b->plan.blocks;
     return SD_OK;
     SD_GUARD_END
 }
 
+// file_checksum (hash.rs:10-24) for n paths.  Each file is read as the reference reads it:
+// one read() of 1 MiB at a time until one returns fewer (hash.rs:15-19) -- the file's
+// length at stat time only picks the route.  Files that fit are packed (64-B aligned)
+// into the current slot's pinned window, one batch per window; while the GPU hashes one
+// slot's window the host reads the next into the other.  A file too large for a window,
+// or one that outgrows the room it was given, is streamed window by window (Streamer),
+// starting with the bytes already read.
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65, int32_t* status) {
     SD_GUARD_BEGIN
     if (!ctx || (n && (!paths || !out_hex65 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
     ctx->bind();
-    // Two slots, each with a pinned window, a device window and a stream.  Files that fit
-    // a window are packed (64-B aligned) into one batch per window; larger files stream
-    // window by window into their own batch's leaf CVs, then reduce.  While the GPU hashes
-    // one slot's window, the host reads the next window into the other slot.
-    const uint64_t W = 256ull << 20;  // a multiple of the 1 MiB leaf block
-    std::unique_ptr<Slot> slots[2] = {ctx->acquire(), ctx->acquire()};
-    struct Rel {
-        sd_cas_ctx* c;
-        std::unique_ptr<Slot>* s;
-        ~Rel() {
-            for (int k = 0; k < 2; k++)
-                if (s[k]) {
-                    (void)hipStreamSynchronize(s[k]->stream);
-                    c->release(std::move(s[k]));
-                }
-        }
-    } rel{ctx, slots};
-    for (int k = 0; k < 2; k++) {
-        slots[k]->window.ensure(W + 128);
-        slots[k]->staged.ensure(W + 128);
-    }
+    constexpr uint64_t W = Streamer::W;
+    constexpr uint64_t RD = MsgSource::CHECKSUM_READ;  // hash.rs:8 BLOCK_LEN
+    SlotPair slots(ctx);
+    Streamer::prepare(slots);
     struct Pending {
         std::vector<size_t> files;  // files whose hashes land in this slot's host_hashes
         bool busy = false;
     } pend[2];
-    sd_checksum_batch pack_batch[2], big;
+    sd_checksum_batch pack_batch[2];
+    Streamer streamer;
     int cur = 0;
     auto harvest = [&](int k) {
         if (!pend[k].busy) return;
-        HIP_CHECK(hipStreamSynchronize(slots[k]->stream));
-        const uint8_t* h = reinterpret_cast<const uint8_t*>(slots[k]->host_hashes.p);
+        HIP_CHECK(hipStreamSynchronize(slots[k].stream));
+        const uint8_t* h = slots[k].host_hashes.u8();
         for (size_t q = 0; q < pend[k].files.size(); q++)
             to_hex(h + 32 * q, 32, out_hex65 + pend[k].files[q] * 65);  // hash.rs:21-23
         pend[k].files.clear();
         pend[k].busy = false;
     };
+    // the pack being filled lives in slot `cur`'s window
     std::vector<size_t> pack;
-    std::vector<uint64_t> pack_len;
-    uint64_t pack_bytes = 0;
+    std::vector<uint64_t> pack_off, pack_len;
+    uint64_t pack_end = 0;
+    bool pack_open = false;
+    auto open_pack = [&]() {
+        if (pack_open) return;
+        harvest(cur);
+        pack_open = true;
+        pack_end = 0;
+    };
     auto submit_pack = [&]() {
-        if (pack.empty()) return;
+        if (!pack_open) return;
+        pack_open = false;
         const int k = cur;
         cur ^= 1;
-        harvest(k);
-        Slot& sl = *slots[k];
-        uint8_t* win = reinterpret_cast<uint8_t*>(sl.window.p);
-        std::vector<uint64_t> offs, lens;
-        std::vector<size_t> ok;
-        uint64_t off = 0;
-        for (size_t q = 0; q < pack.size(); q++) {  // hash.rs:13-20 reads, one pread per file
-            const size_t i = pack[q];
-            const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
-            if (fd < 0) {
-                status[i] = io_status(errno);
-                continue;
-            }
-            const int32_t st = pread_exact(fd, win + off, pack_len[q], 0);
-            close(fd);
-            if (st != SD_FILE_OK) {
-                status[i] = st;
-                continue;
-            }
-            memset(win + off + pack_len[q], 0, align_up(pack_len[q] + 1, 64) - pack_len[q]);
-            offs.push_back(off);
-            lens.push_back(pack_len[q]);
-            ok.push_back(i);
-            off = align_up(off + pack_len[q] + 1, 64);
-        }
-        pack.clear();
-        pack_len.clear();
-        pack_bytes = 0;
-        if (ok.empty()) return;
-        plan_checksum_batch(&pack_batch[k], offs.data(), lens.data(), ok.size(), sl.stream);
-        sl.hashes.ensure(ok.size() * 32);
-        sl.host_hashes.ensure(ok.size() * 32);
-        HIP_CHECK(hipMemcpyAsync(sl.staged.p, win, off + 64, hipMemcpyHostToDevice, sl.stream));
+        if (pack.empty()) return;
+        Slot& sl = slots[k];
+        plan_checksum_batch(&pack_batch[k], pack_off.data(), pack_len.data(), pack.size(), sl.stream);
+        sl.hashes.ensure(pack.size() * 32);
+        sl.host_hashes.ensure(pack.size() * 32);
+        HIP_CHECK(hipMemcpyAsync(sl.staged.p, sl.window.p, pack_end + 64, hipMemcpyHostToDevice, sl.stream));
         run_checksum_batch(&pack_batch[k], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
-        HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, ok.size() * 32, hipMemcpyDeviceToHost, sl.stream));
-        pend[k].files = std::move(ok);
+        HIP_CHECK(
+            hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, pack.size() * 32, hipMemcpyDeviceToHost, sl.stream));
+        pend[k].files = pack;
         pend[k].busy = true;
+        pack.clear();
+        pack_off.clear();
+        pack_len.clear();
     };
-    for (size_t i = 0; i < n; i++) {
-        status[i] = SD_FILE_OK;
-        struct stat stt;
-        if (stat(paths[i], &stt) != 0) {
-            status[i] = io_status(errno);
-            continue;
-        }
-        const uint64_t len = (uint64_t)stt.st_size;  // hash.rs reads to EOF; the length is fixed here
-        if (len + 128 <= W) {
-            if (pack_bytes + align_up(len + 1, 64) + 64 > W) submit_pack();
-            pack.push_back(i);
-            pack_len.push_back(len);
-            pack_bytes += align_up(len + 1, 64);
-            continue;
-        }
-        // a large file: flush the pack, then stream windows through alternating slots
+    auto stream_file = [&](size_t i, MsgSource& src, uint64_t hint) {
         submit_pack();
         harvest(0);
         harvest(1);
-        const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+        uint8_t h[32];
+        status[i] = streamer.hash(slots, cur, src, hint, h);
+        if (status[i] == SD_FILE_OK) to_hex(h, 32, out_hex65 + i * 65);
+    };
+    std::vector<uint8_t> spill;
+    for (size_t i = 0; i < n; i++) {
+        status[i] = SD_FILE_OK;
+        const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);  // hash.rs:11
         if (fd < 0) {
             status[i] = io_status(errno);
             continue;
         }
-        const uint64_t off0 = 0;
-        plan_checksum_batch(&big, &off0, &len, 1, nullptr);
-        for (int k = 0; k < 2; k++) slots[k]->hashes.ensure(32);
-        const uint32_t blocks_per_window = (uint32_t)(W / CK_BLOCK_BYTES);
-        for (uint64_t pos = 0; pos < len && status[i] == SD_FILE_OK; pos += W) {
-            const int k = cur;
-            cur ^= 1;
-            HIP_CHECK(hipStreamSynchronize(slots[k]->stream));  // its window is free again
-            Slot& sl = *slots[k];
-            uint8_t* win = reinterpret_cast<uint8_t*>(sl.window.p);
-            const uint64_t n_here = std::min<uint64_t>(W, len - pos);
-            const int32_t st = pread_exact(fd, win, n_here, pos);
-            if (st != SD_FILE_OK) {
-                status[i] = st;
+        struct stat stt;
+        const uint64_t hint = fstat(fd, &stt) == 0 ? (uint64_t)stt.st_size : 0;
+        MsgSource src(fd, MsgSource::CHECKSUM_READS);
+        if (hint + RD + 128 > W / 2) {  // large: stream it
+            stream_file(i, src, hint);
+            close(fd);
+            continue;
+        }
+        open_pack();
+        if (pack_end + align_up(hint, RD) + RD + 64 > W) {  // this pack is full: start the next
+            submit_pack();
+            open_pack();
+        }
+        uint8_t* win = slots[cur].window.u8();
+        const uint64_t off0 = pack_end;
+        uint64_t got = 0;
+        bool overflowed = false;
+        for (;;) {  // hash.rs:14-20, one 1 MiB read per iteration, straight into the window
+            if (off0 + got + RD + 64 > W) {
+                overflowed = true;
                 break;
             }
-            memset(win + n_here, 0, 64);
-            HIP_CHECK(hipMemcpyAsync(sl.staged.p, win, align_up(n_here, 64) + 64, hipMemcpyHostToDevice, sl.stream));
-            const uint32_t wg0 = (uint32_t)(pos / CK_BLOCK_BYTES);
-            const uint32_t wg1 = (uint32_t)std::min<uint64_t>(big.wg_map_h.size(), (uint64_t)wg0 + blocks_per_window);
-            run_checksum_leaf(&big, sl.staged.as<uint8_t>(), pos, wg0, wg1, sl.hashes.as<uint32_t>(), sl.stream);
+            const uint64_t r = src.read(win + off0 + got, RD);
+            got += r;
+            if (src.err || src.done) break;
+        }
+        if (src.err) {
+            status[i] = io_status(src.err);
+            close(fd);
+            continue;
+        }
+        if (overflowed) {  // outgrew its room: stream it, starting with the bytes read so far
+            spill.assign(win + off0, win + off0 + got);
+            src.set_pending(spill.data(), spill.size());
+            stream_file(i, src, got + RD);
+            close(fd);
+            continue;
         }
         close(fd);
-        HIP_CHECK(hipStreamSynchronize(slots[0]->stream));
-        HIP_CHECK(hipStreamSynchronize(slots[1]->stream));
-        if (status[i] != SD_FILE_OK) continue;
-        Slot& sl = *slots[0];
-        run_checksum_reduce(&big, sl.hashes.as<uint32_t>(), sl.stream);
-        sl.host_hashes.ensure(32);
-        HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, 32, hipMemcpyDeviceToHost, sl.stream));
-        HIP_CHECK(hipStreamSynchronize(sl.stream));
-        to_hex(reinterpret_cast<const uint8_t*>(sl.host_hashes.p), 32, out_hex65 + i * 65);
+        memset(win + off0 + got, 0, align_up(got, 64) + 64 - got);
+        pack.push_back(i);
+        pack_off.push_back(off0);
+        pack_len.push_back(got);
+        pack_end = align_up(off0 + got, 64);
     }
     submit_pack();
     harvest(0);
@@ -1449,16 +1153,6 @@ int sd_valu_peak(sd_cas_ctx* ctx, double* lane_ops_per_s) {
 }
 
 }  // extern "C"
-
-// ----------------------------------------------------------------- internal helpers
-namespace {
-void run_checksum_leaf(const sd_checksum_batch* b, const uint8_t* d_data, uint64_t shift, uint32_t wg0, uint32_t wg1,
-                       uint32_t* out, hipStream_t s) {
-    if (wg1 <= wg0) return;
-    HIP_CHECK(sdk::launch_ck_leaf(d_data, shift, b->files.as<ck_file>(), b->wg_map.as<uint2>() + wg0, wg1 - wg0,
-                                  b->lvl[0].as<uint32_t>(), out, s));
-}
-}  // namespace
 
 static int time_loop(sd_cas_ctx* ctx, void* stream, int iters, float* ms,
                      const std::function<void(hipStream_t)>& fn) {

@@ -1,0 +1,319 @@
+// sd_host.cpp -- GPU-free host logic of libsdcas (see sd_host.h): batch planners, the
+// file stager with generate_cas_id's read semantics (cas.rs:23-62), and the sequential
+// message reader with file_checksum's (hash.rs:10-24).
+#include "sd_host.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+
+// ------------------------------------------------------------------ planners
+sd_extent plan_extent(uint64_t size, uint64_t off) {
+    sd_extent e;
+    e.size = size;
+    const bool whole = size <= SD_MINIMUM_FILE_SIZE;  // cas.rs:27 (<=)
+    e.kind = whole ? SD_KIND_WHOLE : SD_KIND_SAMPLED;
+    e.msg_len = whole ? (uint32_t)(8 + size) : SD_SAMPLED_MSG_LEN;
+    e.msg_offset = off;
+    return e;
+}
+
+void validate_extent(const sd_extent& e, size_t i) {
+    const bool whole = e.size <= SD_MINIMUM_FILE_SIZE;
+    const bool len_ok = whole ? e.msg_len >= 8 : e.msg_len == SD_SAMPLED_MSG_LEN;
+    if (e.kind != (whole ? SD_KIND_WHOLE : SD_KIND_SAMPLED) || !len_ok)
+        throw sd_failure(SD_ERR_INVALID, "extent " + std::to_string(i) + ": kind/msg_len do not match size");
+    if (e.msg_offset % 16)
+        throw sd_failure(SD_ERR_INVALID, "extent " + std::to_string(i) + ": msg_offset not 16-byte aligned");
+}
+
+uint32_t msg_chunks(uint32_t msg_len) { return msg_len == 0 ? 1u : (msg_len + 1023u) / 1024u; }
+
+uint64_t msg_compressions(uint64_t len) {
+    const uint64_t C = len == 0 ? 1 : (len + 1023) / 1024;
+    const uint64_t last = len - (C - 1) * 1024;
+    return (C - 1) * 16 + (last == 0 ? 1 : (last + 63) / 64) + (C - 1);
+}
+
+namespace {
+// compressions of aligned chunk pair (c0, c0 + 1) holding glen (1..2048) message bytes
+uint32_t pair_compressions(uint32_t glen) {
+    const uint32_t l0 = std::min<uint32_t>(glen, 1024), l1 = glen - l0;
+    return (l0 + 63) / 64 + (l1 ? (l1 + 63) / 64 + 1 : 0);
+}
+bool items_message(const sd_extent& e) { return e.kind == SD_KIND_WHOLE && e.msg_len <= SD_WHOLE_ITEMS_MAX; }
+}  // namespace
+
+// Work lists for the whole-file messages (msg_len <= SD_WHOLE_ITEMS_MAX) of ext[0, n):
+//  * full-pair items in file (= staged address) order, so the waves sweep the staged
+//    buffer front to back as the sampled kernel does;
+//  * tail items counting-sorted by compressions, descending (equal trip counts per wave);
+//  * merge8 items -- pass A over aligned groups of <= 8 pair nodes (the whole tree when a
+//    message has <= 8 nodes), pass B over the pass-A nodes of messages with more than 8.
+// CV slots and merge items follow the multi-pair messages sorted by pair count, descending,
+// so the lanes of a merge wave have nearly equal trip counts.
+void plan_whole_items(WholePlan& p, const sd_extent* ext, size_t n) {
+    p.full.clear();
+    p.tail.clear();
+    p.merge_a.clear();
+    p.merge_b.clear();
+    constexpr uint32_t PMAX = (SD_WHOLE_ITEMS_MAX + 2047) / 2048;  // 51 pairs
+    auto pairs = [&](size_t i) { return (msg_chunks(ext[i].msg_len) + 1) / 2; };
+    // multi-pair messages (>= 3 chunks) by pair count, descending: counting sort
+    std::vector<uint32_t> start(PMAX + 2, 0);
+    for (size_t i = 0; i < n; i++)
+        if (items_message(ext[i]) && msg_chunks(ext[i].msg_len) >= 3) start[PMAX - pairs(i)]++;
+    uint32_t acc = 0;
+    for (auto& s : start) {
+        const uint32_t t = s;
+        s = acc;
+        acc += t;
+    }
+    std::vector<uint32_t> sorted(acc);
+    for (size_t i = 0; i < n; i++)
+        if (items_message(ext[i]) && msg_chunks(ext[i].msg_len) >= 3) sorted[start[PMAX - pairs(i)]++] = (uint32_t)i;
+    std::vector<uint32_t> slot(n, 0);  // first CV slot of each multi-pair message
+    uint32_t cv = 0;
+    for (uint32_t f : sorted) {
+        slot[f] = cv;
+        cv += pairs(f);
+    }
+    std::vector<uint8_t> tail_cost;
+    for (size_t file = 0; file < n; file++) {
+        const sd_extent& e = ext[file];
+        if (!items_message(e)) continue;
+        const uint32_t C = msg_chunks(e.msg_len), P = (C + 1) / 2;
+        const bool multi = C >= 3;
+        for (uint32_t j = 0; j < P; j++) {
+            const uint64_t off = e.msg_offset + 2048ull * j;
+            const uint32_t glen = std::min<uint32_t>(2048, e.msg_len - 2048 * j);
+            const uint32_t lo = (uint32_t)off, hi = (uint32_t)(off >> 32);
+            if (multi && glen == 2048) {
+                p.full.push_back({lo, hi, slot[file] + j, 2 * j});
+            } else {
+                const uint32_t w = glen | ((2 * j) << 12) | (multi ? 0u : 0x80000000u);
+                p.tail.push_back({lo, hi, multi ? slot[file] + j : (uint32_t)file, w});
+                tail_cost.push_back((uint8_t)pair_compressions(glen));
+            }
+        }
+    }
+    {  // stable counting sort of the tail items by cost, descending (cost 1..33)
+        std::vector<uint32_t> st(35, 0);
+        for (uint8_t c : tail_cost) st[34 - c]++;
+        uint32_t a = 0;
+        for (auto& s : st) {
+            const uint32_t t = s;
+            s = a;
+            a += t;
+        }
+        std::vector<sd_u32x4> out(p.tail.size());
+        for (size_t i = 0; i < p.tail.size(); i++) out[st[34 - tail_cost[i]]++] = p.tail[i];
+        p.tail.swap(out);
+    }
+    uint32_t cv2 = 0;
+    for (uint32_t file : sorted) {
+        const uint32_t P = pairs(file);
+        if (P <= 8) {
+            p.merge_a.push_back({slot[file], P | 0x80000000u, file, 0});
+            continue;
+        }
+        const uint32_t G = (P + 7) / 8;  // <= 7 for messages of <= 102408 B
+        for (uint32_t a = 0; a < G; a++)
+            p.merge_a.push_back({slot[file] + 8 * a, std::min<uint32_t>(8, P - 8 * a), cv2 + a, 0});
+        p.merge_b.push_back({cv2, G | 0x80000000u, file, 0});
+        cv2 += G;
+    }
+    p.n_cv = cv;
+    p.n_cv2 = cv2;
+}
+
+// Checksum batch over byte ranges: one leaf workgroup per 1 MiB block of each message;
+// reduce passes of groups of 256 CVs per workgroup until every message has its root.
+void plan_checksum(CkPlan& p, const uint64_t* offsets, const uint64_t* lens, size_t n) {
+    if (n >= (1ull << 31)) throw sd_failure(SD_ERR_INVALID, "batch too large");
+    p.files.resize(n);
+    p.wg_map.clear();
+    p.passes.clear();
+    p.total_bytes = p.compressions = p.blocks = 0;
+    std::vector<uint64_t> level_n(n), base(n, 0);
+    uint64_t cv0 = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (offsets[i] % 16)
+            throw sd_failure(SD_ERR_INVALID, "checksum range " + std::to_string(i) + " not 16-byte aligned");
+        const uint64_t nb = lens[i] == 0 ? 1 : (lens[i] + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
+        if (nb >= (1ull << 32)) throw sd_failure(SD_ERR_INVALID, "file too large");
+        p.files[i] = ck_file{offsets[i], lens[i], nb > 1 ? cv0 : 0};
+        for (uint64_t k = 0; k < nb; k++) p.wg_map.push_back({(uint32_t)i, (uint32_t)k});
+        base[i] = p.files[i].cv_base;
+        if (nb > 1) cv0 += nb;
+        level_n[i] = nb;
+        p.total_bytes += lens[i];
+        p.compressions += msg_compressions(lens[i]);
+        p.blocks += nb;
+    }
+    p.lvl_cap[0] = cv0;
+    p.lvl_cap[1] = 0;
+    int src = 0;
+    for (;;) {
+        std::vector<ck_reduce_wg> wgs;
+        uint64_t dst_total = 0;
+        std::vector<uint64_t> nbase(n, 0);
+        for (size_t i = 0; i < n; i++) {
+            const uint64_t cnt = level_n[i];
+            if (cnt <= 1) continue;
+            const uint64_t groups = (cnt + 255) / 256;
+            nbase[i] = dst_total;
+            for (uint64_t g = 0; g < groups; g++) {
+                ck_reduce_wg w{};
+                w.src_base = base[i] + g * 256;
+                w.dst_index = dst_total + g;
+                w.count = (uint32_t)std::min<uint64_t>(256, cnt - g * 256);
+                w.file = (uint32_t)i;
+                w.is_root = groups == 1;
+                wgs.push_back(w);
+            }
+            dst_total += groups == 1 ? 0 : groups;
+            level_n[i] = groups == 1 ? 1 : groups;
+        }
+        if (wgs.empty()) break;
+        p.passes.push_back(std::move(wgs));
+        p.lvl_cap[1 - src] = std::max<uint64_t>(p.lvl_cap[1 - src], dst_total);
+        base = nbase;
+        src = 1 - src;
+    }
+}
+
+// ------------------------------------------------------------------ file reading
+namespace {
+
+// read exactly n bytes at off (read_exact after a seek); 0, SD_FILE_SHORT_READ or io_status
+int32_t pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
+    while (n) {
+        const ssize_t r = pread(fd, dst, n, (off_t)off);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return io_status(errno);
+        }
+        if (r == 0) return SD_FILE_SHORT_READ;
+        dst += r;
+        n -= (uint64_t)r;
+        off += (uint64_t)r;
+    }
+    return SD_FILE_OK;
+}
+
+// one read() call, retried on EINTR (tokio's blocking read is uninterruptible)
+ssize_t read_once(int fd, uint8_t* dst, uint64_t n) {
+    for (;;) {
+        const ssize_t r = read(fd, dst, n);
+        if (r < 0 && errno == EINTR) continue;
+        return r;
+    }
+}
+
+struct Fd {
+    int fd;
+    ~Fd() {
+        if (fd >= 0) close(fd);
+    }
+};
+
+}  // namespace
+
+int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged) {
+    uint8_t* dst = staged + e.msg_offset;
+    const uint64_t size = e.size;
+    for (int i = 0; i < 8; i++) dst[i] = (uint8_t)(size >> (8 * i));  // cas.rs:25 le64
+    const uint64_t padded = sd_align_up(e.msg_len, SD_STAGE_PAD);   // the planned extent's end
+    Fd f{open(path, O_RDONLY | O_CLOEXEC)};
+    if (f.fd < 0) return io_status(errno);
+    if (e.kind == SD_KIND_WHOLE) {  // cas.rs:29 fs::read: read_to_end
+        const uint64_t room = e.msg_len - 8;
+        uint64_t got = 0;
+        for (;;) {
+            if (got == room) {  // planned room full: does the file hold more?
+                uint8_t probe;
+                const ssize_t r = read_once(f.fd, &probe, 1);
+                if (r < 0) return io_status(errno);
+                if (r > 0) return SD_FILE_CHANGED;
+                break;
+            }
+            const ssize_t r = read_once(f.fd, dst + 8 + got, room - got);
+            if (r < 0) return io_status(errno);
+            if (r == 0) break;
+            got += (uint64_t)r;
+        }
+        e.msg_len = (uint32_t)(8 + got);
+        memset(dst + e.msg_len, 0, padded - e.msg_len);
+        return SD_FILE_OK;
+    }
+    // cas.rs:31-58: header, 4 samples at 8192 + k * seek_jump, footer at End(-8192)
+    memset(dst + e.msg_len, 0, padded - e.msg_len);
+    const uint64_t H = SD_HEADER_OR_FOOTER_SIZE, S = SD_SAMPLE_SIZE;
+    const uint64_t jump = (size - 2 * H) / SD_SAMPLE_COUNT;
+    uint8_t* p = dst + 8;
+    int32_t st = pread_exact(f.fd, p, H, 0);  // :35-38
+    p += H;
+    uint64_t current_pos = H;
+    while (st == SD_FILE_OK) {  // :42-51
+        st = pread_exact(f.fd, p, S, current_pos);
+        p += S;
+        if (current_pos >= H + jump * (SD_SAMPLE_COUNT - 1)) break;
+        current_pos += jump;
+    }
+    if (st != SD_FILE_OK) return st;
+    const off_t end = lseek(f.fd, -(off_t)H, SEEK_END);  // :54-55 SeekFrom::End(-8192)
+    if (end < 0) return io_status(errno);
+    return pread_exact(f.fd, p, H, (uint64_t)end);  // :56-58
+}
+
+void MsgSource::set_prefix_le64(uint64_t v) {
+    for (int i = 0; i < 8; i++) prefix_[i] = (uint8_t)(v >> (8 * i));
+    prefix_len_ = 8;
+    prefix_pos_ = 0;
+}
+
+uint64_t MsgSource::read(uint8_t* dst, uint64_t n) {
+    uint64_t got = 0;
+    while (got < n && prefix_pos_ < prefix_len_) dst[got++] = prefix_[prefix_pos_++];
+    if (pend_len_ && got < n) {
+        const uint64_t k = std::min(pend_len_, n - got);
+        memcpy(dst + got, pend_, k);
+        pend_ += k;
+        pend_len_ -= k;
+        got += k;
+    }
+    if (done || err) return got;
+    if (mode_ == READ_TO_EOF) {
+        while (got < n) {
+            const ssize_t r = read_once(fd_, dst + got, n - got);
+            if (r < 0) {
+                err = errno;
+                break;
+            }
+            if (r == 0) {
+                done = true;
+                break;
+            }
+            got += (uint64_t)r;
+        }
+        return got;
+    }
+    while (got < n) {  // hash.rs:14-20
+        const uint64_t want = std::min<uint64_t>(CHECKSUM_READ, n - got);
+        const ssize_t r = read_once(fd_, dst + got, want);
+        if (r < 0) {
+            err = errno;
+            break;
+        }
+        got += (uint64_t)r;
+        if ((uint64_t)r != CHECKSUM_READ) {  // :17-19 a short read ends the file
+            done = true;
+            break;
+        }
+    }
+    return got;
+}

@@ -1,0 +1,180 @@
+// sd_host.h -- the GPU-free half of libsdcas: batch planners, the file stager with the
+// reference's read semantics, the sequential message reader, error plumbing.
+//
+// Nothing here includes HIP, so this code (sd_host.cpp, cpu_blake3.cpp, stage_pool.h) is
+// also built with g++ under ASan/UBSan and TSan by `make sanitize` (csrc/host_selftest.cpp).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/sd_cas.h"
+
+// ------------------------------------------------------------------ errors
+struct sd_failure : std::runtime_error {
+    int rc;
+    sd_failure(int r, const std::string& m) : std::runtime_error(m), rc(r) {}
+};
+void sd_set_err(const char* fmt, ...);
+
+// every extern "C" entry point: no C++ exception crosses the ABI (the reference FFI fences
+// panics with catch_unwind, apps/mobile/modules/sd-core/ios/crate/src/lib.rs:41,60)
+#define SD_GUARD_BEGIN try {
+#define SD_GUARD_END                                   \
+    }                                                  \
+    catch (const sd_failure& f) {                      \
+        sd_set_err("%s", f.what());                    \
+        return f.rc;                                   \
+    }                                                  \
+    catch (const std::bad_alloc&) {                    \
+        sd_set_err("host allocation failed");          \
+        return SD_ERR_NOMEM;                           \
+    }                                                  \
+    catch (const std::exception& ex) {                 \
+        sd_set_err("internal error: %s", ex.what());   \
+        return SD_ERR_INTERNAL;                        \
+    }                                                  \
+    catch (...) {                                      \
+        sd_set_err("internal error");                  \
+        return SD_ERR_INTERNAL;                        \
+    }
+
+inline uint64_t sd_align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+// sd_file_status IO_ERROR with the errno in the high 16 bits
+inline int32_t io_status(int err) { return (int32_t)(SD_FILE_IO_ERROR | ((uint32_t)(err & 0xFFFF) << 16)); }
+
+// What the kernels need of a staged message: a 16-byte aligned start (validate_extent) and
+// zero padding up to the next 64-byte boundary.  The planner places messages on
+// SD_STAGE_ALIGN (128, whole cache lines) but callers' own layouts only need this.
+constexpr uint64_t SD_STAGE_PAD = 64;
+// Whole-file cas messages up to this length (8 + 102400: every file the reference hashes
+// whole when its length equals `size`) go through the work-list kernels; longer ones (a
+// file that grew past the size it was planned with) through the chunk-parallel checksum
+// kernels -- a message is just bytes.
+constexpr uint32_t SD_WHOLE_ITEMS_MAX = 8 + SD_MINIMUM_FILE_SIZE;
+// hash.rs:8 BLOCK_LEN: file_checksum reads 1 MiB per read call; also the checksum
+// kernels' leaf block (1024 chunks per workgroup)
+constexpr uint64_t SD_CK_BLOCK = 1ull << 20;
+
+// ------------------------------------------------------------------ device tables
+struct sd_u32x2 { uint32_t x, y; };        // layout of HIP's uint2
+struct sd_u32x4 { uint32_t x, y, z, w; };  // layout of HIP's uint4
+
+// one message of a checksum batch
+struct ck_file {
+    uint64_t offset;   // byte offset in the data buffer
+    uint64_t len;      // message length
+    uint64_t cv_base;  // first slot of this message's 1 MiB block CVs in the level-0 CV buffer
+};
+
+// one workgroup of a checksum reduce pass
+struct ck_reduce_wg {
+    uint64_t src_base;   // first CV (index into the source level) of this group
+    uint64_t dst_index;  // CV slot in the destination level
+    uint32_t count;      // CVs in this group (1..256)
+    uint32_t file;       // file index (for the root output)
+    uint32_t is_root;    // the group is the file's whole level: ROOT on the final parent
+    uint32_t pad;
+};
+
+// ------------------------------------------------------------------ planners
+// cas.rs:25-58 message layout of a file of `size` bytes at `off`: le64(size) || the whole
+// file (size <= 102400, cas.rs:27 -- inclusive) or head / 4 samples / tail (57 352 B)
+sd_extent plan_extent(uint64_t size, uint64_t off);
+// the kind follows the size argument (cas.rs:27); a sampled message is 57 352 B; a whole
+// message is le64(size) + the bytes the file held when read (any count, cas.rs:29)
+void validate_extent(const sd_extent& e, size_t i);
+uint32_t msg_chunks(uint32_t msg_len);
+// BLAKE3 compressions of a message: block compressions of every chunk + parents
+uint64_t msg_compressions(uint64_t len);
+
+// whole-file work lists (item formats: cas_kernels.hip, k_whole_items / k_whole_merge8)
+struct WholePlan {
+    std::vector<sd_u32x4> full, tail, merge_a, merge_b;
+    uint32_t n_cv = 0, n_cv2 = 0;  // pair-node CV slots, pass-A output slots
+};
+void plan_whole_items(WholePlan& p, const sd_extent* ext, size_t n);
+
+// checksum batch plan: per-message tables, leaf workgroups, reduce passes
+struct CkPlan {
+    std::vector<ck_file> files;
+    std::vector<sd_u32x2> wg_map;                 // leaf workgroup -> (message, 1 MiB block)
+    std::vector<std::vector<ck_reduce_wg>> passes;  // reduce passes, level 0 -> 1 -> 0 ...
+    uint64_t lvl_cap[2] = {0, 0};                 // CVs each level buffer must hold
+    uint64_t total_bytes = 0, compressions = 0, blocks = 0;
+};
+void plan_checksum(CkPlan& p, const uint64_t* offsets, const uint64_t* lens, size_t n);
+
+// ------------------------------------------------------------------ file reading
+// Reads one file's cas message into staged + e.msg_offset exactly as generate_cas_id reads
+// it (cas.rs:25-58) and zero-pads it to the next 64-byte boundary.  Returns an
+// sd_file_status:
+//   whole kind: every byte read() returns until EOF (fs::read, cas.rs:29); e.msg_len is
+//     set to 8 + that count.  SD_FILE_CHANGED if the file holds more bytes than the
+//     extent's planned room (e.msg_len - 8 on entry): the reference would hash them all.
+//   sampled kind: read_exact of the head and the samples at their traced offsets
+//     (SHORT_READ past EOF), then the footer at seek(End(-8192)) -- the file's real end,
+//     EINVAL when it is shorter than 8192 bytes.
+int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged);
+
+// A message read front to back from a file: optional le64 prefix (a cas message's size
+// header), optional bytes already read from the file, then the file itself.
+class MsgSource {
+public:
+    enum Mode {
+        READ_TO_EOF,     // fs::read (cas.rs:29): read() until it returns 0
+        CHECKSUM_READS,  // hash.rs:14-20: one read() of 1 MiB per call until one returns fewer
+    };
+    static constexpr uint64_t CHECKSUM_READ = SD_CK_BLOCK;
+    MsgSource(int fd, Mode m) : fd_(fd), mode_(m) {}
+    void set_prefix_le64(uint64_t v);
+    // bytes already taken from the file (whole 1 MiB reads in CHECKSUM_READS mode)
+    void set_pending(const uint8_t* p, uint64_t n) {
+        pend_ = p;
+        pend_len_ = n;
+    }
+    // Writes up to n message bytes to dst and returns the count; fewer than n only at the
+    // end of the message (done) or on an error (err = errno).  CHECKSUM_READS: n is a
+    // multiple of 1 MiB.
+    uint64_t read(uint8_t* dst, uint64_t n);
+    bool done = false;
+    int err = 0;
+
+private:
+    int fd_;
+    Mode mode_;
+    uint8_t prefix_[8] = {};
+    uint32_t prefix_len_ = 0, prefix_pos_ = 0;
+    const uint8_t* pend_ = nullptr;
+    uint64_t pend_len_ = 0;
+};
+
+// ------------------------------------------------------------------ CPU BLAKE3 (cpu_blake3.cpp)
+// The library's own CPU hasher: the BLAKE3 spec's incremental chunk / CV-stack structure,
+// with whole chunks hashed many at a time across SIMD lanes (AVX-512 16-way, AVX2 8-way,
+// portable 1-way, picked at run time).  Used by the sd_cpu_* entry points and the
+// latency path's CPU route.
+class CpuHasher {
+public:
+    CpuHasher();
+    void update(const uint8_t* p, size_t n);
+    void finalize(uint8_t out[32]) const;
+
+private:
+    void push_chunk_cv(const uint32_t cv[8]);
+    uint32_t stack_[56][8];
+    int sp_ = 0;
+    uint64_t chunks_ = 0;  // complete chunks pushed so far
+    uint8_t buf_[1024];
+    uint32_t buf_len_ = 0;
+};
+void cpu_blake3(const uint8_t* p, size_t n, uint8_t out[32]);
+// lanes of the SIMD chunk hasher this CPU runs (16, 8 or 1)
+int cpu_lanes();
+// generate_cas_id / file_checksum of one file on the calling thread -> sd_file_status
+int32_t cpu_cas_id_file(const char* path, uint64_t size, char out_hex17[17]);
+int32_t cpu_checksum_file(const char* path, char out_hex65[65]);
+void hex_lower(const uint8_t* h, int nbytes, char* out);

@@ -1,6 +1,6 @@
 """The C ABI boundary on a machine without a GPU: the library loads, exports exactly what
-include/sd_cas.h declares, its host-only planning works, and compute entry points fail
-loudly (no CPU fallback)."""
+include/sd_cas.h declares, its host-only planning works, and the GPU entry points fail
+loudly without a device (the CPU path is the separate, explicit sd_cpu_* family)."""
 import ctypes
 import os
 import re
@@ -42,7 +42,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_binds():
     L = lib()
-    assert L.sd_cas_abi_version() == 1
+    assert L.sd_cas_abi_version() == 2
     for name, _, _ in _native.SIGNATURES:
         assert getattr(L, name) is not None
 
@@ -93,7 +93,7 @@ def test_stage_file_errors(tmp_path):
                                   ctypes.c_void_p(staged.ctypes.data), ctypes.byref(st)))
     assert st.value & 0xFFFF == _native.SD_FILE_IO_ERROR and (st.value >> 16) == 2  # ENOENT
     short = tmp_path / "short"
-    short.write_bytes(b"x" * 150000)  # shorter than the planned 200000: read_exact EOF
+    short.write_bytes(b"x" * 150000)  # planned 200000: the last sample (145904..156144) runs past EOF
     check(lib().sd_cas_stage_file(os.fsencode(short), ctypes.c_void_p(ext.ctypes.data),
                                   ctypes.c_void_p(staged.ctypes.data), ctypes.byref(st)))
     assert st.value == _native.SD_FILE_SHORT_READ
@@ -105,11 +105,16 @@ def test_invalid_arguments_do_not_cross_boundary():
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="GPU present")
-def test_no_cpu_fallback_without_gpu():
+def test_gpu_entry_points_fail_without_a_device():
     h = ctypes.c_void_p()
     with pytest.raises(SdCasError) as e:
         check(lib().sd_cas_ctx_create(0, ctypes.byref(h)))
     assert e.value.rc == -2
+
+
+def test_unknown_tuning_key_is_rejected():
+    assert lib().sd_cas_set_tuning(b"whole_variant", 3) == -1  # the A/B kernel variants are gone
+    assert lib().sd_cas_set_tuning(b"files_window_mb", 32) == 0
 
 
 def test_stage_files_threaded_equals_single(tmp_path):
@@ -137,10 +142,13 @@ def test_stage_files_threaded_equals_single(tmp_path):
     st_b = np.full(len(sizes), -7, np.int32)
     check(lib().sd_cas_stage_files(arr, ext.ctypes.data, len(paths), b.ctypes.data, st_b.ctypes.data, 8))
     assert list(st_a) == list(st_b)
-    assert st_b[7] == _native.SD_FILE_SHORT_READ and (st_b[8] & 0xFFFF) == _native.SD_FILE_IO_ERROR
-    for i in range(7):
+    # file 7 is 140000 B planned as 150000: every sample fits and the tail is read at the
+    # file's real end (SeekFrom::End, cas.rs:54) -- the reference returns an id
+    assert st_b[7] == _native.SD_FILE_OK and (st_b[8] & 0xFFFF) == _native.SD_FILE_IO_ERROR
+    for i in range(8):
         o, L = int(ext["msg_offset"][i]), int(ext["msg_len"][i])
-        assert a[o:o + L].tobytes() == b[o:o + L].tobytes() == cs.cas_message(cs.synth_reader(70 + i), sizes[i])
+        content = cs.synth_bytes(70 + i, 0, 0, sizes[i] if i != 7 else 140000)
+        assert a[o:o + L].tobytes() == b[o:o + L].tobytes() == cs.cas_message_file(content, sizes[i])
 
 
 def _header_param_counts():

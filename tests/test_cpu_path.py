@@ -1,0 +1,184 @@
+"""The library's CPU path (libsdcas.so sd_cpu_*, no device) and its GPU-free host logic
+(the stager, the sequential reader) against the oracle: the reference's read semantics
+for files whose length differs from the size argument (cas.rs:23-62), hash.rs's read
+loop, the goldens, and every SIMD width the host has."""
+import ctypes
+import os
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import blake3_spec as b3
+from oracle import cas_spec as cs
+from spacedrive_amd import cpu
+from spacedrive_amd._native import SD_FILE_CHANGED, SD_FILE_OK, SD_FILE_SHORT_READ, check, lib
+from spacedrive_amd.cas import UnexpectedEofError
+from spacedrive_amd.device import stage_plan
+from tests.test_oracle import LENGTH_MISMATCH_CASES
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def pat(n):
+    return bytes(i % 251 for i in range(n))
+
+
+def test_cpu_blake3_official_vectors(golden):
+    for n, h in golden["blake3_official"]["hash"].items():
+        assert cpu.blake3(pat(int(n))).hex() == h, n
+
+
+def test_cpu_blake3_vs_oracle_sizes(oracle_native):
+    rng = np.random.default_rng(3)
+    for n in [0, 1, 63, 64, 65, 1023, 1024, 1025, 2047, 2048, 2049, 16 * 1024, 16 * 1024 + 1, 17 * 1024,
+              33 * 1024 + 5, 57352, 102408, 1 << 20, (1 << 20) + 1, 3 * (1 << 20) + 777]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert cpu.blake3(d) == oracle_native.blake3(d), n
+
+
+@pytest.mark.parametrize("lanes", [4, 8, 16])
+def test_cpu_simd_widths(lanes):
+    """Each chunk-lane width (SSE2 4, AVX2 8, AVX-512 16) the host supports, in a child
+    process (the width is picked once per process)."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from spacedrive_amd import cpu\n"
+            "from oracle import native\n"
+            "import numpy as np\n"
+            "print(cpu.simd_lanes())\n"
+            "rng = np.random.default_rng(9)\n"
+            "for n in [0, 1025, 4096, 16 * 1024 + 3, 40000, 57352, 300001]:\n"
+            "    d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()\n"
+            "    assert cpu.blake3(d) == native.blake3(d), n\n") % ROOT
+    env = dict(os.environ, SD_CPU_LANES=str(lanes))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = int(r.stdout.split()[0])
+    assert got <= lanes
+    if got < lanes:
+        pytest.skip(f"host CPU runs {got} lanes at most")
+
+
+def test_cpu_cas_ids_staged_goldens(golden, oracle_native):
+    files = golden["cas_synth"]["files"]
+    sizes = np.array([f["size"] for f in files], np.uint64)
+    cids = np.array([f["content_id"] for f in files], np.uint64)
+    twins = np.array([f["twin"] for f in files], np.uint32)
+    ext, total = stage_plan(sizes)
+    buf = oracle_native.stage_synth(sizes, cids, twins, ext["msg_offset"], total)
+    got = cpu.cas_ids_staged(buf, ext)
+    assert got == [f["cas_id"] for f in files]
+
+
+def _write(tmp_path, name, content):
+    p = tmp_path / name
+    p.write_bytes(content)
+    return str(p)
+
+
+def test_cpu_cas_ids_files_length_mismatch(tmp_path, oracle_native):
+    """cas.rs with stale sizes (SURVEY.md §3 CS4/CS5 callers pass metadata that may lag the
+    file): every case of tests/test_oracle.py, batched and single-file, equals the oracle's
+    read schedule."""
+    paths, sizes, contents = [], [], []
+    for i, (flen, size) in enumerate(LENGTH_MISMATCH_CASES):
+        content = cs.synth_bytes(900 + i, 0, 0, flen)
+        paths.append(_write(tmp_path, f"m{i}", content))
+        sizes.append(size)
+        contents.append(content)
+    paths.append(str(tmp_path / "missing"))
+    sizes.append(10)
+    want, wst = oracle_native.cas_ids_files(paths, np.array(sizes, np.uint64), nthreads=2)
+    got = cpu.generate_cas_ids(paths, sizes, nthreads=4)
+    for i in range(len(paths)):
+        if wst[i] == 0:
+            assert got[i] == want[i].tobytes().hex(), (i, LENGTH_MISMATCH_CASES[i])
+            assert cpu.generate_cas_id(paths[i], sizes[i]) == got[i]
+        elif wst[i] == SD_FILE_SHORT_READ:
+            assert isinstance(got[i], UnexpectedEofError), i
+        else:
+            assert isinstance(got[i], FileNotFoundError), i
+    assert wst[-1] != 0 and (wst[:-1] == 3).sum() == 2  # two UnexpectedEof cases, one ENOENT
+
+
+def test_cpu_file_checksums_vs_oracle(tmp_path, oracle_native):
+    MiB = 1 << 20
+    sizes = [0, 1, 1024, 1025, MiB - 1, MiB, MiB + 1, 2 * MiB, 5 * MiB + 77]
+    paths = [_write(tmp_path, f"c{i}", oracle_native.synth_bytes(50 + i, 0, 0, s)) for i, s in enumerate(sizes)]
+    paths.insert(3, str(tmp_path / "nope"))
+    want, wst = oracle_native.file_checksums(paths, nthreads=2)
+    got = cpu.file_checksums(paths, nthreads=3)
+    assert isinstance(got[3], FileNotFoundError) and wst[3] != 0
+    for i in range(len(paths)):
+        if i != 3:
+            assert wst[i] == 0 and got[i] == want[i].tobytes().hex(), i
+            assert cpu.file_checksum(paths[i]) == got[i]
+
+
+def test_cpu_file_checksum_of_a_pipe(tmp_path):
+    """hash.rs stops at the first short read: a FIFO (st_size 0) hashes what one read returns."""
+    fifo = str(tmp_path / "fifo")
+    os.mkfifo(fifo)
+    payload = cs.synth_bytes(98, 0, 0, 4000)
+
+    def writer():
+        with open(fifo, "wb", buffering=0) as f:
+            f.write(payload)
+
+    t = threading.Thread(target=writer)
+    t.start()
+    got = cpu.file_checksum(fifo)
+    t.join()
+    assert got == b3.blake3(payload).hex()
+
+
+# -------------------------------------------------------------- the staging ABI (host only)
+def _stage(path, ext_row, staged):
+    st = ctypes.c_int32(-1)
+    check(lib().sd_cas_stage_file(os.fsencode(path), ctypes.c_void_p(ext_row), ctypes.c_void_p(staged.ctypes.data),
+                                  ctypes.byref(st)))
+    return st.value
+
+
+def test_stage_file_length_mismatch(tmp_path):
+    """sd_cas_stage_file: a whole-kind extent is in/out (msg_len = 8 + the bytes read);
+    a file longer than the extent's room reports SD_FILE_CHANGED; a sampled file's tail
+    comes from its real end."""
+    for i, (flen, size) in enumerate(LENGTH_MISMATCH_CASES):
+        content = cs.synth_bytes(900 + i, 0, 0, flen)
+        p = _write(tmp_path, f"s{i}", content)
+        ext, total = stage_plan(np.array([size], np.uint64))
+        staged = np.full(total + 64, 0xAB, np.uint8)
+        st = _stage(p, ext.ctypes.data, staged)
+        try:
+            msg = cs.cas_message_file(content, size)
+        except cs.UnexpectedEof:
+            assert st == SD_FILE_SHORT_READ, i
+            continue
+        if size <= 102400 and flen > size:
+            assert st == SD_FILE_CHANGED, i
+            continue
+        assert st == SD_FILE_OK, i
+        assert int(ext["msg_len"][0]) == len(msg), i
+        assert staged[:len(msg)].tobytes() == msg, i
+        pad = (len(msg) + 63) // 64 * 64
+        assert not staged[len(msg):pad].any(), i
+
+
+def test_cpu_cas_ids_on_restaged_shorter_files(tmp_path):
+    """Shorter whole files staged with their planned extents, then hashed with the
+    updated extents: equals the reference's fs::read message."""
+    sizes = [100, 5000, 102400]
+    flens = [10, 4000, 70000]
+    paths = [_write(tmp_path, f"r{i}", cs.synth_bytes(60 + i, 0, 0, flens[i])) for i in range(3)]
+    ext, total = stage_plan(np.array(sizes, np.uint64))
+    staged = np.zeros(total + 64, np.uint8)
+    arr = (ctypes.c_char_p * 3)(*[os.fsencode(p) for p in paths])
+    status = np.full(3, -1, np.int32)
+    check(lib().sd_cas_stage_files(arr, ext.ctypes.data, 3, staged.ctypes.data, status.ctypes.data, 2))
+    assert (status == 0).all()
+    got = cpu.cas_ids_staged(staged, ext)
+    for i in range(3):
+        assert got[i] == cs.generate_cas_id_file(cs.synth_bytes(60 + i, 0, 0, flens[i]), sizes[i])

@@ -206,9 +206,104 @@ def test_c_oracle_file_backed_reads(oracle_native, tmp_path):
         got, st = oracle_native.cas_ids_files(paths, sizes, nthreads=nt, simd=simd)
         assert (st == 0).all(), st
         assert np.array_equal(got, want)
-    got, st = oracle_native.cas_ids_files([str(tmp_path / "missing"), paths[5]], [10, 555555 + 9000])
+    got, st = oracle_native.cas_ids_files([str(tmp_path / "missing"), paths[5], paths[5]],
+                                          [10, 555555 + 500000, 555555 + 9000])
     assert st[0] & 0xFFFF == 2 and st[0] >> 16 == 2  # ENOENT
-    assert st[1] == 3  # read_exact past EOF
+    assert st[1] == 3  # the last sample's read_exact runs past EOF
+    # planned 9000 B too large, but every sample still fits and the footer is read at the
+    # file's real end (SeekFrom::End, cas.rs:54): the reference returns an id
+    assert st[2] == 0
+    content = open(paths[5], "rb").read()
+    assert got[2].tobytes().hex() == oracle_native.blake3(cs.cas_message_file(content, 555555 + 9000))[:8].hex()
+
+
+# (file length, size passed to generate_cas_id) pairs whose lengths differ, and the
+# reference's outcome: the hashed stream (cas_spec.cas_message_file) or its error
+LENGTH_MISMATCH_CASES = [
+    (5000, 9000),               # whole kind, file shorter than size: fs::read hashes the 5000 bytes
+    (9000, 5000),               # whole kind, file longer than size
+    (150_000, 1000),            # whole kind, file longer than 100 KiB (message > 102408 B)
+    (3 << 20, 100),             # whole kind, message far beyond the whole-file kernels' 128 chunks
+    (777, 0),                   # size 0 (non_indexed.rs:168 passes it): le64(0) || the bytes
+    (700_000, 300_000),         # sampled, file longer than size: footer at the real EOF
+    (700_000, 900_000),         # sampled, file shorter than size, every sample still fits
+    (700_000, 1_600_000),       # sampled, a sample runs past EOF: UnexpectedEof
+    (5000, 200_000),            # sampled, the header runs past EOF: UnexpectedEof
+]
+
+
+def test_c_oracle_length_differs_from_size(oracle_native, tmp_path):
+    """cas.rs on files whose length differs from the size argument: the C restatement's
+    read schedule (fs::read to EOF; read_exact; seek(End(-8192))) == the Python
+    statement, scalar and SIMD."""
+    paths, sizes, want = [], [], []
+    for i, (flen, size) in enumerate(LENGTH_MISMATCH_CASES):
+        content = cs.synth_bytes(900 + i, 0, 0, flen)
+        p = tmp_path / f"m{i}"
+        p.write_bytes(content)
+        paths.append(str(p))
+        sizes.append(size)
+        try:
+            want.append(oracle_native.blake3(cs.cas_message_file(content, size))[:8].hex())
+        except cs.UnexpectedEof:
+            want.append(3)
+    for simd in (0, -1):
+        got, st = oracle_native.cas_ids_files(paths, np.array(sizes, np.uint64), nthreads=2, simd=simd)
+        for i, w in enumerate(want):
+            if w == 3:
+                assert st[i] == 3, i
+            else:
+                assert st[i] == 0 and got[i].tobytes().hex() == w, (i, LENGTH_MISMATCH_CASES[i])
+    # the Python statement itself on small cases, against the pure-Python spec
+    content = cs.synth_bytes(5, 0, 0, 3000)
+    assert cs.generate_cas_id_file(content, 2000) == b3.blake3(b"\xd0\x07" + bytes(6) + content).hex()[:16]
+    with pytest.raises(cs.UnexpectedEof):  # the header fits, the second sample (at 54096) does not
+        cs.cas_message_file(bytes(20000), 200_000)
+    with pytest.raises(cs.UnexpectedEof):
+        cs.cas_message_file(bytes(8000), 200_000)
+
+
+def test_c_oracle_file_checksum_read_schedule(oracle_native, tmp_path):
+    """hash.rs:10-24 from files: 1 MiB read calls until a short one, hashed through a CV
+    stack of 1 MiB subtrees (scalar and SIMD) == the one-shot hash of the whole file."""
+    MiB = 1 << 20
+    sizes = [0, 1, 1024, 1025, MiB - 1, MiB, MiB + 1, 2 * MiB, 3 * MiB + 5, 4 * MiB, 5 * MiB + 77, 8 * MiB + 1]
+    paths, datas = [], []
+    for i, s in enumerate(sizes):
+        d = np.frombuffer(cs.synth_bytes(70 + i, 0, 0, s) if s < 64 else
+                          oracle_native.synth_bytes(70 + i, 0, 0, s), np.uint8)
+        p = tmp_path / f"k{i}"
+        p.write_bytes(d.tobytes())
+        paths.append(str(p))
+        datas.append(d)
+    paths.append(str(tmp_path / "missing"))
+    for simd in (0, -1):
+        got, st = oracle_native.file_checksums(paths, nthreads=3, simd=simd)
+        assert st[-1] & 0xFFFF == 2 and st[-1] >> 16 == 2
+        for i, d in enumerate(datas):
+            buf = np.concatenate([d, np.zeros(64, np.uint8)])
+            assert st[i] == 0
+            assert got[i].tobytes() == oracle_native.checksums(buf, [0], [len(d)])[0].tobytes(), sizes[i]
+
+
+def test_c_oracle_file_checksum_short_read_of_a_pipe(oracle_native, tmp_path):
+    """A FIFO reports st_size 0; hash.rs hashes what its first read returns and stops at
+    that short read.  One atomic write of 4000 bytes (< PIPE_BUF) makes it deterministic."""
+    import os
+    import threading
+    fifo = str(tmp_path / "fifo")
+    os.mkfifo(fifo)
+    payload = cs.synth_bytes(99, 0, 0, 4000)
+
+    def writer():
+        with open(fifo, "wb", buffering=0) as f:
+            f.write(payload)
+
+    t = threading.Thread(target=writer)
+    t.start()
+    got, st = oracle_native.file_checksums([fifo], nthreads=1, simd=0)
+    t.join()
+    assert st[0] == 0 and got[0].tobytes() == b3.blake3(payload)
 
 
 def test_c_oracle_checksum_mt_equals_streaming(oracle_native):
