@@ -66,7 +66,9 @@ typedef enum sd_rc {
     SD_ERR_DEVICE = -2,   /* HIP / device error, or no gfx950 device */
     SD_ERR_NOMEM = -3,    /* device or pinned-host allocation failed */
     SD_ERR_INTERNAL = -4, /* unexpected exception caught at the boundary */
-    SD_ERR_COMM = -5      /* collective (RCCL) failure */
+    SD_ERR_COMM = -5,     /* collective (RCCL) failure */
+    SD_ERR_CAPACITY = -6  /* sd_cas_dedup_mgpu: some rank's output capacity is too small (every
+                             rank returns it, before the exchange; *m_out = own requirement) */
 } sd_rc;
 
 /* per-file status, mapped back to io::ErrorKind by the Rust shim */
@@ -174,6 +176,13 @@ int sd_checksum_batch_run(sd_cas_ctx* ctx, const sd_checksum_batch* batch, const
                           uint8_t* d_hash32, void* stream);
 /* [0] files, [1] total bytes, [2] BLAKE3 compressions, [3] 1 MiB leaf blocks */
 int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
+/* Drop-in over host memory (pinned or pageable; hash.rs:10-24 on data already read):
+ * full BLAKE3 of n byte ranges of `data` -> 65-byte hex each.  Ranges start 16-byte
+ * aligned and `data` is readable up to the next 64-byte boundary after each.  Consecutive
+ * ranges are copied 256 MiB window at a time, larger ranges stream; two windows alternate
+ * so the H2D copies overlap the kernels. */
+int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
+                 char* out_hex65);
 /* Drop-in: checksums of n files on disk -> 65-byte lowercase hex each (hash.rs:21-23);
  * status[n] required.  Each file is read as hash.rs reads it (1 MiB read calls until a
  * short one); small files are packed many per pinned window, large ones (or ones that
@@ -246,6 +255,32 @@ int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, int flags, 
  * step links to it).  Asynchronous on `stream`; no host sync. */
 int sd_dedup_owners(sd_cas_ctx* ctx, const uint64_t* d_records, uint64_t m, const uint64_t* d_rep,
                     uint64_t chunk_size, uint64_t* d_owner, void* stream);
+
+/* ---------------------------------------------------------------- multi-GPU dedup (RCCL) */
+/* One process (or thread) per GPU, files sharded by global index.  The
+ * communicator is RCCL's: rank 0 calls sd_comm_id (ncclGetUniqueId) and hands the 128
+ * bytes to every rank out of band; each rank calls sd_comm_create (ncclCommInitRank,
+ * collective) on its context's device. */
+#define SD_COMM_ID_BYTES 128
+typedef struct sd_comm sd_comm;
+int sd_comm_id(uint8_t* out_id /* SD_COMM_ID_BYTES */);
+int sd_comm_create(sd_cas_ctx* ctx, const uint8_t* id, int nranks, int rank, sd_comm** out);
+void sd_comm_destroy(sd_comm* comm);
+/* The whole post-hash step of one rank, collective over the communicator: partition its n
+ * records by cas_id prefix (sd_dedup_partition), all-gather the count matrix and the
+ * shards' index ranges (ncclAllGather), exchange the 16-byte records with grouped
+ * ncclSend / ncclRecv -- the all-to-all over xGMI --, then group the records this rank
+ * receives (sd_dedup_group; index order is exploited when the shards' ranges ascend with
+ * the rank) and assign their Objects (sd_dedup_owners, identifier steps of chunk_size).
+ * Outputs hold `capacity` entries: d_records_out 2 x u64 each (sorted by (cas_id,
+ * index)), d_rep_out and d_owner_out u64 each; *m_out = the records this rank owns,
+ * *n_groups_out = its groups.  If any rank's capacity is too small, every rank returns
+ * SD_ERR_CAPACITY before the record exchange, with *m_out = its own requirement.  Runs on
+ * `stream`; returns after the group counts are known (host sync). */
+int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, const uint8_t* d_valid, uint64_t n,
+                      uint64_t global_index_base, uint64_t chunk_size, uint64_t* d_records_out, uint64_t* d_rep_out,
+                      uint64_t* d_owner_out, uint64_t capacity, uint64_t* m_out, uint64_t* n_groups_out,
+                      void* stream);
 
 /* ---------------------------------------------------------------- synthetic data */
 /* Device generator of SURVEY.md §8(d) (seed 0x5D5DCA51D, splitmix64 counter stream),

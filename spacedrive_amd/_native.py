@@ -21,7 +21,8 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "sd_cas.h")
 
 SD_OK = 0
 RC_NAMES = {0: "SD_OK", -1: "SD_ERR_INVALID", -2: "SD_ERR_DEVICE", -3: "SD_ERR_NOMEM",
-            -4: "SD_ERR_INTERNAL", -5: "SD_ERR_COMM"}
+            -4: "SD_ERR_INTERNAL", -5: "SD_ERR_COMM", -6: "SD_ERR_CAPACITY"}
+SD_ERR_CAPACITY = -6
 SD_FILE_OK, SD_FILE_SKIPPED_EMPTY, SD_FILE_IO_ERROR, SD_FILE_SHORT_READ, SD_FILE_CHANGED = 0, 1, 2, 3, 4
 SD_KIND_WHOLE, SD_KIND_SAMPLED = 1, 2
 SAMPLED_MSG_LEN = 57352
@@ -71,6 +72,7 @@ SIGNATURES = [
     ("sd_checksum_batch_run", I32, [P, P, P, P, P]),
     ("sd_checksum_batch_stats", I32, [P, P]),
     ("sd_file_checksums", I32, [P, P, SZ, P, P]),
+    ("sd_checksums", I32, [P, P, P, P, SZ, P]),
     ("sd_cas_id_path", I32, [P, ctypes.c_char_p, U64, P, ctypes.POINTER(ctypes.c_int32)]),
     ("sd_file_checksum_path", I32, [P, ctypes.c_char_p, P, ctypes.POINTER(ctypes.c_int32)]),
     ("sd_coalescer_stats", I32, [P, P]),
@@ -84,6 +86,10 @@ SIGNATURES = [
     ("sd_dedup_partition", I32, [P, P, P, U64, U64, I32, P, P, PU64, P]),
     ("sd_dedup_group", I32, [P, P, U64, I32, P, PU64, P]),
     ("sd_dedup_owners", I32, [P, P, U64, P, U64, P, P]),
+    ("sd_comm_id", I32, [P]),
+    ("sd_comm_create", I32, [P, P, I32, I32, ctypes.POINTER(P)]),
+    ("sd_comm_destroy", None, [P]),
+    ("sd_cas_dedup_mgpu", I32, [P, P, P, P, U64, U64, U64, P, P, P, U64, PU64, PU64, P]),
     ("sd_synth_stage_cas", I32, [P, P, P, P, P, SZ, P, P]),
     ("sd_synth_fill", I32, [P, U64, U32, U64, P, P]),
     ("sd_device_malloc", I32, [P, U64, ctypes.POINTER(P)]),

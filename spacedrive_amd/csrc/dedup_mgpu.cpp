@@ -1,0 +1,196 @@
+// dedup_mgpu.cpp -- the multi-GPU post-hash step behind the C ABI.
+//
+// Reference semantics: identifier_job_step links every file_path to the Object that owns
+// an equal cas_id, creating Objects otherwise (core/src/object/file_identifier/mod.rs:
+// 136-333).  With the library sharded by file index over one process per GPU, the only
+// exchange is the one that brings equal cas_ids together: each rank partitions its
+// records (cas_id as big-endian u64, global index) by cas_id prefix into contiguous
+// destination ranges, and an all-to-all over RCCL (xGMI on MI355X) delivers every record
+// to the rank that owns its prefix range, which groups and assigns Objects locally.
+//
+// One call per rank, all on the caller's stream:
+//   1. sd_dedup_partition: stable partition by destination, per-destination counts;
+//   2. ncclAllGather of one row per rank -- its counts, index range and output capacity --
+//      so every rank knows the whole count matrix: the receive sizes, a capacity check
+//      that every rank evaluates identically (so an undersized rank makes all ranks
+//      return before the record exchange rather than leave peers hanging), and whether
+//      the shards' index ranges ascend with the rank (the received records are then in
+//      index order, and the grouping skips one sort);
+//   3. grouped ncclSend / ncclRecv of the 16-byte records (one pair per peer, self
+//      included), the all-to-all;
+//   4. sd_dedup_group + sd_dedup_owners on the received records.
+// A Rust host drives this through sd_comm_id (ncclGetUniqueId on one rank, the 128 bytes
+// passed to the others out of band) and sd_comm_create (ncclCommInitRank).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "sd_internal.h"
+
+struct sd_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 0, rank = 0, device = 0;
+    // device scratch, grown on demand: counts[nranks], the partitioned send records, the
+    // all-gather rows (send row + nranks rows)
+    void* d_counts = nullptr;
+    void* d_send = nullptr;
+    size_t send_bytes = 0;
+    void* d_rows = nullptr;
+    uint64_t* h_rows = nullptr;  // pinned
+    ~sd_comm() {
+        if (d_counts) (void)hipFree(d_counts);
+        if (d_send) (void)hipFree(d_send);
+        if (d_rows) (void)hipFree(d_rows);
+        if (h_rows) (void)hipHostFree(h_rows);
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+};
+
+namespace {
+
+#define HIP_OK(expr)                                                                                    \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess)                                                                           \
+            throw sd_failure(e_ == hipErrorOutOfMemory ? SD_ERR_NOMEM : SD_ERR_DEVICE,                 \
+                             std::string(#expr) + ": " + hipGetErrorString(e_));                       \
+    } while (0)
+
+#define NCCL_OK(expr)                                                                                   \
+    do {                                                                                                \
+        ncclResult_t r_ = (expr);                                                                       \
+        if (r_ != ncclSuccess) throw sd_failure(SD_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+void check_rc(int rc) {
+    if (rc != SD_OK) throw sd_failure(rc, sd_cas_last_error());
+}
+
+// row layout of the all-gather: counts[nranks], index base, local file count, capacity
+constexpr int ROW_EXTRA = 3;
+
+}  // namespace
+
+extern "C" {
+
+int sd_comm_id(uint8_t* out_id) {
+    SD_GUARD_BEGIN
+    if (!out_id) throw sd_failure(SD_ERR_INVALID, "null argument");
+    static_assert(sizeof(ncclUniqueId) == SD_COMM_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    NCCL_OK(ncclGetUniqueId(&id));
+    memcpy(out_id, &id, SD_COMM_ID_BYTES);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_comm_create(sd_cas_ctx* ctx, const uint8_t* id, int nranks, int rank, sd_comm** out) {
+    SD_GUARD_BEGIN
+    if (!ctx || !id || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks)
+        throw sd_failure(SD_ERR_INVALID, "rank / nranks out of range (1..64 ranks)");
+    *out = nullptr;
+    auto c = std::make_unique<sd_comm>();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = sd_ctx_device(ctx);
+    HIP_OK(hipSetDevice(c->device));
+    ncclUniqueId uid;
+    memcpy(&uid, id, SD_COMM_ID_BYTES);
+    NCCL_OK(ncclCommInitRank(&c->comm, nranks, uid, rank));
+    const size_t row = (size_t)nranks + ROW_EXTRA;
+    HIP_OK(hipMalloc(&c->d_counts, sizeof(uint64_t) * nranks));
+    HIP_OK(hipMalloc(&c->d_rows, sizeof(uint64_t) * row * (nranks + 1)));
+    HIP_OK(hipHostMalloc((void**)&c->h_rows, sizeof(uint64_t) * row * (nranks + 1), hipHostMallocDefault));
+    *out = c.release();
+    return SD_OK;
+    SD_GUARD_END
+}
+
+void sd_comm_destroy(sd_comm* comm) {
+    try {
+        if (comm) (void)hipSetDevice(comm->device);
+        delete comm;
+    } catch (...) {
+    }
+}
+
+int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, const uint8_t* d_valid, uint64_t n,
+                      uint64_t global_index_base, uint64_t chunk_size, uint64_t* d_records_out, uint64_t* d_rep_out,
+                      uint64_t* d_owner_out, uint64_t capacity, uint64_t* m_out, uint64_t* n_groups_out,
+                      void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || !comm || !m_out || !n_groups_out || (n && !d_hash32) ||
+        (capacity && (!d_records_out || !d_rep_out || !d_owner_out)))
+        throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (chunk_size == 0) throw sd_failure(SD_ERR_INVALID, "chunk_size must be positive");
+    HIP_OK(hipSetDevice(comm->device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int R = comm->nranks, me = comm->rank;
+    const size_t row = (size_t)R + ROW_EXTRA;
+    // 1. partition this rank's records by destination rank
+    if (comm->send_bytes < 16 * n || !comm->d_send) {
+        if (comm->d_send) HIP_OK(hipFree(comm->d_send));
+        comm->d_send = nullptr;
+        comm->send_bytes = 16 * (n ? n : 1);
+        HIP_OK(hipMalloc(&comm->d_send, comm->send_bytes));
+    }
+    uint64_t n_valid = 0;
+    check_rc(sd_dedup_partition(ctx, d_hash32, d_valid, n, global_index_base, R, (uint64_t*)comm->d_counts,
+                                (uint64_t*)comm->d_send, &n_valid, stream));
+    // 2. all-gather of (counts, index base, file count, capacity)
+    uint64_t* h_row = comm->h_rows;
+    h_row[R] = global_index_base;
+    h_row[R + 1] = n;
+    h_row[R + 2] = capacity;
+    uint64_t* d_row = (uint64_t*)comm->d_rows;
+    uint64_t* d_all = d_row + row;
+    HIP_OK(hipMemcpyAsync(d_row, comm->d_counts, sizeof(uint64_t) * R, hipMemcpyDeviceToDevice, s));
+    HIP_OK(hipMemcpyAsync(d_row + R, h_row + R, sizeof(uint64_t) * ROW_EXTRA, hipMemcpyHostToDevice, s));
+    NCCL_OK(ncclAllGather(d_row, d_all, row, ncclUint64, comm->comm, s));
+    uint64_t* all = comm->h_rows + row;
+    HIP_OK(hipMemcpyAsync(all, d_all, sizeof(uint64_t) * row * R, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    auto cnt = [&](int src, int dst) { return all[(size_t)src * row + dst]; };
+    std::vector<uint64_t> recv_total(R, 0);
+    for (int src = 0; src < R; src++)
+        for (int dst = 0; dst < R; dst++) recv_total[dst] += cnt(src, dst);
+    bool fits = true, ascending = true;
+    for (int r = 0; r < R; r++) {
+        if (recv_total[r] > all[(size_t)r * row + R + 2]) fits = false;
+        if (r + 1 < R && all[(size_t)r * row + R] + all[(size_t)r * row + R + 1] > all[(size_t)(r + 1) * row + R])
+            ascending = false;
+    }
+    *m_out = recv_total[me];
+    *n_groups_out = 0;
+    if (!fits)  // every rank sees the same matrix, so every rank stops here
+        throw sd_failure(SD_ERR_CAPACITY, "an output capacity is smaller than the records its rank receives "
+                                         "(*m_out = this rank's requirement)");
+    // 3. the all-to-all of the 16-byte records: one send and one receive per peer
+    const uint64_t* send = (const uint64_t*)comm->d_send;
+    uint64_t soff = 0, roff = 0;
+    NCCL_OK(ncclGroupStart());
+    for (int p = 0; p < R; p++) {
+        const uint64_t sc = cnt(me, p), rc = cnt(p, me);
+        if (sc) NCCL_OK(ncclSend(send + 2 * soff, 2 * sc, ncclUint64, p, comm->comm, s));
+        if (rc) NCCL_OK(ncclRecv(d_records_out + 2 * roff, 2 * rc, ncclUint64, p, comm->comm, s));
+        soff += sc;
+        roff += rc;
+    }
+    NCCL_OK(ncclGroupEnd());
+    if (soff != n_valid) throw sd_failure(SD_ERR_INTERNAL, "partition counts disagree with the valid records");
+    // 4. group by cas_id and assign Objects (chunk-of-100 rule) on the received records
+    uint64_t ng = 0;
+    check_rc(sd_dedup_group(ctx, d_records_out, *m_out, ascending ? SD_DEDUP_INDEX_SORTED : 0, d_rep_out, &ng,
+                            stream));
+    check_rc(sd_dedup_owners(ctx, d_records_out, *m_out, d_rep_out, chunk_size, d_owner_out, stream));
+    *n_groups_out = ng;
+    return SD_OK;
+    SD_GUARD_END
+}
+
+}  // extern "C"

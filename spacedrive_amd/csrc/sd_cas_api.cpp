@@ -442,6 +442,8 @@ int32_t cas_overflow(SlotPair& sl, int& cur, Streamer& st, const char* path, uin
 
 }  // namespace
 
+int sd_ctx_device(const sd_cas_ctx* ctx) { return ctx->device; }
+
 // ------------------------------------------------------------------ tuning knobs
 // defaults: 200 us coalescing window, 4096-request batches, 32 MiB file windows, LDS-bucket
 // dedup grouping, single-file calls on the CPU while fewer than 16 are in flight
@@ -959,6 +961,97 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
         pack_end = align_up(off0 + got, 64);
     }
     submit_pack();
+    harvest(0);
+    harvest(1);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+// Full BLAKE3 of n byte ranges of a host buffer (hash.rs:10-24 on data already in memory):
+// consecutive ranges whose span fits a 256 MiB window are copied with one H2D each and
+// hashed as one batch; a larger range streams window by window into its leaf CVs (known
+// length: one plan), then reduces.  Two slots alternate so copies overlap kernels.
+int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
+                 char* out_hex65) {
+    SD_GUARD_BEGIN
+    if (!ctx || (n && (!data || !offsets || !lens || !out_hex65))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    for (size_t i = 0; i < n; i++)
+        if (offsets[i] % 16) throw sd_failure(SD_ERR_INVALID, "range " + std::to_string(i) + " not 16-byte aligned");
+    ctx->bind();
+    constexpr uint64_t W = Streamer::W;
+    SlotPair slots(ctx);
+    Streamer::prepare(slots);
+    sd_checksum_batch batches[2], big;
+    struct Pending {
+        size_t i0 = 0, i1 = 0;
+        bool busy = false;
+    } pend[2];
+    auto harvest = [&](int k) {
+        if (!pend[k].busy) return;
+        HIP_CHECK(hipStreamSynchronize(slots[k].stream));
+        const uint8_t* h = slots[k].host_hashes.u8();
+        for (size_t i = pend[k].i0; i < pend[k].i1; i++) to_hex(h + 32 * (i - pend[k].i0), 32, out_hex65 + 65 * i);
+        pend[k].busy = false;
+    };
+    int cur = 0;
+    std::vector<uint64_t> offs, ls;
+    for (size_t i = 0; i < n;) {
+        if (lens[i] + 128 > W) {  // one large range, streamed
+            harvest(0);
+            harvest(1);
+            const uint64_t off0 = 0, L = lens[i];
+            plan_checksum_batch(&big, &off0, &L, 1, nullptr);
+            const uint64_t nb = big.plan.wg_map.size();
+            for (uint64_t pos = 0; pos < L; pos += W) {
+                const int k = cur;
+                cur ^= 1;
+                HIP_CHECK(hipStreamSynchronize(slots[k].stream));
+                const uint64_t here = std::min<uint64_t>(W, L - pos);
+                HIP_CHECK(hipMemcpyAsync(slots[k].staged.p, data + offsets[i] + pos, align_up(here, 64),
+                                         hipMemcpyHostToDevice, slots[k].stream));
+                const uint32_t wg0 = (uint32_t)(pos / SD_CK_BLOCK);
+                const uint32_t wg1 = (uint32_t)std::min<uint64_t>(nb, wg0 + W / SD_CK_BLOCK);
+                HIP_CHECK(sdk::launch_ck_leaf(slots[k].staged.as<uint8_t>(), pos, 0, big.files.as<ck_file>(),
+                                              big.wg_map.as<uint2>() + wg0, wg1 - wg0, big.lvl[0].as<uint32_t>(),
+                                              slots[k].hashes.as<uint32_t>(), slots[k].stream));
+            }
+            slots.sync_all();
+            Slot& sl = slots[0];
+            run_checksum_reduce(&big, sl.hashes.as<uint32_t>(), sl.stream);
+            HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, 32, hipMemcpyDeviceToHost, sl.stream));
+            HIP_CHECK(hipStreamSynchronize(sl.stream));
+            to_hex(sl.host_hashes.u8(), 32, out_hex65 + 65 * i);
+            i++;
+            continue;
+        }
+        // the next window: consecutive ranges whose span fits
+        const uint64_t lo = offsets[i] / 16 * 16;
+        uint64_t hi = 0;
+        size_t j = i;
+        while (j < n && lens[j] + 128 <= W) {
+            const uint64_t nlo = std::min(lo, offsets[j] / 16 * 16);
+            const uint64_t nhi = std::max(hi, align_up(offsets[j] + lens[j], 64));
+            if (j > i && (nlo < lo || nhi - lo > W)) break;
+            hi = nhi;
+            j++;
+        }
+        const int k = cur;
+        cur ^= 1;
+        harvest(k);
+        Slot& sl = slots[k];
+        offs.assign(offsets + i, offsets + j);
+        ls.assign(lens + i, lens + j);
+        for (auto& o : offs) o -= lo;
+        plan_checksum_batch(&batches[k], offs.data(), ls.data(), j - i, sl.stream);
+        sl.hashes.ensure((j - i) * 32);
+        sl.host_hashes.ensure((j - i) * 32);
+        HIP_CHECK(hipMemcpyAsync(sl.staged.p, data + lo, std::max<uint64_t>(hi - lo, 16), hipMemcpyHostToDevice,
+                                 sl.stream));
+        run_checksum_batch(&batches[k], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
+        HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, (j - i) * 32, hipMemcpyDeviceToHost, sl.stream));
+        pend[k] = Pending{i, j, true};
+        i = j;
+    }
     harvest(0);
     harvest(1);
     return SD_OK;

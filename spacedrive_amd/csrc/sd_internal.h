@@ -16,6 +16,8 @@ enum sd_tune_key {
     SD_TUNE_NKEYS = 5
 };
 int tuning_get(int key);
+// the device a context was created on
+int sd_ctx_device(const sd_cas_ctx* ctx);
 // latency path (coalesce.cpp)
 #include <string>
 struct sd_coalescer;

@@ -10,10 +10,18 @@ file index of the group (the "Object-link candidate").
 
 Multi-GPU: files are sharded by index; each rank buckets its records
 ``(cas_id as big-endian u64, global index)`` by cas_id prefix (device kernel
-``sd_dedup_partition``), one ``all_to_all_single`` of the per-destination counts and one
-of the 16-byte records move every record to the rank owning its prefix (backend "nccl"
-= RCCL over xGMI on MI355X; "gloo" on CPU for tests), and each rank sorts and groups
-its bucket (``sd_dedup_group``).  No other collective exists on the data path.
+``sd_dedup_partition``), the records move to the rank owning their prefix range, and
+each rank sorts and groups its bucket (``sd_dedup_group``) and assigns Objects
+(``sd_dedup_owners``).  Two transports for the exchange:
+
+* ``dedup_shard_rccl`` -- the product path on GPUs: the whole step behind the C ABI
+  (``sd_cas_dedup_mgpu``): an RCCL all-gather of the count matrix, then grouped
+  ncclSend/ncclRecv of the records (the all-to-all over xGMI), on libsdcas's own RCCL
+  communicator (``make_comm``), so a Rust host drives the same code;
+* ``dedup_shard`` -- the same step with the exchange in ``torch.distributed``
+  (``all_to_all_single``), which also runs on "gloo" for the CPU tests.
+
+No other collective exists on the data path.
 """
 from __future__ import annotations
 
@@ -66,28 +74,96 @@ def group_device(ctx, records: torch.Tensor, index_sorted: bool = False) -> Tupl
     return records, rep[:m], ng
 
 
+def shards_ascend(n_local: int, global_base: int, group: Optional[dist.ProcessGroup] = None,
+                   device=None) -> bool:
+    """True when every rank's index range [base, base + n) ends before the next rank's
+    starts: the records received in rank order are then in ascending index order."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return True
+    mine = torch.tensor([global_base, n_local], dtype=torch.int64, device=device)
+    rows = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(rows, mine, group=group)
+    r = torch.stack(rows).cpu().tolist()
+    return all(r[k][0] + r[k][1] <= r[k + 1][0] for k in range(world - 1))
+
+
 def dedup_shard(ctx, d_hash32: torch.Tensor, d_valid: Optional[torch.Tensor], n_local: int, global_base: int,
-                group: Optional[dist.ProcessGroup] = None):
+                group: Optional[dist.ProcessGroup] = None, index_sorted: Optional[bool] = None):
     """Full distributed step on one rank: partition -> exchange -> group -> Object owners.
 
     Returns (records int64 [m, 2] sorted by (key, index), rep int64 [m], n_groups,
     owner int64 [m]) for the cas_id prefix range this rank owns; owner is the file whose
     Object each record links to under the reference's chunk-of-100 rule
-    (spacedrive_amd/identifier.py).
+    (spacedrive_amd/identifier.py).  ``index_sorted``: whether the shards' index ranges
+    ascend with the rank (checked with one small all-gather when None).
     """
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     dev = d_hash32.device
+    if index_sorted is None:
+        gloo = world > 1 and dist.get_backend(group) == "gloo"
+        index_sorted = shards_ascend(n_local, global_base, group, "cpu" if gloo else dev)
     counts = torch.empty(world, dtype=torch.int64, device=dev)
     recs = torch.empty((max(n_local, 1), 2), dtype=torch.int64, device=dev)
     nv = ctx.dedup_partition(d_hash32, d_valid, n_local, global_base, world, counts, recs)
     recv = exchange(recs[:nv], counts, group)
-    # the partition is stable and shard r holds indices [r*n, (r+1)*n): the received
-    # records are in ascending index order, so one stable cas_id sort suffices
-    records, rep, ng = group_device(ctx, recv, index_sorted=True)
+    # the partition is stable: with ascending shards the received records are in index
+    # order, and one stable cas_id sort suffices
+    records, rep, ng = group_device(ctx, recv, index_sorted=index_sorted)
     # identifier.object_owners is the torch statement of the same rule (tests compare them)
     owners = torch.empty(max(records.shape[0], 1), dtype=torch.int64, device=dev)
     ctx.dedup_owners(records, records.shape[0], rep, owners)
     return records, rep, ng, owners[:records.shape[0]]
+
+
+def make_comm(ctx, group: Optional[dist.ProcessGroup] = None):
+    """libsdcas's RCCL communicator over the ranks of ``group``: rank 0's ncclUniqueId is
+    broadcast through torch.distributed, then every rank joins (sd_comm_create)."""
+    from .device import Comm
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    uid = [Comm.unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0, group=group)
+    return Comm(ctx, uid[0], world, rank)
+
+
+class RcclDedup:
+    """sd_cas_dedup_mgpu with reusable output buffers (grown when a rank needs more)."""
+
+    def __init__(self, ctx, comm, device, capacity: int = 0):
+        self.ctx, self.comm, self.device = ctx, comm, device
+        self.capacity = 0
+        self._alloc(capacity)
+
+    def _alloc(self, cap: int) -> None:
+        cap = max(int(cap), 1)
+        if cap > self.capacity:
+            self.records = torch.empty((cap, 2), dtype=torch.int64, device=self.device)
+            self.rep = torch.empty(cap, dtype=torch.int64, device=self.device)
+            self.owner = torch.empty(cap, dtype=torch.int64, device=self.device)
+            self.capacity = cap
+
+    def __call__(self, d_hash32, d_valid, n_local: int, global_base: int, chunk_size: int = 100, stream=None):
+        from ._native import SD_ERR_CAPACITY, SdCasError
+        for _ in range(2):
+            try:
+                m, ng = self.ctx.dedup_mgpu(self.comm, d_hash32, d_valid, n_local, global_base, self.records,
+                                            self.rep, self.owner, self.capacity, chunk_size, stream)
+                return self.records[:m], self.rep[:m], ng, self.owner[:m]
+            except SdCasError as e:
+                if e.rc != SD_ERR_CAPACITY:
+                    raise
+                # every rank stopped before the exchange: all retry, each with room for its need
+                self._alloc(max(e.needed, self.capacity) * 5 // 4 + 1024)
+        raise RuntimeError("sd_cas_dedup_mgpu: capacity still short after regrowing")
+
+
+def dedup_shard_rccl(ctx, comm, d_hash32: torch.Tensor, d_valid: Optional[torch.Tensor], n_local: int,
+                     global_base: int, capacity: Optional[int] = None):
+    """dedup_shard through the C ABI's RCCL exchange (sd_cas_dedup_mgpu); same outputs."""
+    runner = RcclDedup(ctx, comm, d_hash32.device, capacity if capacity is not None else n_local + 4096)
+    return runner(d_hash32, d_valid, n_local, global_base)
 
 
 # ------------------------------------------------------------------ host reference

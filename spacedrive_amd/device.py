@@ -11,7 +11,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ._native import Extent, check, lib
+from ._native import Extent, SdCasError, check, lib
 
 EXTENT_DTYPE = np.dtype([("size", "<u8"), ("msg_offset", "<u8"), ("msg_len", "<u4"), ("kind", "<u4")])
 assert EXTENT_DTYPE.itemsize == ctypes.sizeof(Extent) == 24
@@ -103,6 +103,52 @@ class Context:
     def dedup_owners(self, d_records, m: int, d_rep, d_owner, chunk_size: int = 100, stream=None) -> None:
         check(lib().sd_dedup_owners(self.handle, _ptr(d_records), m, _ptr(d_rep), chunk_size, _ptr(d_owner),
                                     _stream(stream)))
+
+    def dedup_mgpu(self, comm: "Comm", d_hash32, d_valid, n: int, base: int, d_records, d_rep, d_owner,
+                   capacity: int, chunk_size: int = 100, stream=None):
+        """sd_cas_dedup_mgpu: partition -> RCCL all-to-all -> group -> owners on this rank.
+        Returns (m, n_groups); raises SdCasError (SD_ERR_CAPACITY) on every rank when some
+        rank's capacity is short -- then ``.needed`` is this rank's requirement."""
+        m = ctypes.c_uint64(0)
+        ng = ctypes.c_uint64(0)
+        rc = lib().sd_cas_dedup_mgpu(self.handle, comm.handle, _ptr(d_hash32), _ptr(d_valid), n, base, chunk_size,
+                                     _ptr(d_records), _ptr(d_rep), _ptr(d_owner), capacity, ctypes.byref(m),
+                                     ctypes.byref(ng), _stream(stream))
+        try:
+            check(rc)
+        except SdCasError as e:
+            e.needed = int(m.value)
+            raise
+        return int(m.value), int(ng.value)
+
+
+class Comm:
+    """libsdcas's RCCL communicator (sd_comm): one per rank, on its context's device."""
+
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(Comm.ID_BYTES)
+        check(lib().sd_comm_id(buf))
+        return buf.raw
+
+    def __init__(self, ctx: Context, uid: bytes, nranks: int, rank: int):
+        assert len(uid) == Comm.ID_BYTES
+        h = ctypes.c_void_p()
+        check(lib().sd_comm_create(ctx.handle, uid, nranks, rank, ctypes.byref(h)))
+        self.handle, self.nranks, self.rank = h, nranks, rank
+
+    def close(self) -> None:
+        if self.handle:
+            lib().sd_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class CasBatch:

@@ -78,3 +78,26 @@ def test_distributed_grouping_equals_single_process(tmp_path, world):
 def test_single_rank_exchange_is_identity():
     recs = torch.arange(10, dtype=torch.int64).view(5, 2)
     assert exchange(recs, torch.tensor([5])) is recs
+
+
+def _ascend_worker(rank, world, port, outdir):
+    from spacedrive_amd.dedup import shards_ascend
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = [shards_ascend(100, rank * 100),          # contiguous, ascending
+               shards_ascend(100, (world - 1 - rank) * 100),  # descending: received records not index-sorted
+               shards_ascend(100, rank * 50)]            # overlapping ranges
+        np.save(os.path.join(outdir, f"a{rank}.npy"), np.array(res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shards_ascend_is_checked_across_ranks(tmp_path):
+    """the index-sorted grouping fast path is taken only when every rank's
+    [base, base + n) ends before the next rank's starts (checked by one all-gather)."""
+    world = 3
+    mp.start_processes(_ascend_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        assert np.load(tmp_path / f"a{r}.npy").tolist() == [True, False, False]

@@ -720,3 +720,70 @@ def test_latency_policy_routes_and_agrees(ctx, tmp_path):
     after = sd.coalescer_stats()
     assert got == want and sums == want_sums
     assert after["cpu"] - before["cpu"] == 2 * len(paths) and after["batches"] == before["batches"]
+
+
+def test_dedup_mgpu_through_rccl_single_rank(ctx):
+    """sd_cas_dedup_mgpu through a real RCCL communicator (1 rank: the
+    all-gather and the grouped send/recv to self run; no world == 1 short-circuit) equals
+    the host grouping; an undersized output fails with SD_ERR_CAPACITY before the exchange
+    and the retrying runner recovers."""
+    from spacedrive_amd import dedup
+    from spacedrive_amd._native import SD_ERR_CAPACITY, SdCasError
+    from spacedrive_amd.identifier import object_owners
+    n = 60000
+    sizes, cids, twins = synth.library(0, n, n, dup_frac=0.3)
+    h = gpu_cas(ctx, sizes, cids, twins)
+    d_hash = torch.from_numpy(h.copy()).cuda()
+    valid = (sizes != 0)
+    d_valid = torch.from_numpy(valid.astype(np.uint8)).cuda()
+    comm = dedup.make_comm(ctx)
+    try:
+        base = 7_000_000  # a shard of a larger library
+        recs_h = np.stack([keys_from_hashes(h)[valid].view(np.int64), np.arange(base, base + n)[valid]], axis=1)
+        gr, grep, gng = group_host(recs_h)
+        small = torch.empty((10, 2), dtype=torch.int64, device="cuda")
+        with pytest.raises(SdCasError) as e:
+            ctx.dedup_mgpu(comm, d_hash, d_valid, n, base, small, small[:, 0].clone(), small[:, 0].clone(), 10)
+        assert e.value.rc == SD_ERR_CAPACITY and e.value.needed == int(valid.sum())
+        runner = dedup.RcclDedup(ctx, comm, d_hash.device, capacity=100)  # regrows once
+        for _ in range(2):  # and reuses its buffers
+            recs, rep, ng, owner = runner(d_hash, d_valid, n, base)
+            torch.cuda.synchronize()
+            assert ng == gng
+            assert np.array_equal(recs.cpu().numpy(), gr)
+            assert np.array_equal(rep.cpu().numpy(), grep)
+            want_owner = object_owners(torch.from_numpy(gr[:, 1].copy()), torch.from_numpy(grep), 100).numpy()
+            assert np.array_equal(owner.cpu().numpy(), want_owner)
+        # the torch.distributed exchange path gives the same outputs
+        r2, rep2, ng2, own2 = dedup.dedup_shard(ctx, d_hash, d_valid, n, base)
+        assert ng2 == gng and np.array_equal(r2.cpu().numpy(), gr) and np.array_equal(own2.cpu().numpy(), want_owner)
+    finally:
+        comm.close()
+
+
+def test_checksums_from_host_memory(ctx, oracle_native):
+    """sd_checksums: ranges of a host buffer (pinned) -> hex, packed windows and a range
+    larger than a window (streamed with a known length), against the oracle."""
+    import ctypes
+    from spacedrive_amd._native import check, lib
+    MiB = 1 << 20
+    lens = [0, 1, 1025, MiB + 3, 5 * MiB, (300 << 20) + 5, 77, 2 * MiB - 1]
+    offs, off = [], 0
+    for L in lens:
+        offs.append(off)
+        off = (off + L + 64 + 63) // 64 * 64
+    host = torch.empty(off + 64, dtype=torch.uint8, pin_memory=True)
+    d = torch.zeros(off + 64, dtype=torch.uint8, device="cuda")
+    for i, (L, o) in enumerate(zip(lens, offs)):
+        if L:
+            ctx.synth_fill(800 + i, 0, L, d[o:])
+    torch.cuda.synchronize()
+    host.copy_(d.cpu())
+    del d
+    arr_o = np.array(offs, np.uint64)
+    arr_l = np.array(lens, np.uint64)
+    out = ctypes.create_string_buffer(65 * len(lens))
+    check(lib().sd_checksums(ctx.handle, host.data_ptr(), arr_o.ctypes.data, arr_l.ctypes.data, len(lens), out))
+    want = oracle_native.checksums_simd(host.numpy(), arr_o, arr_l, nthreads=NT)
+    for i in range(len(lens)):
+        assert out.raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), lens[i]
