@@ -7,21 +7,27 @@ Workload (BASELINE.json configs[4], weak-scaled): a 10 M-file synthetic library 
 configs[0] mixture (60 % of files <= 100 KiB hashed whole, 40 % sampled), sharded by file
 index: each GPU owns ``--files-per-gpu`` (default 1 250 000 = 10 M / 8) files, so N = 8 is
 the full 10 M-file library.  One step = hash every file of the shard (sampled kernel +
-whole-file kernels) + the dedup exchange (partition by cas_id prefix, all-to-all of the
-records over RCCL, sort + group).  Inputs are resident in HBM before timing (generated on
-device from the counter-based generator; host staging + PCIe is reported separately in
-DESIGN.md, never as `value`).
+whole-file kernels) + the dedup step through the C ABI (sd_cas_dedup_mgpu: partition by
+cas_id prefix, RCCL all-gather of the count matrix + grouped send/recv of the records,
+sort + group, Object owners).  Inputs are resident in HBM before timing (generated on
+device from the counter-based generator); PCIe-inclusive rates are reported beside
+`value` ("with_h2d"), never as it.
 
-After the timed steps, rank 0 (N = 1 only) times the CPU baseline (oracle/sd_oracle.c,
-the C restatement of cas.rs + blake3) on a bounded sample of the same files, and every
-rank times configs[3] (full-file checksums of 16 x 4 GiB files) as `checksum`.
+After the timed steps: configs[3] (full-file checksums of 16 x 4 GiB files) on every
+rank as `checksum`; on rank 0 at N = 1 the configs[1]/[2] kernel legs, the with-H2D legs
+(cas_ids and checksums from pinned host memory), the file-backed legs (cas_ids and
+checksums from tmpfs beside the reference's read schedule on the CPU), single-call
+latency percentiles of the GPU-coalesced and CPU paths, and the CPU baseline
+(oracle/sd_oracle_simd.c, the C restatement of cas.rs + blake3) on a bounded sample.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -32,10 +38,19 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
-# int32 VALU: 157.3 TF fp32 vector peak (MI355X_MICROARCH.md) counts packed FMA (2 flop x 2
-# lanes); BLAKE3's add/xor/alignbit have no packed 32-bit forms: 256 CU x 64 lanes x 2.4 GHz
+# The int32 VALU roof.  BLAKE3's G function is 2x v_add3_u32 + 2x v_add_u32 + 4x v_xor_b32
+# + 4x v_alignbit_b32; the 3-source ops (add3, alignbit) issue at half the rate of 2-source
+# VOP2 ops (measured: profiles/r1c_valu_probe.txt), so the mix is bounded by one wave64 op
+# per 4 cycles per SIMD: 256 CU x 64 lane-ops/clk x 2.4 GHz = 39.3 T lane-ops/s.
 VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
+# The guide's full VALU rate (MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 op in 2
+# cycles): 256 x 128 x 2.4 GHz = 78.6 T lane-ops/s -- reported as frac_full_rate.
+VALU_FULL_RATE_TOPS = 256 * 128 * 2.4e9 / 1e12
+PEAK_BASIS = ("3-operand VALU issue bound (probe): 256 CU x 64 lane-ops/clk x 2.4 GHz. BLAKE3's G is "
+              "v_add3/v_alignbit-heavy; 3-source ops issue at half the 2-source rate (profiles/r1c_valu_probe.txt). "
+              "frac_full_rate is against the guide's SIMD-32 full rate, 256 CU x 128 lane-ops/clk x 2.4 GHz = 78.6 T")
 SAMPLED_MSG = 57352
+S_FILES_PER_WG, S_THREADS = 16, 448  # k_cas_sampled launch shape (cas_kernels.hip)
 
 
 def log(*a):
@@ -53,6 +68,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target seconds per CPU-baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (rehearsal)")
+    p.add_argument("--dedup", default=None, choices=["rccl", "torch"],
+                   help="exchange transport: rccl = sd_cas_dedup_mgpu (C ABI; default with nccl), torch = "
+                        "torch.distributed all_to_all (default with gloo)")
     p.add_argument("--share-gpu", action="store_true", help="map every rank onto the visible GPUs (rehearsal)")
     p.add_argument("--config-files", type=int, default=1_000_000,
                    help="N=1 only: files of the configs[1] (small) and configs[2] (sampled) kernel legs; 0 = skip")
@@ -60,20 +78,65 @@ def parse():
     p.add_argument("--file-backed-files", type=int, default=20000,
                    help="N=1 only: time the drop-in from files on disk (pread stager + sd_cas_ids) on this many "
                         "files of the shard, beside the reference's read schedule on the CPU; 0 = skip")
-    p.add_argument("--host-staged-files", type=int, default=0,
-                   help="N=1 only: also time the PCIe-inclusive drop-in path on this many files (DESIGN.md)")
+    p.add_argument("--host-staged-files", type=int, default=300_000,
+                   help="N=1 only: with-H2D leg, sd_cas_ids over this many files from pinned host memory; 0 = skip")
+    p.add_argument("--host-checksum-gib", type=int, default=4,
+                   help="N=1 only: with-H2D checksum leg, sd_checksums over this many GiB of pinned memory; 0 = skip")
+    p.add_argument("--file-checksum-mib", type=int, default=2048,
+                   help="N=1 only: file-backed checksum leg on tmpfs (MiB, 256 MiB files); 0 = skip")
+    p.add_argument("--latency-calls", type=int, default=400, help="N=1 only: single-call latency legs; 0 = skip")
+    p.add_argument("--no-extras", action="store_true", help="skip every N=1 side leg (profiling passes)")
     return p.parse_args()
 
 
-def pmc_traffic(kernels):
-    """HBM bytes per launch (summed over the given kernels) from the committed rocprofv3
-    PMC summary of the same bench command (profiles/pmc_summary.json), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+# ------------------------------------------------------------------ PMC traffic lookup
+def pmc_traffic(kernel: str, grid: int):
+    """HBM bytes per launch of `kernel` at launch shape `grid` (work-items) from the
+    committed rocprofv3 PMC summary (profiles/pmc_summary.json), or None when no pass
+    measured that launch shape."""
     try:
-        d = json.load(open(path))
-        return sum(d["kernels"][k]["hbm_bytes_per_launch"] for k in ([kernels] if isinstance(kernels, str) else kernels))
-    except Exception:
-        return None
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
+        for e in d["kernels"].get(kernel, []):
+            if int(e["grid"]) == int(grid):
+                return {"bytes": e["hbm_bytes_per_launch"], "tag": d.get("tag"), "grid": grid,
+                        "fetch_factor": e["fetch_factor"]}
+    except (OSError, KeyError, ValueError, TypeError, AttributeError):
+        pass
+    return None
+
+
+def sampled_grid(n_sampled: int) -> int:
+    return (n_sampled + S_FILES_PER_WG - 1) // S_FILES_PER_WG * S_THREADS
+
+
+def whole_grid(batch) -> int:
+    return ((batch.full_items + 255) // 256 + (batch.tail_items + 255) // 256) * 256
+
+
+def valu_roof(compressions: int, ms: float) -> dict:
+    a = compressions * 672 / (ms * 1e-3) / 1e12
+    return {"achieved": a, "frac": a / VALU_PEAK_TOPS, "frac_full_rate": a / VALU_FULL_RATE_TOPS}
+
+
+# ------------------------------------------------------------------ host CPU
+def host_cpu() -> dict:
+    import subprocess
+    model = "?"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return {"model": model, "cpus_online": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
 
 
 def cpu_baseline(sizes, cids, twins, seconds: float):
@@ -110,40 +173,100 @@ def cpu_baseline(sizes, cids, twins, seconds: float):
                   f"on {threads} threads; {bT / dtT / 1e9:.2f} GB/s of message bytes",
         "single_thread": {"value": n1 / dt1, "unit": "files/s", "cores": 1, "sample_files": n1,
                           "GBps": b1 / dt1 / 1e9},
-        "simd": simd,
+        "simd": simd, "host_cpu": host_cpu(),
     }
 
 
-def host_staged(ctx, ext, d_staged, batch, k, dev):
-    """PCIe-inclusive drop-in path: the first k files' messages in pinned host memory ->
-    sd_cas_ids (plan, H2D, kernels, D2H, hex).  Reported apart from `value`."""
-    import ctypes
+# ------------------------------------------------------------------ with-H2D legs
+def ev_ms(fn, stream, reps=1):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def host_staged(ctx, ext, d_staged, k, dev, stream):
+    """with-H2D cas_ids: the first k files' staged messages in pinned host memory through
+    the drop-in sd_cas_ids (host plan + H2D + kernels + D2H + hex, windows pipelined on two
+    streams), beside the raw H2D copy of the same bytes and the device-resident kernels."""
     from spacedrive_amd._native import check, lib
     k = min(k, len(ext))
-    nbytes = int(ext["msg_offset"][k - 1]) + int(ext["msg_len"][k - 1])
-    nbytes = (nbytes + 63) // 64 * 64
+    nbytes = (int(ext["msg_offset"][k - 1]) + int(ext["msg_len"][k - 1]) + 63) // 64 * 64
     host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
     host.copy_(d_staged[:nbytes])
     sub = np.ascontiguousarray(ext[:k])
-    out = ctypes.create_string_buffer(17 * k)
     dbuf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    dbuf.copy_(host, non_blocking=True)  # warm the copy path
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    dbuf.copy_(host, non_blocking=True)
-    torch.cuda.synchronize()
-    h2d_s = time.perf_counter() - t0
-    del dbuf
-    check(lib().sd_cas_ids(ctx.handle, host.data_ptr(), nbytes, sub.ctypes.data, k, out, None))  # warm-up
-    t0 = time.perf_counter()
-    check(lib().sd_cas_ids(ctx.handle, host.data_ptr(), nbytes, sub.ctypes.data, k, out, None))
-    e2e_s = time.perf_counter() - t0
-    return {"files": k, "bytes": nbytes, "h2d_GBps": nbytes / h2d_s / 1e9, "h2d_ms": h2d_s * 1e3,
-            "end_to_end_files_per_s": k / e2e_s, "end_to_end_ms": e2e_s * 1e3,
-            "note": "sd_cas_ids from pinned host memory: host plan + H2D + kernels + D2H + hex, one call, "
-                    "not overlapped; the reference's own cost is reading the files (6 preads per sampled file)"}
+    h2d_ms = min(ev_ms(lambda: dbuf.copy_(host, non_blocking=True), stream) for _ in range(3))
+    b = ctx.cas_batch(sub)
+    hh = torch.empty(k * 32, dtype=torch.uint8, device=dev)
+    b.run(dbuf, hh, stream)
+    kernel_ms = ev_ms(lambda: b.run(dbuf, hh, stream), stream, reps=3)
+    want = hh.cpu().numpy().reshape(k, 32)[:, :8]
+    del dbuf, b, hh
+    out = ctypes.create_string_buffer(17 * k)
+    e2e = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        check(lib().sd_cas_ids(ctx.handle, host.data_ptr(), nbytes, sub.ctypes.data, k, out, None))
+        e2e.append(time.perf_counter() - t0)
+    got = np.frombuffer(bytes.fromhex("".join(out.raw[17 * i:17 * i + 16].decode() for i in range(k))),
+                        np.uint8).reshape(k, 8)
+    assert np.array_equal(got, want), "sd_cas_ids differs from the device-resident batch"
+    e2e_s = min(e2e[1:])
+    return {"files": k, "bytes": nbytes, "h2d_ms": h2d_ms, "h2d_GBps": nbytes / (h2d_ms * 1e-3) / 1e9,
+            "kernel_ms": kernel_ms, "kernel_files_per_s": k / (kernel_ms * 1e-3),
+            "end_to_end_ms": e2e_s * 1e3, "end_to_end_files_per_s": k / e2e_s,
+            "end_to_end_GBps": nbytes / e2e_s / 1e9,
+            "note": "sd_cas_ids from pinned host memory (best of 2 warm calls): plan + H2D + kernels + D2H + hex, "
+                    "512 MiB windows on two streams; h2d_ms = one raw copy of the same bytes (HIP events); "
+                    "kernel_ms = the same files device-resident"}
 
 
+def checksum_host(ctx, gib: int, dev, stream):
+    """with-H2D checksums: `gib` GiB of pinned host memory (files of 1 GiB) through the
+    drop-in sd_checksums, beside the raw H2D copy and the device-resident kernels."""
+    from spacedrive_amd._native import check, lib
+    nf, flen = gib, 1 << 30
+    total = nf * flen
+    d = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    for i in range(nf):
+        ctx.synth_fill(20_000 + i, 0, flen, d[i * flen:])
+    host = torch.empty(total + 64, dtype=torch.uint8, pin_memory=True)
+    torch.cuda.synchronize()
+    host.copy_(d)
+    scratch = torch.empty_like(d)
+    h2d_ms = min(ev_ms(lambda: scratch.copy_(host, non_blocking=True), stream) for _ in range(2))
+    del scratch
+    offs = np.arange(nf, dtype=np.uint64) * np.uint64(flen)
+    lens = np.full(nf, flen, np.uint64)
+    cb = ctx.checksum_batch(offs, lens)
+    hs = torch.empty(nf * 32, dtype=torch.uint8, device=dev)
+    cb.run(d, hs, stream)
+    kernel_ms = ev_ms(lambda: cb.run(d, hs, stream), stream, reps=2)
+    want = [hs[32 * i:32 * i + 32].cpu().numpy().tobytes().hex() for i in range(nf)]
+    del d, cb
+    torch.cuda.empty_cache()
+    out = ctypes.create_string_buffer(65 * nf)
+    e2e = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        check(lib().sd_checksums(ctx.handle, host.data_ptr(), offs.ctypes.data, lens.ctypes.data, nf, out))
+        e2e.append(time.perf_counter() - t0)
+    got = [out.raw[65 * i:65 * i + 64].decode() for i in range(nf)]
+    assert got == want, "sd_checksums differs from the device-resident batch"
+    e2e_s = min(e2e)
+    return {"files": nf, "bytes": total, "h2d_ms": h2d_ms, "h2d_GBps": total / (h2d_ms * 1e-3) / 1e9,
+            "kernel_ms": kernel_ms, "kernel_GBps": total / (kernel_ms * 1e-3) / 1e9,
+            "end_to_end_ms": e2e_s * 1e3, "end_to_end_GBps": total / e2e_s / 1e9,
+            "note": f"sd_checksums over {nf} x 1 GiB of pinned host memory (best of 2): 256 MiB windows, H2D on two "
+                    "streams overlapping the kernels; h2d_ms = one raw copy; kernel_ms = device-resident"}
+
+
+# ------------------------------------------------------------------ configs[1] / [2]
 def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: float):
     """configs[1] (1 M files <= 100 KiB, whole-content cas_id) or configs[2] (1 M files
     > 100 KiB, sampled cas_id) on this GPU: kernel-only files/s over device-resident
@@ -163,31 +286,28 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
     h0 = torch.zeros(nfiles * 32, dtype=torch.uint8, device=dev)
     h1 = torch.zeros(nfiles * 32, dtype=torch.uint8, device=dev)
     b.run(d_staged, h0, stream)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    e0.record(stream)
-    for _ in range(reps):
-        b.run(d_staged, h1, stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    ms = ev_ms(lambda: b.run(d_staged, h1, stream), stream, reps=reps)
     deterministic = bool(torch.equal(h0, h1))
-    valu = b.compressions * 672 / (ms * 1e-3)
+    roof = valu_roof(b.compressions, ms)
+    kernels = ["k_cas_sampled"] if which == "sampled" else ["k_whole_items", "k_whole_merge8"]
+    grid = sampled_grid(b.n_sampled) if which == "sampled" else whole_grid(b)
+    tr = pmc_traffic(kernels[0], grid)
     res = {"workload": ("configs[1]: 1M files <= 100 KiB, whole-content cas_id (log-uniform sizes 1..102400)"
                         if which == "small" else
                         "configs[2]: 1M files > 100 KiB, sampled cas_id (log-uniform sizes 102401..4 GiB)"),
            "files": nfiles, "kernel_ms": ms, "files_per_s": nfiles / (ms * 1e-3),
            "msg_GBps": b.msg_bytes / (ms * 1e-3) / 1e9, "compressions": b.compressions,
-           "valu_frac": valu / 1e12 / VALU_PEAK_TOPS,
-           "valu_frac_of_measured_peak": valu / valu_peak if valu_peak else None,
-           "kernels": ["k_cas_sampled"] if which == "sampled" else ["k_whole_items", "k_whole_merge8"],
-           "deterministic": deterministic}
+           "valu_frac": roof["frac"], "valu_frac_full_rate": roof["frac_full_rate"],
+           "valu_frac_of_measured_peak": roof["achieved"] * 1e12 / valu_peak if valu_peak else None,
+           "kernels": kernels, "launch_grid": grid,
+           "traffic": tr["bytes"] if tr else None, "deterministic": deterministic}
     del d_staged, h0, h1, b
     torch.cuda.empty_cache()
     assert deterministic, which
     return res
 
 
+# ------------------------------------------------------------------ file-backed legs
 def _fs_type(path: str) -> str:
     best, fstype = "", "?"
     try:
@@ -200,81 +320,120 @@ def _fs_type(path: str) -> str:
     return fstype
 
 
-def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool):
+def _scratch_dir(need: int) -> str:
+    import tempfile
+    base = "/dev/shm"
+    try:
+        st = os.statvfs(base)
+        if st.f_bavail * st.f_frsize < 4 * need:
+            base = None
+    except OSError:
+        base = None
+    return tempfile.mkdtemp(prefix="sd_fb_", dir=base)
+
+
+def latency(ctx, paths, sizes, calls: int) -> dict:
+    """Single-call latency (p50 / p99, microseconds) of generate_cas_id for the reference's
+    per-file callers (watcher/utils.rs:235,393; non_indexed.rs:168): idle (one caller) and
+    with 64 concurrent callers, for the GPU-coalesced path (latency_cpu_max = 0), the CPU
+    path (sd_cpu_cas_id_path) and the default policy (CPU below 16 calls in flight)."""
+    from spacedrive_amd._native import check, lib
+    L = lib()
+    enc = [os.fsencode(p) for p in paths]
+    n = len(enc)
+
+    def gpu_call(i, out, st):
+        return L.sd_cas_id_path(ctx.handle, enc[i % n], int(sizes[i % n]), out, ctypes.byref(st))
+
+    def cpu_call(i, out, st):
+        return L.sd_cpu_cas_id_path(enc[i % n], int(sizes[i % n]), out, ctypes.byref(st))
+
+    def run(fn, callers, per_caller):
+        lat = [[] for _ in range(callers)]
+        barrier = threading.Barrier(callers)
+
+        def worker(c):
+            out = ctypes.create_string_buffer(17)
+            st = ctypes.c_int32(0)
+            barrier.wait()
+            for j in range(per_caller):
+                t0 = time.perf_counter()
+                check(fn(c * per_caller + j, out, st))
+                lat[c].append(time.perf_counter() - t0)
+                assert st.value == 0
+
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=worker, args=(c,)) for c in range(callers)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        wall = time.perf_counter() - t0
+        v = np.array([x for row in lat for x in row]) * 1e6
+        return {"p50_us": float(np.percentile(v, 50)), "p99_us": float(np.percentile(v, 99)),
+                "calls": int(v.size), "calls_per_s": v.size / wall}
+
+    res = {}
+    for mode, cpu_max in (("gpu_coalesced", 0), ("policy_default", 16)):
+        check(L.sd_cas_set_tuning(b"latency_cpu_max", cpu_max))
+        try:
+            run(gpu_call, 1, 20)  # warm
+            res[mode] = {"idle": run(gpu_call, 1, calls), "concurrent_64": run(gpu_call, 64, max(4, calls // 16))}
+        finally:
+            check(L.sd_cas_set_tuning(b"latency_cpu_max", 16))
+    res["cpu_path"] = {"idle": run(cpu_call, 1, calls), "concurrent_64": run(cpu_call, 64, max(4, calls // 16))}
+    res["note"] = ("files of the file-backed leg on tmpfs (page cache warm), one generate_cas_id per call through "
+                   "ctypes from Python threads; gpu_coalesced = sd_cas_id_path with latency_cpu_max 0 "
+                   "(200 us window), policy_default = latency_cpu_max 16, cpu_path = sd_cpu_cas_id_path")
+    return res
+
+
+def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool, latency_calls: int):
     """The drop-in path from files on disk, as identifier_job_step would drive it
     (file_identifier/mod.rs:107-134): the first k files of this shard are written to a
     scratch directory (sampled files sparse: only the windows cas.rs reads are
-    materialised), then timed end to end -- stage (sd_cas_stage_files: head / 4 samples /
-    tail by pread on 16 threads into pinned memory) + sd_cas_ids (H2D, kernels, D2H, hex)
-    -- and, as the CPU baseline, the reference's own read schedule (open, read_exact,
-    seek; cas.rs:27-58) + the SIMD C restatement on 1 and 16 threads.  Both read from
-    the page cache (files just written).  The two outputs are asserted equal."""
-    import ctypes
+    materialised), then timed end to end through sd_cas_ids_files (read stager pool
+    overlapped with H2D + kernels + D2H), beside the reference's own read schedule
+    (open, read_exact, seek; cas.rs:27-58) + the SIMD C restatement on 1 and 16 threads
+    and the library's CPU path.  All read from the page cache (files just written); the
+    outputs are asserted equal."""
     import shutil
-    import tempfile
     import spacedrive_amd as sd
     from spacedrive_amd import synth
     from spacedrive_amd._native import check, lib
     k = min(k, len(sizes))
     sub_sizes = np.ascontiguousarray(sizes[:k])
-    sub_ext, total = sd.stage_plan(sub_sizes)
     nbytes = int(ext["msg_offset"][k - 1]) + int(ext["msg_len"][k - 1])
     host = d_staged[:nbytes].cpu().numpy()  # messages in the shard layout (same offsets)
-    base = "/dev/shm"
-    try:
-        st = os.statvfs(base)
-        if st.f_bavail * st.f_frsize < 4 * nbytes:
-            base = None
-    except OSError:
-        base = None
-    d = tempfile.mkdtemp(prefix="sd_fb_", dir=base)
+    d = _scratch_dir(nbytes)
     try:
         t0 = time.perf_counter()
         paths = synth.write_files(d, sub_sizes, host, ext[:k])
         write_s = time.perf_counter() - t0
         L = lib()
         arr = (ctypes.c_char_p * k)(*[os.fsencode(p) for p in paths])
-        pin = ctypes.c_void_p()
-        check(L.sd_cas_host_alloc(ctx.handle, total, ctypes.byref(pin)))
-        out = ctypes.create_string_buffer(17 * k)
-        status = np.zeros(k, np.int32)
         threads = 16
-        runs = []
-        try:
-            for _ in range(3):  # first run warms the stager's threads and the context's slots
-                status[:] = 0
-                t0 = time.perf_counter()
-                check(L.sd_cas_stage_files(arr, sub_ext.ctypes.data, k, pin, status.ctypes.data, threads))
-                t1 = time.perf_counter()
-                check(L.sd_cas_ids(ctx.handle, pin, total, sub_ext.ctypes.data, k, out, status.ctypes.data))
-                t2 = time.perf_counter()
-                runs.append((t1 - t0, t2 - t1))
-        finally:
-            L.sd_cas_host_free(ctx.handle, pin)
-        assert (status == 0).all(), np.unique(status)
-        stage_s = min(r[0] for r in runs[1:])
-        hash_s = min(r[1] for r in runs[1:])
-        gpu_ids = [out.raw[17 * i:17 * i + 16].decode() for i in range(k)]
-        # the pipelined path-based drop-in: stager pool preads window k+1 while window k
-        # is copied and hashed (sd_cas_ids_files)
-        out2 = ctypes.create_string_buffer(17 * k)
-        st2 = np.zeros(k, np.int32)
+        out = ctypes.create_string_buffer(17 * k)
+        st = np.zeros(k, np.int32)
         sz = np.ascontiguousarray(sub_sizes, np.uint64)
         pipe = []
-        for _ in range(3):
+        for _ in range(3):  # first run warms the stager's threads and the context's slots
             t0 = time.perf_counter()
-            check(L.sd_cas_ids_files(ctx.handle, arr, sz.ctypes.data, k, out2, st2.ctypes.data, threads))
+            check(L.sd_cas_ids_files(ctx.handle, arr, sz.ctypes.data, k, out, st.ctypes.data, threads))
             pipe.append(time.perf_counter() - t0)
-        assert (st2 == 0).all() and out2.raw == out.raw
+        assert (st == 0).all(), np.unique(st)
+        gpu_ids = [out.raw[17 * i:17 * i + 16].decode() for i in range(k)]
         pipe_s = min(pipe[1:])
         res = {"files": k, "dir_fs": _fs_type(d), "write_s": write_s,
-               "message_bytes": int(sub_ext["msg_len"].astype(np.int64).sum()),
+               "message_bytes": int(ext["msg_len"][:k].astype(np.int64).sum()),
                "gpu": {"files_per_s": k / pipe_s, "ms": pipe_s * 1e3, "stage_threads": threads,
-                       "note": "sd_cas_ids_files: pread on the library's stager pool into pinned windows, "
-                               "overlapped with H2D + kernels + D2H + hex; best of 2 warm runs",
-                       "unpipelined": {"files_per_s": k / (stage_s + hash_s), "stage_ms": stage_s * 1e3,
-                                       "hash_ms": hash_s * 1e3,
-                                       "note": "sd_cas_stage_files then sd_cas_ids, one after the other"}}}
+                       "note": "sd_cas_ids_files: read on the library's stager pool into pinned windows, "
+                               "overlapped with H2D + kernels + D2H + hex; best of 2 warm runs"}}
+        t0 = time.perf_counter()
+        cpu_ids = sd.cpu.generate_cas_ids(paths, sub_sizes, nthreads=threads)
+        res["library_cpu_path"] = {"files_per_s": k / (time.perf_counter() - t0), "threads": threads,
+                                   "lanes": sd.cpu.simd_lanes()}
+        assert cpu_ids == gpu_ids, "the library's CPU path differs from its GPU path"
         if with_cpu:
             from oracle import native
             cpu = {}
@@ -288,13 +447,69 @@ def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool):
             res["cpu_reference_schedule"] = cpu
             res["equal_to_cpu"] = want == gpu_ids
             assert res["equal_to_cpu"], "file-backed GPU cas_ids differ from the CPU restatement"
+        if latency_calls > 0:
+            res["latency"] = latency(ctx, paths[:2000], sub_sizes[:2000], latency_calls)
         return res
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
 
+def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
+    """file_checksum from files on tmpfs (hash.rs:10-24): 256 MiB files through the drop-in
+    sd_file_checksums (1 MiB reads into pinned windows overlapped with H2D + kernels),
+    beside the reference's read schedule + the SIMD C restatement (oracle, 1 and 16
+    threads) and the library's CPU path; outputs asserted equal."""
+    import shutil
+    import spacedrive_amd as sd
+    nf = max(1, mib // 256)
+    flen = 256 << 20
+    d = _scratch_dir(nf * flen)
+    try:
+        buf = torch.empty(flen, dtype=torch.uint8, device=dev)
+        paths = []
+        for i in range(nf):
+            ctx.synth_fill(30_000 + i, 0, flen, buf)
+            torch.cuda.synchronize()
+            p = os.path.join(d, f"ck{i}")
+            buf.cpu().numpy().tofile(p)
+            paths.append(p)
+        del buf
+        sd.file_checksums(paths[:1])  # warm the slots' pinned windows
+        t0 = time.perf_counter()
+        gpu = sd.file_checksums(paths)
+        gpu_s = time.perf_counter() - t0
+        total = nf * flen
+        res = {"files": nf, "bytes": total, "dir_fs": _fs_type(d),
+               "gpu": {"GBps": total / gpu_s / 1e9, "seconds": gpu_s,
+                       "note": "sd_file_checksums: hash.rs's 1 MiB reads into 256 MiB pinned windows, two slots "
+                               "alternating (reads overlap H2D + kernels)"}}
+        t0 = time.perf_counter()
+        lib_cpu = sd.cpu.file_checksums(paths, nthreads=16)
+        res["library_cpu_path"] = {"GBps": total / (time.perf_counter() - t0) / 1e9, "threads": 16}
+        assert lib_cpu == gpu
+        if with_cpu:
+            from oracle import native
+            cpu = {}
+            for nt in (1, 16):
+                t0 = time.perf_counter()
+                got, st = native.file_checksums(paths, nthreads=nt, simd=-1)
+                dt = time.perf_counter() - t0
+                cpu[f"threads_{nt}"] = {"GBps": total / dt / 1e9, "seconds": dt}
+            assert (st == 0).all() and [g.tobytes().hex() for g in got] == gpu
+            res["cpu_reference_schedule"] = cpu
+        return res
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+# ------------------------------------------------------------------ main
 def main():
     args = parse()
+    # stdout carries exactly one JSON line: anything native libraries print there (RCCL's
+    # version banner at communicator init) goes to stderr instead
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -306,6 +521,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(args.dist_backend)
+    transport = args.dedup or ("rccl" if args.dist_backend == "nccl" else "torch")
     import spacedrive_amd as sd
     from spacedrive_amd import dedup, synth
 
@@ -323,29 +539,34 @@ def main():
     batch = ctx.cas_batch(ext)
     d_hash = torch.empty(n * 32, dtype=torch.uint8, device=dev)
     d_valid = torch.from_numpy((sizes != 0).astype(np.uint8)).to(dev)  # size 0: no cas_id (mod.rs:80-88)
+    if transport == "rccl":
+        comm = dedup.make_comm(ctx)
+        rccl = dedup.RcclDedup(ctx, comm, dev, capacity=n * 5 // 4 + 4096)
+    else:
+        comm = rccl = None
+        gloo = world > 1 and dist.get_backend() == "gloo"
+        ascending = dedup.shards_ascend(n, start, None, "cpu" if gloo else dev)
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: {n} files ({batch.n_sampled} sampled), "
-        f"{batch.msg_bytes / 1e9:.2f} GB of messages, {batch.compressions / 1e9:.3f} G compressions")
+        f"{batch.msg_bytes / 1e9:.2f} GB of messages, {batch.compressions / 1e9:.3f} G compressions, "
+        f"dedup transport {transport}")
 
     stream = torch.cuda.current_stream()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    split = True  # separate launches: the dominant kernel is timed on its own
 
     def step(k=None):
         if k is not None:
             ev[k][0].record(stream)
-        if split:
-            batch.run_part(1, d_staged, d_hash, stream)  # k_cas_sampled
-            if k is not None:
-                ev[k][1].record(stream)
-            batch.run_part(2, d_staged, d_hash, stream)  # whole-file leaf + tree kernels
-        else:
-            batch.run(d_staged, d_hash, stream)
-            if k is not None:
-                ev[k][1].record(stream)
+        batch.run_part(1, d_staged, d_hash, stream)  # k_cas_sampled, timed on its own
+        if k is not None:
+            ev[k][1].record(stream)
+        batch.run_part(2, d_staged, d_hash, stream)  # k_whole_items + 2 x k_whole_merge8
         if k is not None:
             ev[k][2].record(stream)
-        r = dedup.dedup_shard(ctx, d_hash.view(n, 32), d_valid, n, start)
+        if rccl is not None:
+            r = rccl(d_hash.view(n, 32), d_valid, n, start, stream=stream)
+        else:
+            r = dedup.dedup_shard(ctx, d_hash.view(n, 32), d_valid, n, start, index_sorted=ascending)
         if k is not None:
             ev[k][3].record(stream)
         return r
@@ -367,8 +588,10 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
     def avg(a, b):
         return sum(ev[k][a].elapsed_time(ev[k][b]) for k in range(args.steps)) / args.steps
+
     hash_ms, sampled_ms, dedup_ms = avg(0, 2), avg(0, 1), avg(2, 3)
     recs, rep, n_groups, owners = res
     # every valid file lands on exactly one rank; groups never straddle ranks
@@ -378,7 +601,7 @@ def main():
         dist.all_reduce(tot)
     dedup_totals = {"records": int(tot[0]), "groups": int(tot[1]), "valid_files": int(tot[2]),
                     "records_on_rank0": int(recs.shape[0]),
-                    "objects_created_on_rank0": int((owners == recs[:, 1]).sum())}
+                    "objects_created_on_rank0": int((owners == recs[:, 1]).sum()), "transport": transport}
     assert dedup_totals["records"] == dedup_totals["valid_files"], dedup_totals
     files_total = n_total * args.steps
     value = files_total / elapsed
@@ -387,20 +610,15 @@ def main():
     # timed on its own with HIP events on its launch stream: 953 compressions x 672 VALU
     # lane-ops per sampled file; bytes = 57 352 B message read + 32 B hash written per file
     valu_peak = ctx.valu_peak()
-    if split:
-        dom_kernel, dom_ms = "k_cas_sampled", sampled_ms
-        dom_comp = 953 * batch.n_sampled
-        dom_bytes = batch.n_sampled * (SAMPLED_MSG + 32)
-    else:
-        dom_kernel, dom_ms = "hash phase", hash_ms
-        dom_comp, dom_bytes = batch.compressions, batch.msg_bytes + 32 * n
-    dom_valu = dom_comp * 672 / (dom_ms * 1e-3)
-    dom_gbps = dom_bytes / (dom_ms * 1e-3) / 1e9
+    dom_comp = 953 * batch.n_sampled
+    dom_bytes = batch.n_sampled * (SAMPLED_MSG + 32)
+    dom = valu_roof(dom_comp, sampled_ms)
+    dom_gbps = dom_bytes / (sampled_ms * 1e-3) / 1e9
     hash_bytes = batch.msg_bytes + 32 * n
-    hash_valu = batch.compressions * 672 / (hash_ms * 1e-3)
-    phase = ["k_cas_sampled", "k_whole_items", "k_whole_merge8"]
-    traffic = pmc_traffic(dom_kernel) if split else pmc_traffic(phase)
-
+    phase_roof = valu_roof(batch.compressions, hash_ms)
+    s_grid, w_grid = sampled_grid(batch.n_sampled), whole_grid(batch)
+    tr = pmc_traffic("k_cas_sampled", s_grid)
+    tr_w = pmc_traffic("k_whole_items", w_grid)
     out = {
         "metric": "cas_id files/sec (10M synthetic files) + checksum GB/s at 1/2/4/8 MI355X",
         "value": value, "unit": "files/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -408,33 +626,40 @@ def main():
         "vs_baseline": None, "dtype": "u32", "data": "synthetic (device-generated, SURVEY.md 8(d) generator)",
         "config": {"workload": f"10M-file library mixture (configs[0] mix: 60% <=100KiB whole-content, 40% sampled; "
                                f"10% dups, 1% sample twins), {n} files per GPU, step = hash shard + "
-                               f"cas_id-prefix all-to-all dedup + Object owners (chunk-of-100 rule)",
+                               f"cas_id-prefix all-to-all dedup ({transport}) + Object owners (chunk-of-100 rule)",
                    "files_per_gpu": n, "global_files": n_total, "parallelism": f"file-sharded x{world}"},
-        "roofline": {"bound": "valu", "achieved": dom_valu / 1e12, "peak": VALU_PEAK_TOPS,
-                     "unit": "T int32 VALU lane-ops/s", "frac": dom_valu / 1e12 / VALU_PEAK_TOPS,
-                     "traffic": traffic, "kernel": dom_kernel, "kernel_ms": dom_ms,
+        "roofline": {"bound": "valu", "achieved": dom["achieved"], "peak": VALU_PEAK_TOPS,
+                     "unit": "T int32 VALU lane-ops/s", "frac": dom["frac"], "peak_basis": PEAK_BASIS,
+                     "peak_full_rate": VALU_FULL_RATE_TOPS, "frac_full_rate": dom["frac_full_rate"],
+                     "traffic": tr["bytes"] if tr else None, "traffic_source": tr,
+                     "kernel": "k_cas_sampled", "kernel_ms": sampled_ms, "launch_grid": s_grid,
                      "algorithmic": {"compressions_per_launch": dom_comp, "lane_ops_per_compression": 672,
                                      "bytes_per_launch": dom_bytes,
                                      "per_unit": "sampled file: 953 compressions, 57352 B read + 32 B written"},
                      "measured_valu_peak": valu_peak / 1e12,
-                     "frac_of_measured_peak": dom_valu / valu_peak if valu_peak else None,
+                     "frac_of_measured_peak": dom["achieved"] * 1e12 / valu_peak if valu_peak else None,
                      "hbm": {"achieved": dom_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                              "frac": dom_gbps / HBM_PEAK_GBPS},
-                     "phase": {"kernels": phase, "ms": hash_ms, "compressions": batch.compressions,
-                               "bytes": hash_bytes, "achieved": hash_valu / 1e12,
-                               "frac": hash_valu / 1e12 / VALU_PEAK_TOPS,
-                               "traffic": pmc_traffic(phase)}},
-        "kernels": {"hash_ms": hash_ms, "sampled_ms": sampled_ms if split else None,
-                    "whole_ms": hash_ms - sampled_ms if split else None, "dedup_and_exchange_ms": dedup_ms,
+                     "phase": {"kernels": ["k_cas_sampled", "k_whole_items", "k_whole_merge8"], "ms": hash_ms,
+                               "compressions": batch.compressions, "bytes": hash_bytes,
+                               "achieved": phase_roof["achieved"], "frac": phase_roof["frac"],
+                               "frac_full_rate": phase_roof["frac_full_rate"],
+                               "whole_items_grid": w_grid, "whole_items_traffic": tr_w["bytes"] if tr_w else None}},
+        "kernels": {"hash_ms": hash_ms, "sampled_ms": sampled_ms, "whole_ms": hash_ms - sampled_ms,
+                    "dedup_and_exchange_ms": dedup_ms,
                     "host_overhead_ms": elapsed / args.steps * 1e3 - hash_ms - dedup_ms,
                     "sampled_files": batch.n_sampled, "whole_files": batch.n_whole},
         "dedup": dedup_totals,
     }
-    if rank == 0 and world == 1 and args.host_staged_files > 0:
-        out["host_staged"] = host_staged(ctx, ext, d_staged, batch, args.host_staged_files, dev)
-    if rank == 0 and world == 1 and args.file_backed_files > 0:
+    solo = rank == 0 and world == 1 and not args.no_extras
+    with_h2d = {}
+    if solo and args.host_staged_files > 0:
+        with_h2d["cas"] = host_staged(ctx, ext, d_staged, args.host_staged_files, dev, stream)
+    if solo and args.file_backed_files > 0:
         out["file_backed"] = file_backed(ctx, sizes, ext, d_staged, args.file_backed_files,
-                                         with_cpu=not args.no_cpu_baseline)
+                                         with_cpu=not args.no_cpu_baseline, latency_calls=args.latency_calls)
+        if "latency" in out["file_backed"]:
+            out["latency"] = out["file_backed"].pop("latency")
     del d_staged, recs, rep, owners
     torch.cuda.empty_cache()
 
@@ -449,29 +674,31 @@ def main():
         cb = ctx.checksum_batch(offs, [flen] * nf)
         d_sum = torch.empty(nf * 32, dtype=torch.uint8, device=dev)
         cb.run(d_data, d_sum, stream)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        e0.record(stream)
-        for _ in range(args.checksum_steps):
-            cb.run(d_data, d_sum, stream)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        ck_ms = e0.elapsed_time(e1) / args.checksum_steps
+        ck_ms = ev_ms(lambda: cb.run(d_data, d_sum, stream), stream, reps=args.checksum_steps)
         gbps = cb.total_bytes / (ck_ms * 1e-3) / 1e9
         tot = torch.tensor([gbps], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(tot)
+        roof = valu_roof(cb.compressions, ck_ms)
+        tr_ck = pmc_traffic("k_ck_leaf", cb.blocks * 256)
         out["checksum"] = {"GBps": float(tot.item()), "unit": "GB/s", "per_gpu_GBps": gbps, "ms_per_run": ck_ms,
                            "workload": f"configs[3]: {nf} x {flen >> 30} GiB files per GPU, full-file BLAKE3",
-                           "roofline": {"bound": "valu",
-                                        "achieved": cb.compressions * 672 / (ck_ms * 1e-3) / 1e12,
-                                        "peak": VALU_PEAK_TOPS, "unit": "T int32 VALU lane-ops/s",
-                                        "frac": cb.compressions * 672 / (ck_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS,
+                           "roofline": {"bound": "valu", "achieved": roof["achieved"], "peak": VALU_PEAK_TOPS,
+                                        "unit": "T int32 VALU lane-ops/s", "frac": roof["frac"],
+                                        "frac_full_rate": roof["frac_full_rate"], "peak_basis": PEAK_BASIS,
                                         "hbm": {"achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                                 "frac": gbps / HBM_PEAK_GBPS}},
-                           "traffic": pmc_traffic("k_ck_leaf")}
-        del d_data
+                           "launch_grid": cb.blocks * 256, "traffic": tr_ck["bytes"] if tr_ck else None}
+        del d_data, cb
         torch.cuda.empty_cache()
+
+    if solo and args.host_checksum_gib > 0:
+        with_h2d["checksum"] = checksum_host(ctx, args.host_checksum_gib, dev, stream)
+    if solo and args.file_checksum_mib > 0:
+        out["file_backed_checksum"] = file_checksums_leg(ctx, args.file_checksum_mib,
+                                                         with_cpu=not args.no_cpu_baseline, dev=dev)
+    if with_h2d:
+        out["with_h2d"] = with_h2d
 
     if world == 1 and args.config_files > 0:
         out["configs"] = {k: config_leg(ctx, k, args.config_files, args.config_reps, dev, stream, valu_peak)
@@ -483,11 +710,13 @@ def main():
             out["cpu_baseline"]["file_backed"] = dict(out["file_backed"]["cpu_reference_schedule"],
                                                       files=out["file_backed"]["files"],
                                                       note="reference read schedule from files (page cache)")
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
 
 
 if __name__ == "__main__":

@@ -162,8 +162,9 @@ int sd_cas_batch_run(sd_cas_ctx* ctx, const sd_cas_batch* batch, const uint8_t* 
 int sd_cas_batch_run_part(sd_cas_ctx* ctx, const sd_cas_batch* batch, int parts, const uint8_t* d_staged,
                           uint8_t* d_hash32, void* stream);
 /* Statistics of a prepared batch: [0] files, [1] sampled files, [2] whole files,
- * [3] chunks of whole files, [4] BLAKE3 compressions, [5] message bytes. */
-int sd_cas_batch_stats(const sd_cas_batch* batch, uint64_t out[6]);
+ * [3] chunks of whole files, [4] BLAKE3 compressions, [5] message bytes, [6] full-pair
+ * and [7] tail work items of the whole-file kernel (its launch shape). */
+int sd_cas_batch_stats(const sd_cas_batch* batch, uint64_t out[8]);
 
 /* ---------------------------------------------------------------- checksums */
 /* Full-file BLAKE3 (hash.rs:10-24) of n files that are byte ranges of one device

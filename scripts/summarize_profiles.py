@@ -22,6 +22,8 @@ CALIB_BYTES = 4 << 30
 CMD = os.environ.get("PROF_CMD", "python3 bench.py --steps 20 --warmup 3 --checksum-steps 5 --no-cpu-baseline "
                                     "--config-files 0 --file-backed-files 0")
 WARMUP = int(os.environ.get("PROF_WARMUP", "3"))
+PMC_CMD = os.environ.get("PMC_CMD", "python3 bench.py --steps 1 --warmup 0 --checksum-steps 1 --no-cpu-baseline "
+                                    "--config-files 1000000 --config-reps 1 --file-backed-files 0 --no-extras")
 
 
 def short(name):
@@ -30,9 +32,11 @@ def short(name):
 
 
 def pmc_rows(path):
+    """(kernel, grid size in work-items) -> counter -> per-launch values"""
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(path)):
-        agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        grid = int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)
+        agg[(short(r["Kernel_Name"]), grid)][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return agg
 
 
@@ -62,7 +66,7 @@ def main(tag):
                         "(clock ramp), i.e. it covers the launches bench.py times.\n\n")
                 f.write("| kernel | grid | calls | avg µs | steady avg µs | min µs |\n|---|---|---|---|---|---|\n")
                 for (k, g), v in sorted(shapes.items(), key=lambda kv: -sum(kv[1])):
-                    if not k.startswith(("k_cas", "k_whole", "k_ck")):
+                    if not k.startswith(("k_cas", "k_whole", "k_ck", "k_gb", "k_part", "k_owners")):
                         continue
                     st = v[WARMUP:] if len(v) > WARMUP else v
                     f.write(f"| `{k}` | {g} | {len(v)} | {sum(v) / len(v):.1f} | {sum(st) / len(st):.1f} | "
@@ -85,24 +89,28 @@ def main(tag):
                 if short(r["Kernel_Name"]) == "k_read_probe" and r["Counter_Name"] == "FETCH_SIZE"]
         for pattern, v in zip((0, 1, 2), vals):
             calib[pattern] = CALIB_BYTES / (v * 1024)
-    # k_cas_sampled (U = 2) reads 2 KiB per lane: probe pattern 2; whole leaf: pattern 1;
-    # checksum leaf (4 KiB per lane, same 16 B x 4 per block shape): pattern 2
-    use = {"k_cas_sampled": 2, "k_whole_leaf": 1, "k_whole_pair_leaf": 2, "k_whole_items": 2, "k_whole_full": 2,
-           "k_ck_leaf": 2}
+    # k_cas_sampled / k_whole_items full pairs read 2 KiB per lane (probe pattern 2); the
+    # checksum leaf 4 KiB per lane in the same 16 B x 4 per block shape (pattern 2)
+    use = {"k_cas_sampled": 2, "k_whole_items": 2, "k_ck_leaf": 2}
     kern = {}
-    for k, cs in pmc.items():
+    for (k, grid), cs in sorted(pmc.items()):
         if "FETCH_SIZE" not in cs:
             continue
         fac = calib.get(use.get(k, 0), 2.0)
         fetch = cs["FETCH_SIZE"]["per_launch"] * 1024
         write = cs.get("WRITE_SIZE", {}).get("per_launch", 0.0) * 1024
-        kern[k] = {"FETCH_SIZE_KB": cs["FETCH_SIZE"]["per_launch"],
-                   "WRITE_SIZE_KB": cs.get("WRITE_SIZE", {}).get("per_launch"),
-                   "fetch_factor": fac, "hbm_bytes_per_launch": fetch * fac + write,
-                   "counters": {c: v["per_launch"] for c, v in cs.items()}}
+        kern.setdefault(k, []).append({
+            "grid": grid, "launches": cs["FETCH_SIZE"]["launches"],
+            "FETCH_SIZE_KB": cs["FETCH_SIZE"]["per_launch"],
+            "WRITE_SIZE_KB": cs.get("WRITE_SIZE", {}).get("per_launch"),
+            "fetch_factor": fac, "hbm_bytes_per_launch": fetch * fac + write,
+            "counters": {c: v["per_launch"] for c, v in cs.items()}})
     out = {"tag": tag, "calibration_fetch_factor_by_pattern": calib,
-           "note": "hbm_bytes = FETCH_SIZE*1024*factor + WRITE_SIZE*1024; factor from read probes of a known "
-                   "4 GiB byte count (scripts/pmc_calib.py), 2.0 (MI355X_MICROARCH.md gfx950 rule) if absent",
+           "command": PMC_CMD,
+           "note": "per kernel and launch shape (grid = work-items); hbm_bytes = FETCH_SIZE*1024*factor + "
+                   "WRITE_SIZE*1024; factor from read probes of a known 4 GiB byte count (scripts/pmc_calib.py), "
+                   "2.0 (MI355X_MICROARCH.md gfx950 rule) if absent.  bench.py emits roofline.traffic only for a "
+                   "launch whose grid matches an entry here",
            "kernels": kern}
     json.dump(out, open(os.path.join(PROF, "pmc_summary.json"), "w"), indent=1)
     print("wrote profiles/pmc_summary.json")

@@ -605,11 +605,12 @@ int sd_cas_batch_run_part(sd_cas_ctx* ctx, const sd_cas_batch* batch, int parts,
     SD_GUARD_END
 }
 
-int sd_cas_batch_stats(const sd_cas_batch* b, uint64_t out[6]) {
+int sd_cas_batch_stats(const sd_cas_batch* b, uint64_t out[8]) {
     SD_GUARD_BEGIN
     if (!b || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
     out[0] = b->n; out[1] = b->n_sampled; out[2] = b->n_whole + b->n_long; out[3] = b->whole_chunks;
     out[4] = b->compressions; out[5] = b->msg_bytes;
+    out[6] = b->whole.full.size(); out[7] = b->whole.tail.size();
     return SD_OK;
     SD_GUARD_END
 }

@@ -160,10 +160,10 @@ class CasBatch:
         h = ctypes.c_void_p()
         check(lib().sd_cas_batch_create(ctx.handle, _ptr(self.extents), len(self.extents), ctypes.byref(h)))
         self.handle = h
-        st = np.zeros(6, np.uint64)
+        st = np.zeros(8, np.uint64)
         check(lib().sd_cas_batch_stats(h, _ptr(st)))
         (self.n, self.n_sampled, self.n_whole, self.whole_chunks, self.compressions,
-         self.msg_bytes) = (int(v) for v in st)
+         self.msg_bytes, self.full_items, self.tail_items) = (int(v) for v in st)
 
     def run(self, d_staged: torch.Tensor, d_hash32: torch.Tensor, stream=None) -> None:
         assert d_hash32.numel() >= 32 * self.n and d_staged.is_cuda and d_hash32.is_cuda
