@@ -185,10 +185,12 @@ int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
 int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
                  char* out_hex65);
 /* Drop-in: checksums of n files on disk -> 65-byte lowercase hex each (hash.rs:21-23);
- * status[n] required.  Each file is read as hash.rs reads it (1 MiB read calls until a
- * short one); small files are packed many per pinned window, large ones (or ones that
- * outgrow their room) streamed window by window, whatever their final length; two
- * windows alternate so host reads overlap the H2D copies and the kernels. */
+ * status[n] required.  Each file is read as hash.rs reads it: 1 MiB read calls until a
+ * short one -- for a regular file its bytes up to EOF, read with parallel preads
+ * ("read_threads"); a pipe or device sequentially.  Small files are packed many per
+ * pinned window, large ones (or ones that grow while read) streamed window by window,
+ * whatever their final length; two windows alternate so host reads overlap the H2D
+ * copies and the kernels. */
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65,
                       int32_t* status);
 
@@ -307,7 +309,8 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
                            uint8_t* d_hash32, int iters, void* stream, float* ms_total);
 /* Process-wide knobs (results are identical for every value): "coalesce_window_us"
  * (200), "coalesce_max" (4096) and "latency_cpu_max" (16) of the latency path;
- * "files_window_mb" (32) of sd_cas_ids_files; "dedup_variant" (sd_dedup_group) 0 =
+ * "files_window_mb" (32) of sd_cas_ids_files; "read_threads" (16) of sd_file_checksums;
+ * "dedup_variant" (sd_dedup_group) 0 =
  * rocPRIM radix sort, 1 = LDS buckets with the radix sort as overflow fallback (default).
  * Unknown keys fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);

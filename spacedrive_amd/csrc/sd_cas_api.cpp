@@ -446,8 +446,9 @@ int sd_ctx_device(const sd_cas_ctx* ctx) { return ctx->device; }
 
 // ------------------------------------------------------------------ tuning knobs
 // defaults: 200 us coalescing window, 4096-request batches, 32 MiB file windows, LDS-bucket
-// dedup grouping, single-file calls on the CPU while fewer than 16 are in flight
-static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}};
+// dedup grouping, single-file calls on the CPU while fewer than 16 are in flight, 16 reader
+// threads for sd_file_checksums
+static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}};
 int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
 
 // ============================================================================ C ABI
@@ -457,7 +458,7 @@ int sd_cas_set_tuning(const char* key, int value) {
     SD_GUARD_BEGIN
     if (!key) throw sd_failure(SD_ERR_INVALID, "null key");
     static const char* names[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max", "files_window_mb",
-                                               "dedup_variant", "latency_cpu_max"};
+                                               "dedup_variant", "latency_cpu_max", "read_threads"};
     for (int k = 0; k < SD_TUNE_NKEYS; k++)
         if (strcmp(key, names[k]) == 0) {
             g_tune[k].store(value, std::memory_order_relaxed);
@@ -839,20 +840,32 @@ int sd_checksum_batch_stats(const sd_checksum_batch* b, uint64_t out[4]) {
 }
 
 // file_checksum (hash.rs:10-24) for n paths.  Each file is read as the reference reads it:
-// one read() of 1 MiB at a time until one returns fewer (hash.rs:15-19) -- the file's
-// length at stat time only picks the route.  Files that fit are packed (64-B aligned)
-// into the current slot's pinned window, one batch per window; while the GPU hashes one
-// slot's window the host reads the next into the other.  A file too large for a window,
-// or one that outgrows the room it was given, is streamed window by window (Streamer),
-// starting with the bytes already read.
+// hash.rs's 1 MiB read calls until one returns fewer.  For a regular file those reads are
+// exactly its bytes up to EOF, so regular files are read with parallel preads on the
+// context's stager pool ("read_threads"); anything else (a pipe, a device) with the
+// literal sequential loop.  Small regular files are packed (64-B aligned) into the current
+// slot's pinned window by their stat length -- one batch per window, read in parallel,
+// each file probed past its length in case it grew --; while the GPU hashes one slot's
+// window the host reads the next into the other.  Larger files, files that grew, and
+// non-regular files stream window by window (Streamer), whatever their final length.
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65, int32_t* status) {
     SD_GUARD_BEGIN
     if (!ctx || (n && (!paths || !out_hex65 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
     ctx->bind();
     constexpr uint64_t W = Streamer::W;
-    constexpr uint64_t RD = MsgSource::CHECKSUM_READ;  // hash.rs:8 BLOCK_LEN
+    std::shared_ptr<StagePool> pool = ctx->stage_pool(std::max(1, std::min(64, tuning_get(SD_TUNE_READ_THREADS))));
     SlotPair slots(ctx);
     Streamer::prepare(slots);
+    // stat every file in parallel: its length picks the route (regular files only)
+    std::vector<uint64_t> hint(n, 0);
+    std::vector<uint8_t> regular(n, 0);
+    pool->run(n, [&](size_t i) {
+        struct stat st;
+        if (stat(paths[i], &st) == 0 && S_ISREG(st.st_mode)) {
+            hint[i] = (uint64_t)st.st_size;
+            regular[i] = 1;
+        }
+    });
     struct Pending {
         std::vector<size_t> files;  // files whose hashes land in this slot's host_hashes
         bool busy = false;
@@ -869,101 +882,107 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
         pend[k].files.clear();
         pend[k].busy = false;
     };
-    // the pack being filled lives in slot `cur`'s window
-    std::vector<size_t> pack;
-    std::vector<uint64_t> pack_off, pack_len;
-    uint64_t pack_end = 0;
-    bool pack_open = false;
-    auto open_pack = [&]() {
-        if (pack_open) return;
-        harvest(cur);
-        pack_open = true;
-        pack_end = 0;
-    };
-    auto submit_pack = [&]() {
-        if (!pack_open) return;
-        pack_open = false;
-        const int k = cur;
-        cur ^= 1;
-        if (pack.empty()) return;
-        Slot& sl = slots[k];
-        plan_checksum_batch(&pack_batch[k], pack_off.data(), pack_len.data(), pack.size(), sl.stream);
-        sl.hashes.ensure(pack.size() * 32);
-        sl.host_hashes.ensure(pack.size() * 32);
-        HIP_CHECK(hipMemcpyAsync(sl.staged.p, sl.window.p, pack_end + 64, hipMemcpyHostToDevice, sl.stream));
-        run_checksum_batch(&pack_batch[k], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
-        HIP_CHECK(
-            hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, pack.size() * 32, hipMemcpyDeviceToHost, sl.stream));
-        pend[k].files = pack;
-        pend[k].busy = true;
-        pack.clear();
-        pack_off.clear();
-        pack_len.clear();
-    };
-    auto stream_file = [&](size_t i, MsgSource& src, uint64_t hint) {
-        submit_pack();
+    // one file streamed (sequential reads, or parallel preads for a regular file)
+    auto stream_file = [&](size_t i) {
         harvest(0);
         harvest(1);
-        uint8_t h[32];
-        status[i] = streamer.hash(slots, cur, src, hint, h);
-        if (status[i] == SD_FILE_OK) to_hex(h, 32, out_hex65 + i * 65);
-    };
-    std::vector<uint8_t> spill;
-    for (size_t i = 0; i < n; i++) {
-        status[i] = SD_FILE_OK;
         const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);  // hash.rs:11
         if (fd < 0) {
             status[i] = io_status(errno);
-            continue;
+            return;
         }
-        struct stat stt;
-        const uint64_t hint = fstat(fd, &stt) == 0 ? (uint64_t)stt.st_size : 0;
+        struct stat st;
+        const bool reg = fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
         MsgSource src(fd, MsgSource::CHECKSUM_READS);
-        if (hint + RD + 128 > W / 2) {  // large: stream it
-            stream_file(i, src, hint);
+        if (reg) src.set_parallel(pool.get());
+        uint8_t h[32];
+        try {
+            status[i] = streamer.hash(slots, cur, src, reg ? (uint64_t)st.st_size : 0, h);
+        } catch (...) {
             close(fd);
-            continue;
-        }
-        open_pack();
-        if (pack_end + align_up(hint, RD) + RD + 64 > W) {  // this pack is full: start the next
-            submit_pack();
-            open_pack();
-        }
-        uint8_t* win = slots[cur].window.u8();
-        const uint64_t off0 = pack_end;
-        uint64_t got = 0;
-        bool overflowed = false;
-        for (;;) {  // hash.rs:14-20, one 1 MiB read per iteration, straight into the window
-            if (off0 + got + RD + 64 > W) {
-                overflowed = true;
-                break;
-            }
-            const uint64_t r = src.read(win + off0 + got, RD);
-            got += r;
-            if (src.err || src.done) break;
-        }
-        if (src.err) {
-            status[i] = io_status(src.err);
-            close(fd);
-            continue;
-        }
-        if (overflowed) {  // outgrew its room: stream it, starting with the bytes read so far
-            spill.assign(win + off0, win + off0 + got);
-            src.set_pending(spill.data(), spill.size());
-            stream_file(i, src, got + RD);
-            close(fd);
-            continue;
+            throw;
         }
         close(fd);
-        memset(win + off0 + got, 0, align_up(got, 64) + 64 - got);
+        if (status[i] == SD_FILE_OK) to_hex(h, 32, out_hex65 + i * 65);
+    };
+    // the pack: regular files laid out by their stat lengths in slot `cur`'s window
+    std::vector<size_t> pack, grew;
+    std::vector<uint64_t> pack_off, pack_len;
+    uint64_t pack_end = 0;
+    auto submit_pack = [&]() {
+        if (pack.empty()) return;
+        const int k = cur;
+        harvest(k);  // slot k's previous batch is done: its window is free
+        Slot& sl = slots[k];
+        uint8_t* win = sl.window.u8();
+        pool->run(pack.size(), [&](size_t q) {
+            const size_t i = pack[q];
+            const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+            if (fd < 0) {
+                status[i] = io_status(errno);
+                return;
+            }
+            const int64_t got = pread_full(fd, win + pack_off[q], hint[i], 0);
+            uint8_t probe;
+            const int64_t more = got == (int64_t)hint[i] ? pread_full(fd, &probe, 1, hint[i]) : 0;
+            close(fd);
+            if (got < 0 || more < 0) {
+                status[i] = io_status((int)-(got < 0 ? got : more));
+            } else if (more > 0) {
+                status[i] = SD_FILE_CHANGED;  // grew since stat: stream it below
+            } else {
+                status[i] = SD_FILE_OK;
+                pack_len[q] = (uint64_t)got;  // shrank: hash.rs stops at EOF
+                memset(win + pack_off[q] + got, 0, align_up(got, 64) - got);
+            }
+        });
+        std::vector<uint64_t> offs, lens;
+        std::vector<size_t> ok;
+        for (size_t q = 0; q < pack.size(); q++) {
+            if (status[pack[q]] == SD_FILE_OK) {
+                ok.push_back(pack[q]);
+                offs.push_back(pack_off[q]);
+                lens.push_back(pack_len[q]);
+            } else if (status[pack[q]] == SD_FILE_CHANGED) {
+                grew.push_back(pack[q]);
+            }
+        }
+        pack.clear();
+        pack_off.clear();
+        pack_len.clear();
+        const uint64_t span = pack_end;
+        pack_end = 0;
+        if (ok.empty()) return;
+        cur ^= 1;
+        plan_checksum_batch(&pack_batch[k], offs.data(), lens.data(), ok.size(), sl.stream);
+        sl.hashes.ensure(ok.size() * 32);
+        sl.host_hashes.ensure(ok.size() * 32);
+        HIP_CHECK(hipMemcpyAsync(sl.staged.p, win, span + 64, hipMemcpyHostToDevice, sl.stream));
+        run_checksum_batch(&pack_batch[k], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
+        HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, ok.size() * 32, hipMemcpyDeviceToHost, sl.stream));
+        pend[k].files = std::move(ok);
+        pend[k].busy = true;
+    };
+    for (size_t i = 0; i < n; i++) {
+        status[i] = SD_FILE_OK;
+        if (!regular[i] || hint[i] + 128 > W / 2) {  // a pipe / device / unreadable path, or large
+            submit_pack();
+            stream_file(i);
+            continue;
+        }
+        if (pack_end + align_up(hint[i], 64) + 64 > W) submit_pack();
         pack.push_back(i);
-        pack_off.push_back(off0);
-        pack_len.push_back(got);
-        pack_end = align_up(off0 + got, 64);
+        pack_off.push_back(pack_end);
+        pack_len.push_back(hint[i]);
+        pack_end = align_up(pack_end + hint[i], 64);
     }
     submit_pack();
     harvest(0);
     harvest(1);
+    for (size_t i : grew) {
+        status[i] = SD_FILE_OK;
+        stream_file(i);
+    }
     return SD_OK;
     SD_GUARD_END
 }

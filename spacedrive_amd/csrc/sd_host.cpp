@@ -223,6 +223,20 @@ struct Fd {
 
 }  // namespace
 
+int64_t pread_full(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
+    uint64_t got = 0;
+    while (got < n) {
+        const ssize_t r = pread(fd, dst + got, n - got, (off_t)(off + got));
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return -(int64_t)errno;
+        }
+        if (r == 0) break;
+        got += (uint64_t)r;
+    }
+    return (int64_t)got;
+}
+
 int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged) {
     uint8_t* dst = staged + e.msg_offset;
     const uint64_t size = e.size;
@@ -287,6 +301,7 @@ uint64_t MsgSource::read(uint8_t* dst, uint64_t n) {
         got += k;
     }
     if (done || err) return got;
+    if (pool_ && mode_ == CHECKSUM_READS && got < n) return got + read_parallel(dst + got, n - got);
     if (mode_ == READ_TO_EOF) {
         while (got < n) {
             const ssize_t r = read_once(fd_, dst + got, n - got);
@@ -300,8 +315,10 @@ uint64_t MsgSource::read(uint8_t* dst, uint64_t n) {
             }
             got += (uint64_t)r;
         }
+        file_pos_ += got;
         return got;
     }
+    const uint64_t got0 = got;
     while (got < n) {  // hash.rs:14-20
         const uint64_t want = std::min<uint64_t>(CHECKSUM_READ, n - got);
         const ssize_t r = read_once(fd_, dst + got, want);
@@ -315,5 +332,29 @@ uint64_t MsgSource::read(uint8_t* dst, uint64_t n) {
             break;
         }
     }
+    file_pos_ += got - got0;
+    return got;
+}
+
+uint64_t MsgSource::read_parallel(uint8_t* dst, uint64_t n) {
+    const uint64_t pieces = (n + CHECKSUM_READ - 1) / CHECKSUM_READ;
+    std::vector<int64_t> r(pieces, 0);
+    pool_->run(pieces, [&](size_t k) {
+        const uint64_t len = std::min<uint64_t>(CHECKSUM_READ, n - k * CHECKSUM_READ);
+        r[k] = pread_full(fd_, dst + k * CHECKSUM_READ, len, file_pos_ + k * CHECKSUM_READ);
+    });
+    uint64_t got = 0;
+    for (uint64_t k = 0; k < pieces; k++) {
+        if (r[k] < 0) {
+            err = (int)-r[k];
+            break;
+        }
+        got += (uint64_t)r[k];
+        if ((uint64_t)r[k] != CHECKSUM_READ) {  // the first short piece is EOF
+            done = true;
+            break;
+        }
+    }
+    file_pos_ += got;
     return got;
 }

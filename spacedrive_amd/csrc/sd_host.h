@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/sd_cas.h"
+#include "stage_pool.h"
 
 // ------------------------------------------------------------------ errors
 struct sd_failure : std::runtime_error {
@@ -119,6 +120,8 @@ void plan_checksum(CkPlan& p, const uint64_t* offsets, const uint64_t* lens, siz
 //     (SHORT_READ past EOF), then the footer at seek(End(-8192)) -- the file's real end,
 //     EINVAL when it is shorter than 8192 bytes.
 int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged);
+// pread until n bytes or EOF; returns the count, or -errno
+int64_t pread_full(int fd, uint8_t* dst, uint64_t n, uint64_t off);
 
 // A message read front to back from a file: optional le64 prefix (a cas message's size
 // header), optional bytes already read from the file, then the file itself.
@@ -131,11 +134,16 @@ public:
     static constexpr uint64_t CHECKSUM_READ = SD_CK_BLOCK;
     MsgSource(int fd, Mode m) : fd_(fd), mode_(m) {}
     void set_prefix_le64(uint64_t v);
-    // bytes already taken from the file (whole 1 MiB reads in CHECKSUM_READS mode)
+    // the file's first n bytes, already taken from it (whole 1 MiB reads in CHECKSUM_READS mode)
     void set_pending(const uint8_t* p, uint64_t n) {
         pend_ = p;
         pend_len_ = n;
+        file_pos_ = n;
     }
+    // A regular file (S_ISREG) read in CHECKSUM_READS mode: hash.rs's 1 MiB reads until a
+    // short one return exactly the bytes up to EOF, so each window is filled with 1 MiB
+    // preads at their offsets in parallel on `pool`, and ends at the first short piece.
+    void set_parallel(StagePool* pool) { pool_ = pool; }
     // Writes up to n message bytes to dst and returns the count; fewer than n only at the
     // end of the message (done) or on an error (err = errno).  CHECKSUM_READS: n is a
     // multiple of 1 MiB.
@@ -144,8 +152,11 @@ public:
     int err = 0;
 
 private:
+    uint64_t read_parallel(uint8_t* dst, uint64_t n);
     int fd_;
     Mode mode_;
+    StagePool* pool_ = nullptr;
+    uint64_t file_pos_ = 0;  // bytes taken from the file so far
     uint8_t prefix_[8] = {};
     uint32_t prefix_len_ = 0, prefix_pos_ = 0;
     const uint8_t* pend_ = nullptr;

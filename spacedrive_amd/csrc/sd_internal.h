@@ -13,7 +13,8 @@ enum sd_tune_key {
     SD_TUNE_FILES_WINDOW_MB = 2,  // sd_cas_ids_files: pinned staging window (MiB)
     SD_TUNE_DEDUP_VARIANT = 3,    // sd_dedup_group: 0 = radix sort, 1 = LDS buckets (radix on overflow)
     SD_TUNE_LATENCY_CPU_MAX = 4,  // latency path: hash on the CPU while fewer calls are in flight
-    SD_TUNE_NKEYS = 5
+    SD_TUNE_READ_THREADS = 5,     // sd_file_checksums: parallel preads of regular files
+    SD_TUNE_NKEYS = 6
 };
 int tuning_get(int key);
 // the device a context was created on
