@@ -19,11 +19,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
 CALIB_BYTES = 4 << 30
-CMD = os.environ.get("PROF_CMD", "python3 bench.py --steps 20 --warmup 3 --checksum-steps 5 --no-cpu-baseline "
-                                    "--config-files 0 --file-backed-files 0")
+CMD = os.environ.get("PROF_CMD", "python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extras")
 WARMUP = int(os.environ.get("PROF_WARMUP", "3"))
 PMC_CMD = os.environ.get("PMC_CMD", "python3 bench.py --steps 1 --warmup 0 --checksum-steps 1 --no-cpu-baseline "
-                                    "--config-files 1000000 --config-reps 1 --file-backed-files 0 --no-extras")
+                                    "--no-extras --config-reps 1 --warm-ms 0")
 
 
 def short(name):
