@@ -31,11 +31,17 @@ def short(name):
 
 
 def pmc_rows(path):
-    """(kernel, grid size in work-items) -> counter -> per-launch values"""
+    """(kernel, grid size in work-items) -> counter -> per-launch values; the launch
+    duration under the counter pass goes in as the pseudo-counter "DURATION_NS"."""
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    seen = set()
     for r in csv.DictReader(open(path)):
         grid = int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)
-        agg[(short(r["Kernel_Name"]), grid)][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        key = (short(r["Kernel_Name"]), grid)
+        agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if r.get("Start_Timestamp") and (key, r["Dispatch_Id"]) not in seen:
+            seen.add((key, r["Dispatch_Id"]))
+            agg[key]["DURATION_NS"].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
     return agg
 
 
@@ -113,6 +119,29 @@ def main(tag):
            "kernels": kern}
     json.dump(out, open(os.path.join(PROF, "pmc_summary.json"), "w"), indent=1)
     print("wrote profiles/pmc_summary.json")
+    # the hashing and dedup kernels: HBM bytes, clock and VALU issue per launch shape
+    with open(os.path.join(PROF, f"{tag}_pmc.md"), "w") as f:
+        f.write(f"# rocprofv3 PMC per launch shape ({tag})\n\nCommand of every pass: `rocprofv3 --pmc <group> -- "
+                f"{PMC_CMD}` (scripts/profile.sh); one counter group per pass.  HBM bytes = FETCH_SIZE x 1024 x "
+                "calibrated factor + WRITE_SIZE x 1024 (factor from `scripts/pmc_calib.py`'s 4 GiB read probes: "
+                f"{ {k: round(v, 4) for k, v in calib.items()} }).  MHz = GRBM_GUI_ACTIVE / 8 XCDs / launch duration "
+                "in the counter pass (GRBM_GUI_ACTIVE sums the 8 XCDs; a lower bound on the shader clock); lane-ops/clk/CU "
+                "= SQ_INSTS_VALU x 64 lanes / (GUI cycles / 8 x 256 CUs): 64 is the 3-operand issue bound (one wave64 "
+                "op per 4 cycles on each of the 4 SIMDs), 128 the guide's full rate.\n\n")
+        f.write("| kernel | grid | HBM GB/launch | VALU wave-insts | GUI cycles | MHz | lane-ops/clk/CU |\n"
+                "|---|---|---|---|---|---|---|\n")
+        for k, lst in sorted(kern.items()):
+            if not k.startswith(("k_cas", "k_whole", "k_ck", "k_gb", "k_part", "k_owners", "rccl")):
+                continue
+            for e in lst:
+                c = e["counters"]
+                gui, dur, valu = c.get("GRBM_GUI_ACTIVE"), c.get("DURATION_NS"), c.get("SQ_INSTS_VALU")
+                mhz = gui / 8 / dur * 1e3 if gui and dur else None
+                ipc = valu * 64 / (gui / 8 * 256) if gui and valu else None
+                f.write(f"| `{k}` | {e['grid']} | {e['hbm_bytes_per_launch'] / 1e9:.4g} | "
+                        f"{'%.4g' % valu if valu is not None else '-'} | {'%.4g' % gui if gui is not None else '-'} | "
+                        f"{'%.0f' % mhz if mhz else '-'} | {'%.1f' % ipc if ipc else '-'} |\n")
+    print(f"wrote profiles/{tag}_pmc.md")
 
 
 if __name__ == "__main__":

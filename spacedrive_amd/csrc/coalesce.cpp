@@ -14,7 +14,6 @@
 // call.  Requests that arrive meanwhile form the next batch, so a busy watcher is served
 // at batch throughput and an idle one at CPU latency.  Each caller blocks only on its own
 // request.
-#include <hip/hip_runtime.h>
 #include <string.h>
 
 #include <algorithm>
@@ -26,7 +25,7 @@
 #include <thread>
 #include <vector>
 
-#include "sd_internal.h"
+#include "sd_host.h"
 
 struct sd_coalescer {
     struct Req {

@@ -33,19 +33,6 @@
 #include "stage_pool.h"
 
 namespace {
-thread_local std::string g_err;
-}  // namespace
-
-void sd_set_err(const char* fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    g_err = buf;
-}
-
-namespace {
 
 #define HIP_CHECK(expr)                                                                              \
     do {                                                                                             \
@@ -444,33 +431,8 @@ int32_t cas_overflow(SlotPair& sl, int& cur, Streamer& st, const char* path, uin
 
 int sd_ctx_device(const sd_cas_ctx* ctx) { return ctx->device; }
 
-// ------------------------------------------------------------------ tuning knobs
-// defaults: 200 us coalescing window, 4096-request batches, 32 MiB file windows, LDS-bucket
-// dedup grouping, single-file calls on the CPU while fewer than 16 are in flight, 16 reader
-// threads for sd_file_checksums
-static std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}};
-int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
-
 // ============================================================================ C ABI
 extern "C" {
-
-int sd_cas_set_tuning(const char* key, int value) {
-    SD_GUARD_BEGIN
-    if (!key) throw sd_failure(SD_ERR_INVALID, "null key");
-    static const char* names[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max", "files_window_mb",
-                                               "dedup_variant", "latency_cpu_max", "read_threads"};
-    for (int k = 0; k < SD_TUNE_NKEYS; k++)
-        if (strcmp(key, names[k]) == 0) {
-            g_tune[k].store(value, std::memory_order_relaxed);
-            return SD_OK;
-        }
-    throw sd_failure(SD_ERR_INVALID, std::string("unknown tuning key ") + key);
-    SD_GUARD_END
-}
-
-int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }
-
-const char* sd_cas_last_error(void) { return g_err.c_str(); }
 
 int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
     SD_GUARD_BEGIN

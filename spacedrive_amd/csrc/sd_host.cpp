@@ -5,10 +5,51 @@
 
 #include <errno.h>
 #include <fcntl.h>
+#include <stdarg.h>
+#include <stdio.h>
 #include <string.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+
+// ------------------------------------------------------------------ errors, knobs
+namespace {
+thread_local std::string g_err;
+// defaults: 200 us coalescing window, 4096-request batches, 32 MiB file windows, LDS-bucket
+// dedup grouping, single-file calls on the CPU while fewer than 16 are in flight, 16 reader
+// threads for sd_file_checksums
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}};
+const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max", "files_window_mb",
+                                               "dedup_variant",      "latency_cpu_max", "read_threads"};
+}  // namespace
+
+void sd_set_err(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
+
+extern "C" {
+const char* sd_cas_last_error(void) { return g_err.c_str(); }
+int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }
+int sd_cas_set_tuning(const char* key, int value) {
+    SD_GUARD_BEGIN
+    if (!key) throw sd_failure(SD_ERR_INVALID, "null key");
+    for (int k = 0; k < SD_TUNE_NKEYS; k++)
+        if (strcmp(key, TUNE_NAMES[k]) == 0) {
+            g_tune[k].store(value, std::memory_order_relaxed);
+            return SD_OK;
+        }
+    throw sd_failure(SD_ERR_INVALID, std::string("unknown tuning key ") + key);
+    SD_GUARD_END
+}
+}  // extern "C"
 
 // ------------------------------------------------------------------ planners
 sd_extent plan_extent(uint64_t size, uint64_t off) {

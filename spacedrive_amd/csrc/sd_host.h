@@ -43,6 +43,26 @@ void sd_set_err(const char* fmt, ...);
         return SD_ERR_INTERNAL;                        \
     }
 
+// process-wide tuning knobs (sd_cas_set_tuning, defined in sd_host.cpp); read at call time
+enum sd_tune_key {
+    SD_TUNE_COALESCE_US = 0,      // latency path: GPU batch collection window (us)
+    SD_TUNE_COALESCE_MAX = 1,     // latency path: largest coalesced GPU batch
+    SD_TUNE_FILES_WINDOW_MB = 2,  // sd_cas_ids_files: pinned staging window (MiB)
+    SD_TUNE_DEDUP_VARIANT = 3,    // sd_dedup_group: 0 = radix sort, 1 = LDS buckets (radix on overflow)
+    SD_TUNE_LATENCY_CPU_MAX = 4,  // latency path: hash on the CPU while fewer calls are in flight
+    SD_TUNE_READ_THREADS = 5,     // sd_file_checksums: parallel preads of regular files
+    SD_TUNE_NKEYS = 6
+};
+int tuning_get(int key);
+
+// latency path (coalesce.cpp): single-file calls, CPU route or coalesced GPU batches
+struct sd_coalescer;
+sd_coalescer* coalescer_create(sd_cas_ctx* ctx);
+void coalescer_destroy(sd_coalescer* c);
+int coalescer_submit(sd_coalescer* c, int kind, const char* path, uint64_t size, char* out, int32_t* status,
+                     std::string* err);
+void coalescer_stats(sd_coalescer* c, uint64_t out[4]);
+
 inline uint64_t sd_align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 // sd_file_status IO_ERROR with the errno in the high 16 bits
 inline int32_t io_status(int err) { return (int32_t)(SD_FILE_IO_ERROR | ((uint32_t)(err & 0xFFFF) << 16)); }

@@ -6,28 +6,8 @@
 #include "../../include/sd_cas.h"
 #include "sd_host.h"
 
-// process-wide tuning knobs (sd_cas_set_tuning); read at call time
-enum sd_tune_key {
-    SD_TUNE_COALESCE_US = 0,      // latency path: GPU batch collection window (us)
-    SD_TUNE_COALESCE_MAX = 1,     // latency path: largest coalesced GPU batch
-    SD_TUNE_FILES_WINDOW_MB = 2,  // sd_cas_ids_files: pinned staging window (MiB)
-    SD_TUNE_DEDUP_VARIANT = 3,    // sd_dedup_group: 0 = radix sort, 1 = LDS buckets (radix on overflow)
-    SD_TUNE_LATENCY_CPU_MAX = 4,  // latency path: hash on the CPU while fewer calls are in flight
-    SD_TUNE_READ_THREADS = 5,     // sd_file_checksums: parallel preads of regular files
-    SD_TUNE_NKEYS = 6
-};
-int tuning_get(int key);
 // the device a context was created on
 int sd_ctx_device(const sd_cas_ctx* ctx);
-// latency path (coalesce.cpp)
-#include <string>
-struct sd_coalescer;
-sd_coalescer* coalescer_create(sd_cas_ctx* ctx);
-void coalescer_destroy(sd_coalescer* c);
-int coalescer_submit(sd_coalescer* c, int kind, const char* path, uint64_t size, char* out, int32_t* status,
-                     std::string* err);
-void coalescer_stats(sd_coalescer* c, uint64_t out[4]);
-
 namespace sdk {
 hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const uint32_t* idx, uint32_t n,
                               uint32_t* out, hipStream_t s);
