@@ -16,7 +16,9 @@ import os
 import torch  # noqa: F401  -- must precede the CDLL load (one HIP runtime per process)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsdcas.so")
+# SD_CAS_LIB: an alternative build of the same library (the sanitizer build of
+# scripts/sanitize_pytest.sh); the default is the in-tree gfx950 build
+LIB_PATH = os.environ.get("SD_CAS_LIB") or os.path.join(HERE, "libsdcas.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "sd_cas.h")
 
 SD_OK = 0

@@ -127,7 +127,11 @@ struct sd_coalescer {
             if (q.empty() && stop) return;
             const size_t cap = (size_t)std::max(1, tuning_get(SD_TUNE_COALESCE_MAX));
             const auto deadline =
-                std::chrono::steady_clock::now() + std::chrono::microseconds(std::max(0, tuning_get(SD_TUNE_COALESCE_US)));
+                // system_clock: libstdc++ waits on it with pthread_cond_timedwait, which every
+                // ThreadSanitizer runtime intercepts (a steady_clock wait becomes
+                // pthread_cond_clockwait, which GCC 11's does not: false "double lock"
+                // reports); a wall-clock step can only shorten or stretch one window
+                std::chrono::system_clock::now() + std::chrono::microseconds(std::max(0, tuning_get(SD_TUNE_COALESCE_US)));
             while (!stop && q.size() < cap && work.wait_until(g, deadline) != std::cv_status::timeout) {
             }
             std::vector<Req*> cas, ck;
