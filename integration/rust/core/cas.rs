@@ -8,8 +8,9 @@ use tokio::{io, task::spawn_blocking};
 // contract now: SD_SAMPLE_COUNT / SD_SAMPLE_SIZE / SD_HEADER_OR_FOOTER_SIZE /
 // SD_MINIMUM_FILE_SIZE in include/sd_cas.h, checked against cas.rs:10-21 by the oracle tests.
 
-/// Unchanged signature (cas.rs:23).  One file: the library coalesces concurrent callers
-/// (watcher, non_indexed) into GPU batches.
+/// Unchanged signature (cas.rs:23).  One file (watcher, non_indexed): the library's
+/// latency policy hashes it on the CPU while few calls are in flight and coalesces
+/// concurrent callers into GPU batches beyond that; without a device, the CPU path.
 pub async fn generate_cas_id(path: impl AsRef<Path>, size: u64) -> Result<String, io::Error> {
     let p: PathBuf = path.as_ref().to_path_buf();
     spawn_blocking(move || sd_cas_sys::cas_id_blocking(&p, size))

@@ -1,5 +1,6 @@
 // Replacement body of core/src/object/validation/hash.rs (reference :1-24): same
-// signature and 64-hex output, hashing on the GPU (sd_file_checksum_path).
+// signature and 64-hex output, the same reads (1 MiB read calls until a short one), hashed
+// by libsdcas (sd_file_checksum_path; the CPU path when the node has no gfx950 device).
 use std::path::{Path, PathBuf};
 
 use tokio::{io, task::spawn_blocking};
