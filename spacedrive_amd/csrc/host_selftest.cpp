@@ -237,24 +237,33 @@ void test_readers() {
     for (size_t n : {0ul, 1ul, (1ul << 20) - 1, 1ul << 20, (1ul << 20) + 1, (5ul << 20) + 3}) {
         const auto data = content(n + 1, n);
         const std::string p = write_file("rd" + std::to_string(n), data);
-        for (int par = 0; par < 2; par++) {
-            const int fd = open(p.c_str(), O_RDONLY);
-            MsgSource src(fd, MsgSource::CHECKSUM_READS);
-            if (par) src.set_parallel(&pool);
-            std::vector<uint8_t> got, win(2 << 20);
-            for (;;) {
-                const uint64_t k = src.read(win.data(), win.size());
-                got.insert(got.end(), win.begin(), win.begin() + k);
-                if (src.done || src.err) break;
-                CHECK(k == win.size());
+        // par: parallel preads; hint: the EOF probe at the stat length (exact, or stale by
+        // one byte short, as for a file that grew after its stat)
+        for (int par = 0; par < 2; par++)
+            for (int hint = 0; hint < 3; hint++) {
+                const int fd = open(p.c_str(), O_RDONLY);
+                MsgSource src(fd, MsgSource::CHECKSUM_READS);
+                if (par) src.set_parallel(&pool);
+                if (hint) src.set_eof_hint(hint == 1 ? n : (n ? n - 1 : 0));
+                std::vector<uint8_t> got, win(2 << 20);
+                int reads = 0;
+                for (;;) {
+                    const uint64_t k = src.read(win.data(), win.size());
+                    reads++;
+                    got.insert(got.end(), win.begin(), win.begin() + k);
+                    if (src.done || src.err) break;
+                    CHECK(k == win.size());
+                }
+                close(fd);
+                CHECK(src.err == 0 && got == data);
+                // an exact hint ends a window-multiple file with its last full window
+                if (hint == 1) CHECK(reads == (int)(n / win.size()) + (n % win.size() || n == 0 ? 1 : 0));
             }
-            close(fd);
-            CHECK(src.err == 0 && got == data);
-        }
-        // READ_TO_EOF with the le64 prefix (a cas message's size header)
+        // READ_TO_EOF with the le64 prefix (a cas message's size header) and the EOF probe
         const int fd = open(p.c_str(), O_RDONLY);
         MsgSource src(fd, MsgSource::READ_TO_EOF);
         src.set_prefix_le64(0x1122334455667788ull);
+        src.set_eof_hint(n);
         std::vector<uint8_t> got, win(333333);
         for (;;) {
             const uint64_t k = src.read(win.data(), win.size());

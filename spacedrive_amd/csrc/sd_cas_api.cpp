@@ -321,18 +321,48 @@ void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_ha
 }
 
 // ------------------------------------------------------- streaming (unknown length)
-// Hashes one message read front to back from a MsgSource through 256 MiB windows on two
-// alternating slots.  The message's length is only known when the source ends, which is
-// all the 1 MiB-block tree needs: a full window (more than 1 MiB) holds 256 complete,
-// non-final blocks whose subtree CVs do not depend on the total, so they are hashed as the
-// windows arrive (a provisional one-message table of unbounded length); the final window
-// then runs with the message's real length, and the reduce passes merge all block CVs.
+// Hashes messages read front to back from a MsgSource through 256 MiB windows on the two
+// alternating slots.  A message's length is only known when its source ends, which is all
+// the 1 MiB-block tree needs: a full window (more than 1 MiB) holds 256 complete, non-final
+// blocks whose subtree CVs do not depend on the total, so they are hashed as the windows
+// arrive (a provisional one-message table of unbounded length); the final window then runs
+// with the message's real length, and the reduce passes merge all block CVs.
+//
+// Nothing waits for a message to finish: its final window, reduce and the 32-byte D2H are
+// queued on one slot's stream (after an event wait on the other slot's last window of the
+// same message), and the hash is handed to `done(tag, h32)` the next time that stream is
+// synchronised -- by the Streamer itself before it reuses the slot's window, by the
+// caller's collect(), or by finish().  So the host reads the next file while the GPU
+// finishes the last one.  Two per-message plans alternate; a plan is rebuilt only after
+// the events of the message that last used it have completed.
 struct Streamer {
     static constexpr uint64_t W = 256ull << 20;  // a multiple of the 1 MiB leaf block
     static constexpr uint32_t BPW = (uint32_t)(W / SD_CK_BLOCK);
-    sd_checksum_batch fin;        // the final plan: one message of the final length
+    static constexpr size_t RING = 16;  // results queued per slot between two syncs of it
+    using Done = std::function<void(size_t tag, const uint8_t* h32)>;
+
+    struct Msg {
+        sd_checksum_batch fin;  // the final plan: one message of the final length
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        bool used[2] = {false, false};  // ev[k] recorded since the plan was last rebuilt
+    };
+    Msg msg[2];
+    int next_msg = 0;
     DevBuf prov_files, prov_map;  // full windows: {0, 2^62, 0} and (0, b) for b < BPW
     bool prov_ready = false;
+    DevBuf rdev[2];
+    PinnedBuf rhost[2];
+    std::vector<size_t> rtag[2];
+    Done done;
+
+    explicit Streamer(Done d) : done(std::move(d)) {}
+    Streamer(const Streamer&) = delete;
+    Streamer& operator=(const Streamer&) = delete;
+    ~Streamer() {
+        for (auto& m : msg)
+            for (auto& e : m.ev)
+                if (e) (void)hipEventDestroy(e);
+    }
 
     static void prepare(SlotPair& sl) {
         for (int k = 0; k < 2; k++) {
@@ -342,51 +372,89 @@ struct Streamer {
             sl[k].host_hashes.ensure(32);
         }
     }
+    // Hands over the hashes queued on slot k.  The caller has synchronised its stream.
+    void collect(int k) {
+        for (size_t q = 0; q < rtag[k].size(); q++) done(rtag[k][q], rhost[k].u8() + 32 * q);
+        rtag[k].clear();
+    }
+    void sync_collect(SlotPair& sl, int k) {
+        HIP_CHECK(hipStreamSynchronize(sl[k].stream));
+        collect(k);
+    }
+    void finish(SlotPair& sl) {
+        sync_collect(sl, 0);
+        sync_collect(sl, 1);
+    }
+    void record(Msg& m, SlotPair& sl, int k) {
+        if (!m.ev[k]) HIP_CHECK(hipEventCreateWithFlags(&m.ev[k], hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(m.ev[k], sl[k].stream));
+        m.used[k] = true;
+    }
+    void wait_idle(Msg& m) {  // every launch of the message that last used this plan is done
+        for (int k = 0; k < 2; k++)
+            if (m.used[k]) {
+                HIP_CHECK(hipEventSynchronize(m.ev[k]));
+                m.used[k] = false;
+            }
+    }
 
-    // Returns SD_FILE_OK with the 32-byte hash in out32, or the source's I/O status.
-    int32_t hash(SlotPair& sl, int& cur, MsgSource& src, uint64_t size_hint, uint8_t out32[32]) {
+    // Queues the hash of one message; SD_FILE_OK means done(tag, ...) will follow, anything
+    // else is the source's I/O status (no result for this tag).
+    int32_t hash_async(SlotPair& sl, int& cur, MsgSource& src, uint64_t size_hint, size_t tag) {
         prepare(sl);
         if (!prov_ready) {
             std::vector<ck_file> f{ck_file{0, 1ull << 62, 0}};
-            std::vector<sd_u32x2> m(BPW);
-            for (uint32_t b = 0; b < BPW; b++) m[b] = sd_u32x2{0, b};
+            std::vector<sd_u32x2> mp(BPW);
+            for (uint32_t b = 0; b < BPW; b++) mp[b] = sd_u32x2{0, b};
             prov_files.upload(f);
-            prov_map.upload(m);
+            prov_map.upload(mp);
+            for (int k = 0; k < 2; k++) {
+                rdev[k].ensure(RING * 32);
+                rhost[k].ensure(RING * 32);
+            }
             prov_ready = true;
         }
-        sl.sync_all();
-        fin.lvl[0].grow_preserve((size_t)std::max<uint64_t>(size_hint / SD_CK_BLOCK + 2, 2 * BPW) * 32);
+        Msg& m = msg[next_msg];
+        next_msg ^= 1;
+        wait_idle(m);
+        sd_checksum_batch& fin = m.fin;
+        const uint64_t cap0 = (uint64_t)std::max<uint64_t>(size_hint / SD_CK_BLOCK + 2, 2 * BPW) * 32;
+        if (cap0 > fin.lvl[0].bytes) fin.lvl[0].grow_preserve(cap0);  // nothing of this plan in flight
         uint64_t pos = 0;
         for (;;) {
             const int k = cur;
             cur ^= 1;
-            HIP_CHECK(hipStreamSynchronize(sl[k].stream));  // its window is free again
+            sync_collect(sl, k);  // its window is free again
             uint8_t* win = sl[k].window.u8();
             const uint64_t got = src.read(win, W);
-            if (src.err) {
-                sl.sync_all();
-                return io_status(src.err);
-            }
+            if (src.err) return io_status(src.err);
             if (got == W && !src.done) {  // a full window with more to come
                 const uint32_t blk0 = (uint32_t)(pos / SD_CK_BLOCK);
                 if ((uint64_t)(blk0 + BPW) * 32 > fin.lvl[0].bytes) {
-                    sl.sync_all();
+                    sl.sync_all();  // both slots may hold windows of this message
                     fin.lvl[0].grow_preserve((size_t)(blk0 + BPW) * 64);
                 }
                 HIP_CHECK(hipMemcpyAsync(sl[k].staged.p, win, W, hipMemcpyHostToDevice, sl[k].stream));
                 HIP_CHECK(sdk::launch_ck_leaf(sl[k].staged.as<uint8_t>(), pos, blk0, prov_files.as<ck_file>(),
                                               prov_map.as<uint2>(), BPW, fin.lvl[0].as<uint32_t>(),
                                               sl[k].hashes.as<uint32_t>(), sl[k].stream));
+                record(m, sl, k);
                 pos += W;
                 continue;
             }
             const uint64_t L = pos + got;
             const uint64_t nb = L == 0 ? 1 : (L + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
-            sl.sync_all();
-            fin.lvl[0].grow_preserve((size_t)nb * 32);  // plan_checksum_batch must not reallocate it
+            if (nb * 32 > fin.lvl[0].bytes) {  // grew past the hint: keep the CVs
+                sl.sync_all();
+                fin.lvl[0].grow_preserve((size_t)nb * 32);
+            }
+            if (m.used[k ^ 1]) HIP_CHECK(hipStreamWaitEvent(sl[k].stream, m.ev[k ^ 1], 0));  // its windows first
             const uint64_t off0 = 0;
-            plan_checksum_batch(&fin, &off0, &L, 1, nullptr);
-            uint32_t* out = sl[k].hashes.as<uint32_t>();
+            // async uploads from fin's host tables: they stay valid until wait_idle(m)
+            plan_checksum_batch(&fin, &off0, &L, 1, sl[k].stream);
+            if (rtag[k].size() == RING) sync_collect(sl, k);
+            const size_t q = rtag[k].size();
+            uint32_t* out = rdev[k].as<uint32_t>() + 8 * q;
             if (got > 0 || L == 0) {
                 memset(win + got, 0, 64);
                 HIP_CHECK(hipMemcpyAsync(sl[k].staged.p, win, align_up(got, 64) + 64, hipMemcpyHostToDevice,
@@ -397,11 +465,28 @@ struct Streamer {
                                               fin.lvl[0].as<uint32_t>(), out, sl[k].stream));
             }
             run_checksum_reduce(&fin, out, sl[k].stream);
-            HIP_CHECK(hipMemcpyAsync(sl[k].host_hashes.p, out, 32, hipMemcpyDeviceToHost, sl[k].stream));
-            HIP_CHECK(hipStreamSynchronize(sl[k].stream));
-            memcpy(out32, sl[k].host_hashes.p, 32);
+            HIP_CHECK(hipMemcpyAsync(rhost[k].u8() + 32 * q, out, 32, hipMemcpyDeviceToHost, sl[k].stream));
+            record(m, sl, k);
+            rtag[k].push_back(tag);
             return SD_FILE_OK;
         }
+    }
+
+    // One message, waited for (the rare paths: cas messages that outgrew their extent).
+    int32_t hash(SlotPair& sl, int& cur, MsgSource& src, uint64_t size_hint, uint8_t out32[32]) {
+        finish(sl);  // earlier messages' results go to their own callback
+        Done keep = std::move(done);
+        done = [&](size_t, const uint8_t* h) { memcpy(out32, h, 32); };
+        int32_t rc;
+        try {
+            rc = hash_async(sl, cur, src, size_hint, 0);
+            finish(sl);
+        } catch (...) {
+            done = std::move(keep);
+            throw;
+        }
+        done = std::move(keep);
+        return rc;
     }
 };
 
@@ -726,7 +811,7 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
     harvest(0);
     harvest(1);
     if (!overflow.empty()) {
-        Streamer st;
+        Streamer st([](size_t, const uint8_t*) {});
         int cur = 0;
         for (size_t f : overflow) status[f] = cas_overflow(slots, cur, st, paths[f], sizes[f], out_hex17 + f * 17);
     }
@@ -833,21 +918,22 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
         bool busy = false;
     } pend[2];
     sd_checksum_batch pack_batch[2];
-    Streamer streamer;
+    // streamed files' hashes arrive when their slot is next synchronised
+    Streamer streamer([&](size_t i, const uint8_t* h) { to_hex(h, 32, out_hex65 + i * 65); });  // hash.rs:21-23
     int cur = 0;
-    auto harvest = [&](int k) {
-        if (!pend[k].busy) return;
+    auto harvest = [&](int k) {  // slot k idle: its window is free, its results delivered
         HIP_CHECK(hipStreamSynchronize(slots[k].stream));
+        streamer.collect(k);
+        if (!pend[k].busy) return;
         const uint8_t* h = slots[k].host_hashes.u8();
         for (size_t q = 0; q < pend[k].files.size(); q++)
             to_hex(h + 32 * q, 32, out_hex65 + pend[k].files[q] * 65);  // hash.rs:21-23
         pend[k].files.clear();
         pend[k].busy = false;
     };
-    // one file streamed (sequential reads, or parallel preads for a regular file)
+    // one file streamed (sequential reads, or parallel preads for a regular file); its hash
+    // lands in out_hex65 through the streamer's callback, at a later sync of its slot
     auto stream_file = [&](size_t i) {
-        harvest(0);
-        harvest(1);
         const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);  // hash.rs:11
         if (fd < 0) {
             status[i] = io_status(errno);
@@ -856,16 +942,17 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
         struct stat st;
         const bool reg = fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
         MsgSource src(fd, MsgSource::CHECKSUM_READS);
-        if (reg) src.set_parallel(pool.get());
-        uint8_t h[32];
+        if (reg) {
+            src.set_parallel(pool.get());
+            src.set_eof_hint((uint64_t)st.st_size);  // a window-multiple file ends with its last window
+        }
         try {
-            status[i] = streamer.hash(slots, cur, src, reg ? (uint64_t)st.st_size : 0, h);
+            status[i] = streamer.hash_async(slots, cur, src, reg ? (uint64_t)st.st_size : 0, i);
         } catch (...) {
             close(fd);
             throw;
         }
         close(fd);
-        if (status[i] == SD_FILE_OK) to_hex(h, 32, out_hex65 + i * 65);
     };
     // the pack: regular files laid out by their stat lengths in slot `cur`'s window
     std::vector<size_t> pack, grew;
@@ -939,12 +1026,13 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
         pack_end = align_up(pack_end + hint[i], 64);
     }
     submit_pack();
-    harvest(0);
-    harvest(1);
     for (size_t i : grew) {
         status[i] = SD_FILE_OK;
         stream_file(i);
     }
+    harvest(0);
+    harvest(1);
+    streamer.finish(slots);
     return SD_OK;
     SD_GUARD_END
 }

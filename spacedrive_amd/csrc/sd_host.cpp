@@ -332,6 +332,18 @@ void MsgSource::set_prefix_le64(uint64_t v) {
 }
 
 uint64_t MsgSource::read(uint8_t* dst, uint64_t n) {
+    const uint64_t got = read_impl(dst, n);
+    if (has_eof_hint_ && !done && !err && got == n && file_pos_ == eof_hint_ && pend_len_ == 0) {
+        uint8_t probe;
+        ssize_t r;
+        do r = pread(fd_, &probe, 1, (off_t)file_pos_);
+        while (r < 0 && errno == EINTR);
+        if (r == 0) done = true;  // the next read would return 0: the message ends here
+    }
+    return got;
+}
+
+uint64_t MsgSource::read_impl(uint8_t* dst, uint64_t n) {
     uint64_t got = 0;
     while (got < n && prefix_pos_ < prefix_len_) dst[got++] = prefix_[prefix_pos_++];
     if (pend_len_ && got < n) {
@@ -344,6 +356,7 @@ uint64_t MsgSource::read(uint8_t* dst, uint64_t n) {
     if (done || err) return got;
     if (pool_ && mode_ == CHECKSUM_READS && got < n) return got + read_parallel(dst + got, n - got);
     if (mode_ == READ_TO_EOF) {
+        const uint64_t got0 = got;  // prefix and pending bytes are not new file bytes
         while (got < n) {
             const ssize_t r = read_once(fd_, dst + got, n - got);
             if (r < 0) {
@@ -356,7 +369,7 @@ uint64_t MsgSource::read(uint8_t* dst, uint64_t n) {
             }
             got += (uint64_t)r;
         }
-        file_pos_ += got;
+        file_pos_ += got - got0;
         return got;
     }
     const uint64_t got0 = got;

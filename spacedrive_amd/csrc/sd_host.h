@@ -164,6 +164,15 @@ public:
     // short one return exactly the bytes up to EOF, so each window is filled with 1 MiB
     // preads at their offsets in parallel on `pool`, and ends at the first short piece.
     void set_parallel(StagePool* pool) { pool_ = pool; }
+    // A regular file's stat length: when the reads reach exactly that many file bytes, one
+    // 1-byte pread past it decides whether the message has ended (a read there returns 0,
+    // as the reference's next read would), so a reader of W-byte windows learns the end
+    // with the last full window instead of from an extra, empty one.  A file that grew
+    // keeps going: nothing is consumed by the probe.
+    void set_eof_hint(uint64_t file_len) {
+        eof_hint_ = file_len;
+        has_eof_hint_ = true;
+    }
     // Writes up to n message bytes to dst and returns the count; fewer than n only at the
     // end of the message (done) or on an error (err = errno).  CHECKSUM_READS: n is a
     // multiple of 1 MiB.
@@ -173,6 +182,7 @@ public:
 
 private:
     uint64_t read_parallel(uint8_t* dst, uint64_t n);
+    uint64_t read_impl(uint8_t* dst, uint64_t n);
     int fd_;
     Mode mode_;
     StagePool* pool_ = nullptr;
@@ -181,6 +191,8 @@ private:
     uint32_t prefix_len_ = 0, prefix_pos_ = 0;
     const uint8_t* pend_ = nullptr;
     uint64_t pend_len_ = 0;
+    uint64_t eof_hint_ = 0;
+    bool has_eof_hint_ = false;
 };
 
 // ------------------------------------------------------------------ CPU BLAKE3 (cpu_blake3.cpp)

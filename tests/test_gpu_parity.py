@@ -357,8 +357,9 @@ def test_valu_peak_plausible(ctx):
 
 
 def test_file_checksums_packing_and_streaming(ctx, tmp_path):
-    # many small files packed per window, a file larger than the 256 MiB window streamed
-    # between them, an unreadable path in the middle: results in input order
+    # many small files packed per window, files larger than half the 256 MiB window streamed
+    # between them (their hashes arrive asynchronously, at later syncs of their slot), an
+    # unreadable path in the middle: results in input order
     import spacedrive_amd as sd
     from oracle import native
     rng = np.random.default_rng(11)
@@ -366,6 +367,8 @@ def test_file_checksums_packing_and_streaming(ctx, tmp_path):
     sizes[40] = (300 << 20) + 7
     sizes[41] = 256 << 20  # exactly one window + nothing: packed? no -> streamed (len + 128 > W)
     sizes[42] = 0
+    sizes[43] = (129 << 20) + 1  # a third streamed file in a row: the two message plans alternate
+    sizes[100] = 128 << 20  # streamed between packs
     paths = []
     for i, sz in enumerate(sizes):
         p = tmp_path / f"c{i}"
