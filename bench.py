@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--files-per-gpu", type=int, default=1_250_000)
     p.add_argument("--checksum-gib", type=int, default=64, help="configs[3] size per GPU; 0 = skip")
     p.add_argument("--checksum-steps", type=int, default=5)
+    p.add_argument("--split-gib", type=int, default=32,
+                   help="one file of this many GiB (+12345 B) split over the ranks; 0 = skip")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target seconds per CPU-baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (rehearsal)")
@@ -522,6 +524,69 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int, warm_ms: float):
+    """file_checksum (hash.rs:10-24) of ONE file spread over the ranks: rank r
+    holds its contiguous run of 1 MiB blocks (sd_split_range), hashes them to block CVs, the
+    CVs are all-gathered in place over libsdcas's RCCL communicator (32 B per MiB), and every
+    rank reduces them to the file's hash (sd_split_checksum_mgpu).  Strong scaling: the file
+    is the same at every N.  Timed with a barrier on both sides, max over ranks."""
+    from spacedrive_amd.device import SplitChecksum
+    total = (gib << 30) + 12345  # not block-aligned: the last rank's final block is partial
+    sc = SplitChecksum(ctx, total, world, rank)
+    d_slice = torch.zeros(sc.len + 128, dtype=torch.uint8, device=dev)
+    if sc.len:
+        ctx.synth_fill(20_000, 0, sc.len, d_slice, offset=sc.offset)
+    cvs = torch.zeros(sc.cv_bytes, dtype=torch.uint8, device=dev)
+    out32 = torch.zeros(32, dtype=torch.uint8, device=dev)
+    if comm is not None:
+        def run():
+            sc.mgpu(comm, d_slice, cvs, out32, stream)
+    elif world == 1:
+        def run():
+            sc.leaves(d_slice, cvs, stream)
+            sc.root(cvs, out32, stream)
+    else:
+        return {"skipped": "needs libsdcas's RCCL communicator at N > 1 (--dedup rccl, nccl backend)"}
+    run()
+    warm(run, stream, warm_ms)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    wall_ms = float(dt.item()) / reps * 1e3
+    leaves_ms = ev_ms(lambda: sc.leaves(d_slice, cvs, stream), stream, reps=reps)
+    res = {"file_bytes": total, "ranks": world, "blocks": (total + (1 << 20) - 1) >> 20,
+           "ms_per_file": wall_ms, "GBps": total / (wall_ms * 1e-3) / 1e9, "scaling": "strong",
+           "rank0_leaves_ms": leaves_ms, "rank0_bytes": sc.len,
+           "rank0_leaves_GBps": sc.len / (leaves_ms * 1e-3) / 1e9 if sc.len else None,
+           "transport": "rccl" if comm is not None else "none (N=1)",
+           "note": "one file over all ranks: per-rank block CVs, in-place ncclAllGather of the CV slots, "
+                   "reduce on every rank (sd_split_checksum_mgpu); wall time with barriers, max over ranks"}
+    h = out32.clone()
+    if world > 1:  # every rank must hold the same hash
+        allh = [torch.zeros_like(h) for _ in range(world)]
+        dist.all_gather(allh, h)
+        res["ranks_agree"] = all(torch.equal(x, h) for x in allh)
+    else:  # the whole file is here: the same bytes through the regular checksum batch
+        cb = ctx.checksum_batch([0], [total])
+        ref = torch.zeros(32, dtype=torch.uint8, device=dev)
+        cb.run(d_slice, ref, stream)
+        torch.cuda.synchronize()
+        res["equal_to_checksum_batch"] = bool(torch.equal(ref, h))
+        cb.close()
+    res["hash"] = bytes(h.cpu().numpy()).hex()
+    sc.close()
+    del d_slice, cvs
+    torch.cuda.empty_cache()
+    return res
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse()
@@ -726,6 +791,10 @@ def main():
                            "launch_grid": cb.blocks * 256, "traffic": tr_ck["bytes"] if tr_ck else None}
         del d_data, cb
         torch.cuda.empty_cache()
+
+    if args.split_gib > 0:
+        out["checksum_one_file"] = split_leg(ctx, comm, args.split_gib, rank, world, dev, stream,
+                                             args.checksum_steps, args.warm_ms)
 
     if solo and args.host_checksum_gib > 0:
         with_h2d["checksum"] = checksum_host(ctx, args.host_checksum_gib, dev, stream)

@@ -285,6 +285,43 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
                       uint64_t* d_owner_out, uint64_t capacity, uint64_t* m_out, uint64_t* n_groups_out,
                       void* stream);
 
+/* ---------------------------------------------------------------- one file over many GPUs */
+/* file_checksum (hash.rs:10-24) of ONE file whose bytes are spread over the ranks of a
+ * communicator (a file's 1 MiB blocks shard naturally).  The file's
+ * total_len bytes are cut into nb = max(1, ceil(total_len / 1 MiB)) blocks; rank r of R
+ * holds blocks [r*q, min((r+1)*q, nb)) with q = ceil(nb / R) -- sd_split_range gives its
+ * byte range [offset, offset + len) and the CV buffer size, R * q * 32 bytes.  Each rank
+ * hashes its blocks to their 32-byte chaining values at block index b of the CV buffer
+ * (a block's CV depends only on its bytes and its position, not on the total); the
+ * buffers of all ranks laid end to end in rank order are the file's block CVs in order,
+ * and one reduce gives the BLAKE3 of the whole file, bit-identical to file_checksum's.
+ * A file of one block (total_len <= 1 MiB) is held by rank 0, whose "CV" slot 0 then
+ * holds the root hash itself.  GPU-free. */
+int sd_split_range(uint64_t total_len, int nranks, int rank, uint64_t* offset, uint64_t* len,
+                   uint64_t* cv_bytes);
+typedef struct sd_split_checksum sd_split_checksum;
+int sd_split_checksum_create(sd_cas_ctx* ctx, uint64_t total_len, int nranks, int rank,
+                             sd_split_checksum** out);
+void sd_split_checksum_destroy(sd_split_checksum* split);
+/* This rank's blocks -> d_cvs (device, cv_bytes; only this rank's slots are written).
+ * d_slice = the rank's `len` bytes (device, 16-byte aligned, zero-padded to the next
+ * 64-byte boundary).  Asynchronous on `stream`. */
+int sd_split_checksum_leaves(sd_cas_ctx* ctx, const sd_split_checksum* split, const uint8_t* d_slice,
+                             uint8_t* d_cvs, void* stream);
+/* All ranks' CVs (device, every slot filled) -> the 32-byte file hash (device).
+ * Asynchronous on `stream`; one call at a time per split object. */
+int sd_split_checksum_root(sd_cas_ctx* ctx, sd_split_checksum* split, const uint8_t* d_cvs,
+                           uint8_t* d_hash32, void* stream);
+/* Collective over the communicator (nranks / rank must match the split's): leaves, an
+ * in-place ncclAllGather of the CV slots (32 B per MiB of file: 1 MB per 32 GiB), root.
+ * Every rank gets the hash.  Asynchronous on `stream`. */
+int sd_split_checksum_mgpu(sd_cas_ctx* ctx, sd_comm* comm, sd_split_checksum* split, const uint8_t* d_slice,
+                           uint8_t* d_cvs, uint8_t* d_hash32, void* stream);
+/* The same two steps on host cores (host pointers). */
+int sd_cpu_split_leaves(const uint8_t* slice, uint64_t total_len, int nranks, int rank, uint8_t* cvs,
+                        int nthreads);
+int sd_cpu_split_root(const uint8_t* cvs, uint64_t total_len, uint8_t* out_hash32);
+
 /* ---------------------------------------------------------------- synthetic data */
 /* Device generator of SURVEY.md §8(d) (seed 0x5D5DCA51D, splitmix64 counter stream),
  * for benchmarks and parity tests: writes the exact cas message of each synthetic file
@@ -295,6 +332,9 @@ int sd_synth_stage_cas(sd_cas_ctx* ctx, const uint64_t* d_sizes, const uint64_t*
 /* bytes [0, len) of synthetic content (cid, twin) -> d_out (device) */
 int sd_synth_fill(sd_cas_ctx* ctx, uint64_t cid, uint32_t twin, uint64_t len, uint8_t* d_out,
                   void* stream);
+/* bytes [offset, offset + len) of the same content -> d_out (offset and d_out 8-aligned) */
+int sd_synth_fill_at(sd_cas_ctx* ctx, uint64_t cid, uint32_t twin, uint64_t offset, uint64_t len,
+                     uint8_t* d_out, void* stream);
 
 /* ---------------------------------------------------------------- device utilities */
 int sd_device_malloc(sd_cas_ctx* ctx, uint64_t bytes, void** out);

@@ -30,6 +30,11 @@ pub struct sd_comm {
 }
 
 #[repr(C)]
+pub struct sd_split_checksum {
+    _p: [u8; 0],
+}
+
+#[repr(C)]
 #[derive(Clone, Copy, Default, Debug)]
 pub struct sd_extent {
     pub size: u64,
@@ -82,6 +87,17 @@ extern "C" {
                              n: u64, global_index_base: u64, chunk_size: u64, d_records_out: *mut u64,
                              d_rep_out: *mut u64, d_owner_out: *mut u64, capacity: u64, m_out: *mut u64,
                              n_groups_out: *mut u64, stream: *mut c_void) -> c_int;
+    // one file's checksum over many GPUs (its 1 MiB blocks sharded by rank)
+    pub fn sd_split_range(total_len: u64, nranks: c_int, rank: c_int, offset: *mut u64, len: *mut u64,
+                          cv_bytes: *mut u64) -> c_int;
+    pub fn sd_split_checksum_create(ctx: *mut sd_cas_ctx, total_len: u64, nranks: c_int, rank: c_int,
+                                    out: *mut *mut sd_split_checksum) -> c_int;
+    pub fn sd_split_checksum_destroy(split: *mut sd_split_checksum);
+    pub fn sd_split_checksum_mgpu(ctx: *mut sd_cas_ctx, comm: *mut sd_comm, split: *mut sd_split_checksum,
+                                  d_slice: *const u8, d_cvs: *mut u8, d_hash32: *mut u8, stream: *mut c_void) -> c_int;
+    pub fn sd_cpu_split_leaves(slice: *const u8, total_len: u64, nranks: c_int, rank: c_int, cvs: *mut u8,
+                               nthreads: c_int) -> c_int;
+    pub fn sd_cpu_split_root(cvs: *const u8, total_len: u64, out_hash32: *mut u8) -> c_int;
 }
 
 /// One context per process on device 0 (the job system's 5 concurrent jobs, watcher and

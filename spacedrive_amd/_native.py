@@ -92,8 +92,17 @@ SIGNATURES = [
     ("sd_comm_create", I32, [P, P, I32, I32, ctypes.POINTER(P)]),
     ("sd_comm_destroy", None, [P]),
     ("sd_cas_dedup_mgpu", I32, [P, P, P, P, U64, U64, U64, P, P, P, U64, PU64, PU64, P]),
+    ("sd_split_range", I32, [U64, I32, I32, PU64, PU64, PU64]),
+    ("sd_split_checksum_create", I32, [P, U64, I32, I32, ctypes.POINTER(P)]),
+    ("sd_split_checksum_destroy", None, [P]),
+    ("sd_split_checksum_leaves", I32, [P, P, P, P, P]),
+    ("sd_split_checksum_root", I32, [P, P, P, P, P]),
+    ("sd_split_checksum_mgpu", I32, [P, P, P, P, P, P, P]),
+    ("sd_cpu_split_leaves", I32, [P, U64, I32, I32, P, I32]),
+    ("sd_cpu_split_root", I32, [P, U64, P]),
     ("sd_synth_stage_cas", I32, [P, P, P, P, P, SZ, P, P]),
     ("sd_synth_fill", I32, [P, U64, U32, U64, P, P]),
+    ("sd_synth_fill_at", I32, [P, U64, U32, U64, U64, P, P]),
     ("sd_device_malloc", I32, [P, U64, ctypes.POINTER(P)]),
     ("sd_device_free", None, [P, P]),
     ("sd_memcpy", I32, [P, P, P, U64, P]),

@@ -118,6 +118,7 @@ const Simd& simd() {
 int cpu_lanes() { return simd().lanes; }
 
 CpuHasher::CpuHasher() {}
+CpuHasher::CpuHasher(uint64_t chunk0) : ctr0_(chunk0) {}
 
 void CpuHasher::push_chunk_cv(const uint32_t cv[8]) {
     uint32_t cur[8];
@@ -135,7 +136,7 @@ void CpuHasher::update(const uint8_t* p, size_t n) {
     while (n) {
         if (buf_len_ == 1024) {  // the buffered chunk is not the last one: push it
             uint32_t cv[8];
-            chunk_cv(buf_, 1024, chunks_, false, cv);
+            chunk_cv(buf_, 1024, ctr0_ + chunks_, false, cv);
             push_chunk_cv(cv);
             buf_len_ = 0;
         }
@@ -146,7 +147,7 @@ void CpuHasher::update(const uint8_t* p, size_t n) {
             while (k) {
                 const int g = (int)std::min<size_t>(k, (size_t)s.lanes);
                 for (int i = 0; i < g; i++) ptrs[i] = p + 1024 * (size_t)i;
-                s.fn(ptrs, g, chunks_, cvs);
+                s.fn(ptrs, g, ctr0_ + chunks_, cvs);
                 for (int i = 0; i < g; i++) push_chunk_cv(cvs[i]);
                 p += 1024 * (size_t)g;
                 n -= 1024 * (size_t)g;
@@ -165,13 +166,36 @@ void CpuHasher::update(const uint8_t* p, size_t n) {
 void CpuHasher::finalize(uint8_t out[32]) const {
     uint32_t cur[8];
     if (sp_ == 0) {
-        chunk_cv(buf_, buf_len_, chunks_, true, cur);
+        chunk_cv(buf_, buf_len_, ctr0_ + chunks_, true, cur);
     } else {
-        chunk_cv(buf_, buf_len_, chunks_, false, cur);
+        chunk_cv(buf_, buf_len_, ctr0_ + chunks_, false, cur);
         for (int i = sp_ - 1; i >= 1; i--) parent_cv(stack_[i], cur, 0, cur);
         parent_cv(stack_[0], cur, ROOT, cur);
     }
     memcpy(out, cur, 32);  // little-endian words = the hash bytes
+}
+
+void CpuHasher::finalize_cv(uint8_t out[32]) const {
+    uint32_t cur[8];
+    chunk_cv(buf_, buf_len_, ctr0_ + chunks_, false, cur);
+    for (int i = sp_ - 1; i >= 0; i--) parent_cv(stack_[i], cur, 0, cur);
+    memcpy(out, cur, 32);
+}
+
+// Level-wise pairwise merge with the odd node carried up (= BLAKE3's left-heavy tree over
+// power-of-two aligned blocks), ROOT on the final parent.
+void cpu_root_from_cvs(const uint8_t* cvs, uint64_t nb, uint8_t out[32]) {
+    std::vector<uint32_t> lvl(nb * 8);
+    memcpy(lvl.data(), cvs, nb * 32);
+    uint64_t n = nb;
+    while (n > 1) {
+        const uint64_t pairs = n / 2;
+        for (uint64_t i = 0; i < pairs; i++)
+            parent_cv(&lvl[16 * i], &lvl[16 * i + 8], n == 2 ? ROOT : 0, &lvl[8 * i]);
+        if (n & 1) memmove(&lvl[8 * pairs], &lvl[8 * (n - 1)], 32);
+        n = pairs + (n & 1);
+    }
+    memcpy(out, lvl.data(), 32);
 }
 
 void cpu_blake3(const uint8_t* p, size_t n, uint8_t out[32]) {
@@ -314,6 +338,37 @@ int sd_cpu_cas_id_path(const char* path, uint64_t size, char* out_hex17, int32_t
     SD_GUARD_BEGIN
     if (!path || !out_hex17 || !status) throw sd_failure(SD_ERR_INVALID, "null argument");
     *status = cpu_cas_id_file(path, size, out_hex17);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cpu_split_leaves(const uint8_t* slice, uint64_t total_len, int nranks, int rank, uint8_t* cvs,
+                        int nthreads) {
+    SD_GUARD_BEGIN
+    const SplitPlan p = split_plan(total_len, nranks, rank);
+    if (!cvs || (p.len && !slice)) throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (p.nb == 1) {  // one block: rank 0 holds the file and slot 0 its root hash
+        if (rank == 0) cpu_blake3(slice, p.len, cvs);
+        return SD_OK;
+    }
+    parallel_for(p.b1 - p.b0, nthreads, [&](size_t k) {
+        const uint64_t b = p.b0 + k;
+        const uint64_t off = b * SD_CK_BLOCK - p.off;
+        const uint64_t len = std::min<uint64_t>(SD_CK_BLOCK, p.total - b * SD_CK_BLOCK);
+        CpuHasher h(b * (SD_CK_BLOCK / 1024));
+        h.update(slice + off, len);
+        h.finalize_cv(cvs + 32 * b);
+    });
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cpu_split_root(const uint8_t* cvs, uint64_t total_len, uint8_t* out_hash32) {
+    SD_GUARD_BEGIN
+    if (!cvs || !out_hash32) throw sd_failure(SD_ERR_INVALID, "null argument");
+    const SplitPlan p = split_plan(total_len, 1, 0);
+    if (p.nb == 1) memcpy(out_hash32, cvs, 32);
+    else cpu_root_from_cvs(cvs, p.nb, out_hash32);
     return SD_OK;
     SD_GUARD_END
 }

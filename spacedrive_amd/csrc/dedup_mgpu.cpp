@@ -193,4 +193,26 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
     SD_GUARD_END
 }
 
+// One file over the ranks (include/sd_cas.h): each rank's block CVs, then an in-place
+// all-gather of the CV slots -- rank r's q slots sit at r * q, so the gathered buffer is the
+// file's block CVs in order (the padding past nb is never read) --, then the reduce.
+int sd_split_checksum_mgpu(sd_cas_ctx* ctx, sd_comm* comm, sd_split_checksum* split, const uint8_t* d_slice,
+                           uint8_t* d_cvs, uint8_t* d_hash32, void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || !comm || !split || !d_cvs || !d_hash32) throw sd_failure(SD_ERR_INVALID, "null argument");
+    const SplitPlan& p = sd_split_plan_of(split);
+    if (p.nranks != comm->nranks || p.rank != comm->rank)
+        throw sd_failure(SD_ERR_INVALID, "the split's nranks / rank differ from the communicator's");
+    HIP_OK(hipSetDevice(comm->device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    check_rc(sd_split_checksum_leaves(ctx, split, d_slice, d_cvs, stream));
+    if (comm->nranks > 1) {
+        const size_t slot_bytes = (size_t)p.q * 32;
+        NCCL_OK(ncclAllGather(d_cvs + (size_t)p.rank * slot_bytes, d_cvs, slot_bytes, ncclUint8, comm->comm, s));
+    }
+    check_rc(sd_split_checksum_root(ctx, split, d_cvs, d_hash32, stream));
+    return SD_OK;
+    SD_GUARD_END
+}
+
 }  // extern "C"

@@ -199,6 +199,12 @@ struct sd_checksum_batch {
     std::vector<std::unique_ptr<DevBuf>> pass_wgs;  // capacity reused across replans
 };
 
+// one file over the ranks of a communicator (include/sd_cas.h, sd_split_range)
+struct sd_split_checksum {
+    SplitPlan sp;
+    sd_checksum_batch plan;  // the whole file as one message: leaf table + reduce passes
+};
+
 struct sd_cas_batch {
     size_t n = 0;
     uint32_t n_sampled = 0, n_whole = 0, n_long = 0;
@@ -515,6 +521,7 @@ int32_t cas_overflow(SlotPair& sl, int& cur, Streamer& st, const char* path, uin
 }  // namespace
 
 int sd_ctx_device(const sd_cas_ctx* ctx) { return ctx->device; }
+const SplitPlan& sd_split_plan_of(const sd_split_checksum* x) { return x->sp; }
 
 // ============================================================================ C ABI
 extern "C" {
@@ -886,6 +893,65 @@ int sd_checksum_batch_stats(const sd_checksum_batch* b, uint64_t out[4]) {
     SD_GUARD_END
 }
 
+// ------------------------------------------------------------ one file over many GPUs
+int sd_split_checksum_create(sd_cas_ctx* ctx, uint64_t total_len, int nranks, int rank, sd_split_checksum** out) {
+    SD_GUARD_BEGIN
+    if (!ctx || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    *out = nullptr;
+    ctx->bind();
+    auto x = std::make_unique<sd_split_checksum>();
+    x->sp = split_plan(total_len, nranks, rank);
+    const uint64_t off0 = 0;
+    plan_checksum_batch(&x->plan, &off0, &total_len, 1, nullptr);
+    *out = x.release();
+    return SD_OK;
+    SD_GUARD_END
+}
+
+void sd_split_checksum_destroy(sd_split_checksum* x) {
+    try {
+        delete x;
+    } catch (...) {
+    }
+}
+
+// k_ck_leaf over this rank's blocks of the one-message plan: the slice holds message bytes
+// [off, off + len) (shift = off), block b's CV lands in d_cvs slot b (cv_base 0); a
+// one-block file writes its root hash to `out` = slot 0.
+int sd_split_checksum_leaves(sd_cas_ctx* ctx, const sd_split_checksum* x, const uint8_t* d_slice, uint8_t* d_cvs,
+                             void* stream) {
+    SD_GUARD_BEGIN
+    const SplitPlan& p = x ? x->sp : SplitPlan{};
+    if (!ctx || !x || !d_cvs || (p.b1 > p.b0 && !d_slice)) throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (p.b1 > p.b0 && reinterpret_cast<uintptr_t>(d_slice) % 16)
+        throw sd_failure(SD_ERR_INVALID, "d_slice not 16-byte aligned");
+    ctx->bind();
+    if (p.b1 > p.b0) {  // a rank past the last block holds nothing
+        uint32_t* cvs = reinterpret_cast<uint32_t*>(d_cvs);
+        HIP_CHECK(sdk::launch_ck_leaf(d_slice, p.off, 0, x->plan.files.as<ck_file>(),
+                                      x->plan.wg_map.as<uint2>() + p.b0, (uint32_t)(p.b1 - p.b0), cvs, cvs,
+                                      ctx->pick(stream)));
+    }
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_split_checksum_root(sd_cas_ctx* ctx, sd_split_checksum* x, const uint8_t* d_cvs, uint8_t* d_hash32,
+                           void* stream) {
+    SD_GUARD_BEGIN
+    if (!ctx || !x || !d_cvs || !d_hash32) throw sd_failure(SD_ERR_INVALID, "null argument");
+    ctx->bind();
+    hipStream_t s = ctx->pick(stream);
+    if (x->sp.nb == 1) {
+        HIP_CHECK(hipMemcpyAsync(d_hash32, d_cvs, 32, hipMemcpyDeviceToDevice, s));
+    } else {
+        HIP_CHECK(hipMemcpyAsync(x->plan.lvl[0].p, d_cvs, x->sp.nb * 32, hipMemcpyDeviceToDevice, s));
+        run_checksum_reduce(&x->plan, reinterpret_cast<uint32_t*>(d_hash32), s);
+    }
+    return SD_OK;
+    SD_GUARD_END
+}
+
 // file_checksum (hash.rs:10-24) for n paths.  Each file is read as the reference reads it:
 // hash.rs's 1 MiB read calls until one returns fewer.  For a regular file those reads are
 // exactly its bytes up to EOF, so regular files are read with parallel preads on the
@@ -1220,10 +1286,17 @@ int sd_synth_stage_cas(sd_cas_ctx* ctx, const uint64_t* d_sizes, const uint64_t*
 }
 
 int sd_synth_fill(sd_cas_ctx* ctx, uint64_t cid, uint32_t twin, uint64_t len, uint8_t* d_out, void* stream) {
+    return sd_synth_fill_at(ctx, cid, twin, 0, len, d_out, stream);
+}
+
+int sd_synth_fill_at(sd_cas_ctx* ctx, uint64_t cid, uint32_t twin, uint64_t offset, uint64_t len, uint8_t* d_out,
+                     void* stream) {
     SD_GUARD_BEGIN
     if (!ctx || (len && !d_out)) throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (offset % 8 || reinterpret_cast<uintptr_t>(d_out) % 8)
+        throw sd_failure(SD_ERR_INVALID, "offset and d_out must be 8-byte aligned");
     ctx->bind();
-    HIP_CHECK(sdk::launch_synth_fill(cid, twin, len, d_out, ctx->pick(stream)));
+    HIP_CHECK(sdk::launch_synth_fill(cid, twin, offset, len, d_out, ctx->pick(stream)));
     return SD_OK;
     SD_GUARD_END
 }

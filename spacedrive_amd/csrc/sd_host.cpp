@@ -35,9 +35,37 @@ void sd_set_err(const char* fmt, ...) {
 
 int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }
 
+SplitPlan split_plan(uint64_t total, int nranks, int rank) {
+    if (nranks < 1 || nranks > 4096 || rank < 0 || rank >= nranks)
+        throw sd_failure(SD_ERR_INVALID, "rank / nranks out of range");
+    SplitPlan p;
+    p.total = total;
+    p.nranks = nranks;
+    p.rank = rank;
+    p.nb = total == 0 ? 1 : (total + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
+    if (p.nb >= (1ull << 32)) throw sd_failure(SD_ERR_INVALID, "file too large");
+    p.q = (p.nb + (uint64_t)nranks - 1) / (uint64_t)nranks;
+    p.b0 = std::min<uint64_t>(p.nb, (uint64_t)rank * p.q);
+    p.b1 = std::min<uint64_t>(p.nb, p.b0 + p.q);
+    p.off = std::min<uint64_t>(total, p.b0 * SD_CK_BLOCK);
+    p.len = std::min<uint64_t>(total, p.b1 * SD_CK_BLOCK) - p.off;
+    return p;
+}
+
 extern "C" {
 const char* sd_cas_last_error(void) { return g_err.c_str(); }
 int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }
+int sd_split_range(uint64_t total_len, int nranks, int rank, uint64_t* offset, uint64_t* len, uint64_t* cv_bytes) {
+    SD_GUARD_BEGIN
+    if (!offset || !len || !cv_bytes) throw sd_failure(SD_ERR_INVALID, "null argument");
+    const SplitPlan p = split_plan(total_len, nranks, rank);
+    *offset = p.off;
+    *len = p.len;
+    *cv_bytes = p.cv_bytes();
+    return SD_OK;
+    SD_GUARD_END
+}
+
 int sd_cas_set_tuning(const char* key, int value) {
     SD_GUARD_BEGIN
     if (!key) throw sd_failure(SD_ERR_INVALID, "null key");

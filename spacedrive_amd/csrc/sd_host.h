@@ -129,6 +129,16 @@ struct CkPlan {
 };
 void plan_checksum(CkPlan& p, const uint64_t* offsets, const uint64_t* lens, size_t n);
 
+// One file over R ranks (sd_split_range, include/sd_cas.h): nb = max(1, ceil(total / 1 MiB))
+// blocks, rank r holds blocks [b0, b1) = [r*q, min((r+1)*q, nb)), q = ceil(nb / R), i.e.
+// file bytes [off, off + len).  Throws SD_ERR_INVALID on a bad rank / rank count.
+struct SplitPlan {
+    uint64_t total = 0, nb = 1, q = 1, b0 = 0, b1 = 0, off = 0, len = 0;
+    int nranks = 1, rank = 0;
+    uint64_t cv_bytes() const { return (uint64_t)nranks * q * 32; }
+};
+SplitPlan split_plan(uint64_t total, int nranks, int rank);
+
 // ------------------------------------------------------------------ file reading
 // Reads one file's cas message into staged + e.msg_offset exactly as generate_cas_id reads
 // it (cas.rs:25-58) and zero-pads it to the next 64-byte boundary.  Returns an
@@ -203,18 +213,25 @@ private:
 class CpuHasher {
 public:
     CpuHasher();
+    // a subtree whose first chunk has index chunk0 (a 1 MiB block of a longer message)
+    explicit CpuHasher(uint64_t chunk0);
     void update(const uint8_t* p, size_t n);
     void finalize(uint8_t out[32]) const;
+    // the subtree's chaining value: no ROOT flag (a block of a message of several blocks)
+    void finalize_cv(uint8_t out[32]) const;
 
 private:
     void push_chunk_cv(const uint32_t cv[8]);
     uint32_t stack_[56][8];
     int sp_ = 0;
+    uint64_t ctr0_ = 0;    // chunk index of the first chunk
     uint64_t chunks_ = 0;  // complete chunks pushed so far
     uint8_t buf_[1024];
     uint32_t buf_len_ = 0;
 };
 void cpu_blake3(const uint8_t* p, size_t n, uint8_t out[32]);
+// BLAKE3 root of a message from its nb >= 2 consecutive 1 MiB block CVs (32 B each)
+void cpu_root_from_cvs(const uint8_t* cvs, uint64_t nb, uint8_t out[32]);
 // lanes of the SIMD chunk hasher this CPU runs (16, 8 or 1)
 int cpu_lanes();
 // generate_cas_id / file_checksum of one file on the calling thread -> sd_file_status

@@ -8,6 +8,8 @@
 
 // the device a context was created on
 int sd_ctx_device(const sd_cas_ctx* ctx);
+// the block partition of a split-file checksum object
+const SplitPlan& sd_split_plan_of(const sd_split_checksum* x);
 namespace sdk {
 hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const uint32_t* idx, uint32_t n,
                               uint32_t* out, hipStream_t s);
@@ -23,7 +25,8 @@ hipError_t launch_ck_reduce(const uint32_t* src, uint32_t* dst, const ck_reduce_
                             uint32_t* out, hipStream_t s);
 hipError_t launch_synth_stage_cas(const uint64_t* sizes, const uint64_t* cids, const uint32_t* twins,
                                   const sd_extent* ext, uint32_t n, uint8_t* staged, hipStream_t s);
-hipError_t launch_synth_fill(uint64_t cid, uint32_t twin, uint64_t len, uint8_t* out, hipStream_t s);
+hipError_t launch_synth_fill(uint64_t cid, uint32_t twin, uint64_t offset, uint64_t len, uint8_t* out,
+                             hipStream_t s);
 hipError_t launch_read_probe(const uint8_t* buf, uint64_t bytes, int pattern, hipStream_t s);
 hipError_t launch_valu_peak(uint32_t* sink, uint32_t iters, uint32_t grid, hipStream_t s);
 // dedup

@@ -74,13 +74,13 @@ __global__ __launch_bounds__(256) void k_synth_stage_cas(const uint64_t* __restr
     }
 }
 
-__global__ __launch_bounds__(256) void k_synth_fill(uint64_t key, uint32_t twin, uint64_t len,
+__global__ __launch_bounds__(256) void k_synth_fill(uint64_t key, uint32_t twin, uint64_t offset, uint64_t len,
                                                     uint8_t* __restrict__ out) {
     const uint64_t words = (len + 7) / 8;
     uint64_t* o = reinterpret_cast<uint64_t*>(out);
     for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < words;
          w += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t v = content8(key, w * 8, twin);
+        uint64_t v = content8(key, offset + w * 8, twin);
         if (w == words - 1 && (len & 7)) v &= (1ull << (8 * (len & 7))) - 1;
         o[w] = v;
     }
@@ -157,12 +157,14 @@ hipError_t launch_synth_stage_cas(const uint64_t* sizes, const uint64_t* cids, c
     return hipGetLastError();
 }
 
-hipError_t launch_synth_fill(uint64_t cid, uint32_t twin, uint64_t len, uint8_t* out, hipStream_t s) {
+hipError_t launch_synth_fill(uint64_t cid, uint32_t twin, uint64_t offset, uint64_t len, uint8_t* out,
+                             hipStream_t s) {
     if (len == 0) return hipSuccess;
     const uint64_t words = (len + 7) / 8;
     uint64_t grid = (words + 255) / 256;
     if (grid > 65536) grid = 65536;
-    hipLaunchKernelGGL(k_synth_fill, dim3((uint32_t)grid), dim3(256), 0, s, SEED ^ (cid * GOLDEN), twin, len, out);
+    hipLaunchKernelGGL(k_synth_fill, dim3((uint32_t)grid), dim3(256), 0, s, SEED ^ (cid * GOLDEN), twin, offset, len,
+                       out);
     return hipGetLastError();
 }
 

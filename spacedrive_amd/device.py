@@ -78,8 +78,9 @@ class Context:
         check(lib().sd_synth_stage_cas(self.handle, _ptr(d_sizes), _ptr(d_cids), _ptr(d_twins),
                                        _ptr(d_extents), n, _ptr(d_staged), _stream(stream)))
 
-    def synth_fill(self, cid: int, twin: int, length: int, d_out, stream=None) -> None:
-        check(lib().sd_synth_fill(self.handle, cid, twin, length, _ptr(d_out), _stream(stream)))
+    def synth_fill(self, cid: int, twin: int, length: int, d_out, stream=None, offset: int = 0) -> None:
+        """bytes [offset, offset + length) of synthetic content (cid, twin) -> d_out"""
+        check(lib().sd_synth_fill_at(self.handle, cid, twin, offset, length, _ptr(d_out), _stream(stream)))
 
     def valu_peak(self) -> float:
         v = ctypes.c_double(0)
@@ -222,6 +223,47 @@ class ChecksumBatch:
     def close(self) -> None:
         if self.handle:
             lib().sd_checksum_batch_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SplitChecksum:
+    """One file's checksum over the ranks of a communicator (sd_split_checksum): this rank
+    hashes its block range to CVs; the gathered CVs reduce to the file's BLAKE3."""
+
+    def __init__(self, ctx: Context, total_len: int, nranks: int = 1, rank: int = 0):
+        from .split import split_range
+        self.ctx = ctx
+        self.total_len, self.nranks, self.rank = int(total_len), nranks, rank
+        self.offset, self.len, self.cv_bytes = split_range(total_len, nranks, rank)
+        h = ctypes.c_void_p()
+        check(lib().sd_split_checksum_create(ctx.handle, self.total_len, nranks, rank, ctypes.byref(h)))
+        self.handle = h
+
+    def leaves(self, d_slice: torch.Tensor, d_cvs: torch.Tensor, stream=None) -> None:
+        assert d_cvs.numel() >= self.cv_bytes and d_slice.numel() >= self.len
+        check(lib().sd_split_checksum_leaves(self.ctx.handle, self.handle, _ptr(d_slice), _ptr(d_cvs),
+                                             _stream(stream)))
+
+    def root(self, d_cvs: torch.Tensor, d_hash32: torch.Tensor, stream=None) -> None:
+        assert d_cvs.numel() >= self.cv_bytes and d_hash32.numel() >= 32
+        check(lib().sd_split_checksum_root(self.ctx.handle, self.handle, _ptr(d_cvs), _ptr(d_hash32),
+                                           _stream(stream)))
+
+    def mgpu(self, comm: "Comm", d_slice: torch.Tensor, d_cvs: torch.Tensor, d_hash32: torch.Tensor,
+             stream=None) -> None:
+        assert d_cvs.numel() >= self.cv_bytes and d_slice.numel() >= self.len and d_hash32.numel() >= 32
+        check(lib().sd_split_checksum_mgpu(self.ctx.handle, comm.handle, self.handle, _ptr(d_slice), _ptr(d_cvs),
+                                           _ptr(d_hash32), _stream(stream)))
+
+    def close(self) -> None:
+        if self.handle:
+            lib().sd_split_checksum_destroy(self.handle)
             self.handle = None
 
     def __del__(self):  # pragma: no cover

@@ -790,3 +790,60 @@ def test_checksums_from_host_memory(ctx, oracle_native):
     want = oracle_native.checksums_simd(host.numpy(), arr_o, arr_l, nthreads=NT)
     for i in range(len(lens)):
         assert out.raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), lens[i]
+
+
+def test_split_checksum_ranks_on_one_gpu(ctx, oracle_native):
+    """One file over R ranks (sd_split_checksum_leaves / _root), the ranks emulated on one
+    device: each rank's leaves read only its own slice (a view at its byte range) and write
+    only its own CV slots, so one shared CV buffer stands for the gathered one.  Bit-exact
+    vs the oracle's BLAKE3 of the whole file, up to 4 GiB + 12345 (block CVs past 2^32)."""
+    from spacedrive_amd.device import SplitChecksum
+    MiB = 1 << 20
+    cases = [(0, (1, 2)), (1, (1, 3)), (MiB, (1, 2)), (MiB + 1, (1, 2, 3)), (5 * MiB + 3, (1, 2, 4, 7)),
+             (300 * MiB + 77, (3, 8)), ((4 << 30) + 12345, (1, 3, 8))]
+    for total, ranks in cases:
+        d = torch.zeros(total + 128, dtype=torch.uint8, device="cuda")
+        if total:
+            ctx.synth_fill(900, 0, total, d)
+        want = oracle_native.checksum_synth_mt(total, 900, 0, nthreads=NT).hex()
+        for R in ranks:
+            cvs = None
+            splits = [SplitChecksum(ctx, total, R, r) for r in range(R)]
+            for sc in splits:
+                if cvs is None:
+                    cvs = torch.zeros(sc.cv_bytes, dtype=torch.uint8, device="cuda")
+                sc.leaves(d[sc.offset:], cvs)
+            out = torch.zeros(32, dtype=torch.uint8, device="cuda")
+            splits[0].root(cvs, out)
+            torch.cuda.synchronize()
+            assert bytes(out.cpu().numpy()).hex() == want, (total, R)
+            for sc in splits:
+                sc.close()
+        del d
+
+
+def test_split_checksum_mgpu_through_rccl_single_rank(ctx, oracle_native):
+    """sd_split_checksum_mgpu over a real (single-rank) RCCL communicator, and the
+    torch.distributed statement (checksum_split) on the device, against the oracle."""
+    from spacedrive_amd import dedup
+    from spacedrive_amd._native import SdCasError
+    from spacedrive_amd.device import SplitChecksum
+    from spacedrive_amd.split import checksum_split
+    total = (37 << 20) + 5
+    d = torch.zeros(total + 128, dtype=torch.uint8, device="cuda")
+    ctx.synth_fill(901, 0, total, d)
+    want = oracle_native.checksum_synth_mt(total, 901, 0, nthreads=NT).hex()
+    comm = dedup.make_comm(ctx)
+    try:
+        sc = SplitChecksum(ctx, total, 1, 0)
+        cvs = torch.zeros(sc.cv_bytes, dtype=torch.uint8, device="cuda")
+        out = torch.zeros(32, dtype=torch.uint8, device="cuda")
+        sc.mgpu(comm, d, cvs, out)
+        torch.cuda.synchronize()
+        assert bytes(out.cpu().numpy()).hex() == want
+        bad = SplitChecksum(ctx, total, 2, 0)  # a split for another world size
+        with pytest.raises(SdCasError):
+            bad.mgpu(comm, d, torch.zeros(bad.cv_bytes, dtype=torch.uint8, device="cuda"), out)
+    finally:
+        comm.close()
+    assert checksum_split(d[:total + 64], total, ctx=ctx) == want
