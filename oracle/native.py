@@ -52,6 +52,8 @@ def lib():
         L.sdo_file_checksums.restype = I
         L.sdo_checksum_synth_mt.argtypes = [U64, U64, ctypes.c_uint32, I, I, P]
         L.sdo_checksum_synth_mt.restype = I
+        L.sdo_checksum_mt.argtypes = [P, U64, I, I, P]
+        L.sdo_checksum_mt.restype = I
         L.sdo_simd_level.argtypes = [I]
         L.sdo_simd_level.restype = I
         _lib = L
@@ -135,6 +137,13 @@ def checksum_synth_mt(size: int, cid: int, twin: int = 0, nthreads: int = 8, sim
     """Full BLAKE3 of one synthetic file, chunk-parallel on nthreads (multi-GiB files)."""
     out = ctypes.create_string_buffer(32)
     lib().sdo_checksum_synth_mt(size, cid, twin, nthreads, simd, out)
+    return out.raw
+
+
+def checksum_mt(data: np.ndarray, size: int, nthreads: int = 8, simd: int = -1) -> bytes:
+    """Full BLAKE3 of data[:size] (any uint8 array, e.g. a memmap), chunk-parallel."""
+    out = ctypes.create_string_buffer(32)
+    lib().sdo_checksum_mt(_p(data), size, nthreads, simd, out)
     return out.raw
 
 

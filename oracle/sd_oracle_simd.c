@@ -375,6 +375,7 @@ void sdo_subtree_simd(const uint8_t* data, uint64_t len, uint64_t chunk0, int ro
 void sdo_synth_fill(uint64_t cid, uint32_t twin, uint64_t offset, uint64_t length, uint8_t* out);
 
 typedef struct {
+    const uint8_t* data; /* the message in memory, or NULL: generate (cid, twin) per block */
     uint64_t size, C, cid;
     uint32_t twin;
     int lvl;
@@ -392,17 +393,19 @@ static void* mt_worker(void* arg) {
         if (c_begin >= j->C) break;
         uint64_t off = c_begin * 1024;
         uint64_t n = j->size - off < (1u << 20) ? j->size - off : (1u << 20);
-        sdo_synth_fill(j->cid, j->twin, off, n, buf);
+        const uint8_t* src = buf;
+        if (j->data) src = j->data + off;
+        else sdo_synth_fill(j->cid, j->twin, off, n, buf);
         uint64_t c_end = c_begin + 1024 < j->C ? c_begin + 1024 : j->C;
         uint64_t full_end = c_end == j->C ? j->C - 1 : c_end; /* the file's last chunk: scalar */
         for (uint64_t c0 = c_begin; c0 < full_end; c0 += 64) {
             int k = (int)((full_end - c0) < 64 ? (full_end - c0) : 64);
-            for (int i = 0; i < k; i++) ptrs[i] = buf + 1024 * (c0 + i - c_begin);
+            for (int i = 0; i < k; i++) ptrs[i] = src + 1024 * (c0 + i - c_begin);
             hash_many(j->lvl, ptrs, k, 16, c0, 1, 0, FS_CHUNK_START, FS_CHUNK_END, j->cvs + 32 * c0);
         }
         if (c_end == j->C) {
             uint32_t cv[8];
-            scalar_chunk(buf + 1024 * (j->C - 1 - c_begin), (uint32_t)(j->size - 1024 * (j->C - 1)), j->C - 1, 0, cv);
+            scalar_chunk(src + 1024 * (j->C - 1 - c_begin), (uint32_t)(j->size - 1024 * (j->C - 1)), j->C - 1, 0, cv);
             memcpy(j->cvs + 32 * (j->C - 1), cv, 32);
         }
     }
@@ -410,17 +413,23 @@ static void* mt_worker(void* arg) {
     return NULL;
 }
 
-int sdo_checksum_synth_mt(uint64_t size, uint64_t cid, uint32_t twin, int nthreads, int simd, uint8_t out[32]) {
+static int checksum_mt(const uint8_t* data, uint64_t size, uint64_t cid, uint32_t twin, int nthreads, int simd,
+                       uint8_t out[32]) {
     int lvl = sdo_simd_level(simd < 0 ? -1 : simd);
     if (lvl == 0 || size <= 1024) { /* scalar path or a single chunk */
+        void sdo_blake3(const uint8_t*, size_t, uint8_t*);
+        if (data) {
+            sdo_blake3(data, size, out);
+            return lvl;
+        }
         uint8_t* b = (uint8_t*)malloc(size ? size : 1);
         sdo_synth_fill(cid, twin, 0, size, b);
-        void sdo_blake3(const uint8_t*, size_t, uint8_t*);
         sdo_blake3(b, size, out);
         free(b);
         return lvl;
     }
     mt_job j;
+    j.data = data;
     j.size = size; j.C = (size + 1023) / 1024; j.cid = cid; j.twin = twin; j.lvl = lvl;
     j.cvs = (uint8_t*)malloc(32 * j.C);
     atomic_store(&j.next, 0);
@@ -449,4 +458,13 @@ int sdo_checksum_synth_mt(uint64_t size, uint64_t cid, uint32_t twin, int nthrea
     memcpy(out, o, 32);
     free(j.cvs);
     return lvl;
+}
+
+int sdo_checksum_synth_mt(uint64_t size, uint64_t cid, uint32_t twin, int nthreads, int simd, uint8_t out[32]) {
+    return checksum_mt(NULL, size, cid, twin, nthreads, simd, out);
+}
+
+/* the same, chunk-parallel, over a message in memory (a multi-GiB file's bytes) */
+int sdo_checksum_mt(const uint8_t* data, uint64_t size, int nthreads, int simd, uint8_t out[32]) {
+    return checksum_mt(data, size, 0, 0, nthreads, simd, out);
 }

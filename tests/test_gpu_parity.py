@@ -29,6 +29,16 @@ def ctx():
     return c
 
 
+@pytest.fixture(scope="module")
+def rccl_comm(ctx):
+    """One single-rank RCCL communicator (sd_comm_create) shared by the RCCL tests: creating
+    one costs seconds (RCCL init), the collectives themselves microseconds."""
+    from spacedrive_amd import dedup
+    comm = dedup.make_comm(ctx)
+    yield comm
+    comm.close()
+
+
 def stage_synth(ctx, sizes, cids, twins):
     from spacedrive_amd.device import stage_plan
     n = len(sizes)
@@ -573,7 +583,7 @@ def test_file_api_past_4gib_sparse(ctx, tmp_path, oracle_native):
     assert not st.any() and [g.tobytes().hex() for g in got] == ids
     sums = sd.file_checksums(paths[:1])
     data = np.memmap(paths[0], dtype=np.uint8, mode="r")
-    want = oracle_native.checksums_simd(data, [0], [sizes[0]], nthreads=1)[0].tobytes().hex()
+    want = oracle_native.checksum_mt(data, sizes[0], nthreads=NT).hex()
     assert sums[0] == want
 
 
@@ -725,7 +735,7 @@ def test_latency_policy_routes_and_agrees(ctx, tmp_path):
     assert after["cpu"] - before["cpu"] == 2 * len(paths) and after["batches"] == before["batches"]
 
 
-def test_dedup_mgpu_through_rccl_single_rank(ctx):
+def test_dedup_mgpu_through_rccl_single_rank(ctx, rccl_comm):
     """sd_cas_dedup_mgpu through a real RCCL communicator (1 rank: the
     all-gather and the grouped send/recv to self run; no world == 1 short-circuit) equals
     the host grouping; an undersized output fails with SD_ERR_CAPACITY before the exchange
@@ -739,29 +749,26 @@ def test_dedup_mgpu_through_rccl_single_rank(ctx):
     d_hash = torch.from_numpy(h.copy()).cuda()
     valid = (sizes != 0)
     d_valid = torch.from_numpy(valid.astype(np.uint8)).cuda()
-    comm = dedup.make_comm(ctx)
-    try:
-        base = 7_000_000  # a shard of a larger library
-        recs_h = np.stack([keys_from_hashes(h)[valid].view(np.int64), np.arange(base, base + n)[valid]], axis=1)
-        gr, grep, gng = group_host(recs_h)
-        small = torch.empty((10, 2), dtype=torch.int64, device="cuda")
-        with pytest.raises(SdCasError) as e:
-            ctx.dedup_mgpu(comm, d_hash, d_valid, n, base, small, small[:, 0].clone(), small[:, 0].clone(), 10)
-        assert e.value.rc == SD_ERR_CAPACITY and e.value.needed == int(valid.sum())
-        runner = dedup.RcclDedup(ctx, comm, d_hash.device, capacity=100)  # regrows once
-        for _ in range(2):  # and reuses its buffers
-            recs, rep, ng, owner = runner(d_hash, d_valid, n, base)
-            torch.cuda.synchronize()
-            assert ng == gng
-            assert np.array_equal(recs.cpu().numpy(), gr)
-            assert np.array_equal(rep.cpu().numpy(), grep)
-            want_owner = object_owners(torch.from_numpy(gr[:, 1].copy()), torch.from_numpy(grep), 100).numpy()
-            assert np.array_equal(owner.cpu().numpy(), want_owner)
-        # the torch.distributed exchange path gives the same outputs
-        r2, rep2, ng2, own2 = dedup.dedup_shard(ctx, d_hash, d_valid, n, base)
-        assert ng2 == gng and np.array_equal(r2.cpu().numpy(), gr) and np.array_equal(own2.cpu().numpy(), want_owner)
-    finally:
-        comm.close()
+    comm = rccl_comm
+    base = 7_000_000  # a shard of a larger library
+    recs_h = np.stack([keys_from_hashes(h)[valid].view(np.int64), np.arange(base, base + n)[valid]], axis=1)
+    gr, grep, gng = group_host(recs_h)
+    small = torch.empty((10, 2), dtype=torch.int64, device="cuda")
+    with pytest.raises(SdCasError) as e:
+        ctx.dedup_mgpu(comm, d_hash, d_valid, n, base, small, small[:, 0].clone(), small[:, 0].clone(), 10)
+    assert e.value.rc == SD_ERR_CAPACITY and e.value.needed == int(valid.sum())
+    runner = dedup.RcclDedup(ctx, comm, d_hash.device, capacity=100)  # regrows once
+    for _ in range(2):  # and reuses its buffers
+        recs, rep, ng, owner = runner(d_hash, d_valid, n, base)
+        torch.cuda.synchronize()
+        assert ng == gng
+        assert np.array_equal(recs.cpu().numpy(), gr)
+        assert np.array_equal(rep.cpu().numpy(), grep)
+        want_owner = object_owners(torch.from_numpy(gr[:, 1].copy()), torch.from_numpy(grep), 100).numpy()
+        assert np.array_equal(owner.cpu().numpy(), want_owner)
+    # the torch.distributed exchange path gives the same outputs
+    r2, rep2, ng2, own2 = dedup.dedup_shard(ctx, d_hash, d_valid, n, base)
+    assert ng2 == gng and np.array_equal(r2.cpu().numpy(), gr) and np.array_equal(own2.cpu().numpy(), want_owner)
 
 
 def test_checksums_from_host_memory(ctx, oracle_native):
@@ -822,10 +829,9 @@ def test_split_checksum_ranks_on_one_gpu(ctx, oracle_native):
         del d
 
 
-def test_split_checksum_mgpu_through_rccl_single_rank(ctx, oracle_native):
+def test_split_checksum_mgpu_through_rccl_single_rank(ctx, oracle_native, rccl_comm):
     """sd_split_checksum_mgpu over a real (single-rank) RCCL communicator, and the
     torch.distributed statement (checksum_split) on the device, against the oracle."""
-    from spacedrive_amd import dedup
     from spacedrive_amd._native import SdCasError
     from spacedrive_amd.device import SplitChecksum
     from spacedrive_amd.split import checksum_split
@@ -833,17 +839,14 @@ def test_split_checksum_mgpu_through_rccl_single_rank(ctx, oracle_native):
     d = torch.zeros(total + 128, dtype=torch.uint8, device="cuda")
     ctx.synth_fill(901, 0, total, d)
     want = oracle_native.checksum_synth_mt(total, 901, 0, nthreads=NT).hex()
-    comm = dedup.make_comm(ctx)
-    try:
-        sc = SplitChecksum(ctx, total, 1, 0)
-        cvs = torch.zeros(sc.cv_bytes, dtype=torch.uint8, device="cuda")
-        out = torch.zeros(32, dtype=torch.uint8, device="cuda")
-        sc.mgpu(comm, d, cvs, out)
-        torch.cuda.synchronize()
-        assert bytes(out.cpu().numpy()).hex() == want
-        bad = SplitChecksum(ctx, total, 2, 0)  # a split for another world size
-        with pytest.raises(SdCasError):
-            bad.mgpu(comm, d, torch.zeros(bad.cv_bytes, dtype=torch.uint8, device="cuda"), out)
-    finally:
-        comm.close()
+    comm = rccl_comm
+    sc = SplitChecksum(ctx, total, 1, 0)
+    cvs = torch.zeros(sc.cv_bytes, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(32, dtype=torch.uint8, device="cuda")
+    sc.mgpu(comm, d, cvs, out)
+    torch.cuda.synchronize()
+    assert bytes(out.cpu().numpy()).hex() == want
+    bad = SplitChecksum(ctx, total, 2, 0)  # a split for another world size
+    with pytest.raises(SdCasError):
+        bad.mgpu(comm, d, torch.zeros(bad.cv_bytes, dtype=torch.uint8, device="cuda"), out)
     assert checksum_split(d[:total + 64], total, ctx=ctx) == want

@@ -314,3 +314,13 @@ def test_c_oracle_checksum_mt_equals_streaming(oracle_native):
                                              np.array([3], np.uint32))[0].tobytes()
         for nt in (1, 3):
             assert oracle_native.checksum_synth_mt(size, 9, 3, nthreads=nt) == want, (size, nt)
+
+
+def test_checksum_mt_over_memory_equals_simd(oracle_native):
+    # the chunk-parallel in-memory checker (used for multi-GiB files in the GPU tests)
+    # agrees with the per-message SIMD restatement at the block and chunk boundaries
+    rng = np.random.default_rng(17)
+    for n in (0, 1, 1024, 1025, (1 << 20) - 1, 1 << 20, (1 << 20) + 1, (3 << 20) + 777):
+        d = rng.integers(0, 256, n + 64, dtype=np.uint8)
+        want = oracle_native.checksums_simd(d, [0], [n], nthreads=1)[0].tobytes()
+        assert oracle_native.checksum_mt(d, n, nthreads=3) == want, n
