@@ -115,6 +115,12 @@ void sd_cas_host_free(sd_cas_ctx* ctx, void* p);
  * staged-buffer size.  Pure host arithmetic; no device needed. */
 int sd_cas_stage_plan(const uint64_t* sizes, size_t n, sd_extent* extents_out,
                       uint64_t* total_bytes_out);
+/* Shards a library of n files (by global index, as the multi-GPU scan does) over nranks
+ * ranks in contiguous index ranges of balanced hashing cost: the cost
+ * of a file is the BLAKE3 compressions of its cas message (953 for every sampled file,
+ * 1..146 for a small one).  bounds_out[nranks + 1]: rank r hashes [bounds[r], bounds[r+1]),
+ * bounds ascending (sd_cas_dedup_mgpu's index-ordered fast path).  Pure host arithmetic. */
+int sd_shard_plan(const uint64_t* sizes, size_t n, int nranks, uint64_t* bounds_out);
 /* Reads one file into its extent exactly as generate_cas_id does (le64 header, then the
  * whole file until EOF, or head/samples by read_exact and the tail at the file's real end),
  * zero-padding to the next 64-byte boundary.  The extent is in/out: for a whole-kind file

@@ -87,6 +87,7 @@ extern "C" {
                              n: u64, global_index_base: u64, chunk_size: u64, d_records_out: *mut u64,
                              d_rep_out: *mut u64, d_owner_out: *mut u64, capacity: u64, m_out: *mut u64,
                              n_groups_out: *mut u64, stream: *mut c_void) -> c_int;
+    pub fn sd_shard_plan(sizes: *const u64, n: usize, nranks: c_int, bounds_out: *mut u64) -> c_int;
     // one file's checksum over many GPUs (its 1 MiB blocks sharded by rank)
     pub fn sd_split_range(total_len: u64, nranks: c_int, rank: c_int, offset: *mut u64, len: *mut u64,
                           cv_bytes: *mut u64) -> c_int;

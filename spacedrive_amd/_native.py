@@ -93,6 +93,7 @@ SIGNATURES = [
     ("sd_comm_destroy", None, [P]),
     ("sd_cas_dedup_mgpu", I32, [P, P, P, P, U64, U64, U64, P, P, P, U64, PU64, PU64, P]),
     ("sd_split_range", I32, [U64, I32, I32, PU64, PU64, PU64]),
+    ("sd_shard_plan", I32, [P, SZ, I32, P]),
     ("sd_split_checksum_create", I32, [P, U64, I32, I32, ctypes.POINTER(P)]),
     ("sd_split_checksum_destroy", None, [P]),
     ("sd_split_checksum_leaves", I32, [P, P, P, P, P]),

@@ -55,6 +55,28 @@ SplitPlan split_plan(uint64_t total, int nranks, int rank) {
 extern "C" {
 const char* sd_cas_last_error(void) { return g_err.c_str(); }
 int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }
+int sd_shard_plan(const uint64_t* sizes, size_t n, int nranks, uint64_t* bounds_out) {
+    SD_GUARD_BEGIN
+    if (!bounds_out || (n && !sizes)) throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (nranks < 1 || nranks > 4096) throw sd_failure(SD_ERR_INVALID, "nranks out of range");
+    std::vector<uint64_t> prefix(n + 1, 0);  // prefix[i] = cost of files [0, i)
+    for (size_t i = 0; i < n; i++) {
+        const uint64_t len = sizes[i] <= SD_MINIMUM_FILE_SIZE ? 8 + sizes[i] : SD_SAMPLED_MSG_LEN;
+        prefix[i + 1] = prefix[i] + msg_compressions(len);
+    }
+    const uint64_t total = prefix[n];
+    bounds_out[0] = 0;
+    for (int r = 1; r < nranks; r++) {  // first file whose cost starts at or past r/R of the total
+        const unsigned __int128 target = (unsigned __int128)total * (unsigned)r / (unsigned)nranks;
+        const uint64_t t = (uint64_t)target;
+        const size_t i = (size_t)(std::lower_bound(prefix.begin(), prefix.end(), t) - prefix.begin());
+        bounds_out[r] = std::max<uint64_t>(bounds_out[r - 1], std::min<uint64_t>(i, n));
+    }
+    bounds_out[nranks] = n;
+    return SD_OK;
+    SD_GUARD_END
+}
+
 int sd_split_range(uint64_t total_len, int nranks, int rank, uint64_t* offset, uint64_t* len, uint64_t* cv_bytes) {
     SD_GUARD_BEGIN
     if (!offset || !len || !cv_bytes) throw sd_failure(SD_ERR_INVALID, "null argument");

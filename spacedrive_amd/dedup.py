@@ -32,6 +32,18 @@ import torch
 import torch.distributed as dist
 
 
+def shard_plan(sizes, nranks: int) -> np.ndarray:
+    """Contiguous index ranges of balanced hashing cost for a library scan over `nranks`
+    GPUs (sd_shard_plan): rank r hashes files [bounds[r], bounds[r+1]).  The cost of a file
+    is the BLAKE3 compressions of its cas message."""
+    import ctypes
+    from ._native import check, lib
+    s = np.ascontiguousarray(sizes, dtype=np.uint64)
+    bounds = np.zeros(nranks + 1, np.uint64)
+    check(lib().sd_shard_plan(s.ctypes.data if s.size else None, ctypes.c_size_t(s.size), nranks, bounds.ctypes.data))
+    return bounds
+
+
 def dest_of(keys: np.ndarray, nparts: int) -> np.ndarray:
     """Destination rank of a cas_id key: its top 16 bits scaled to nparts (contiguous ranges)."""
     return (((keys >> np.uint64(48)) * np.uint64(nparts)) >> np.uint64(16)).astype(np.int64)

@@ -101,3 +101,27 @@ def test_shards_ascend_is_checked_across_ranks(tmp_path):
                        start_method="spawn")
     for r in range(world):
         assert np.load(tmp_path / f"a{r}.npy").tolist() == [True, False, False]
+
+
+def test_shard_plan_balances_hashing_cost():
+    """sd_shard_plan: contiguous, ascending, complete, and balanced in BLAKE3 compressions
+    (a sampled file costs 953, a small one 1..146) to within one file's cost per boundary."""
+    from spacedrive_amd.dedup import shard_plan
+    from spacedrive_amd import synth
+
+    def cost(s):
+        m = 8 + s if s <= 102400 else 57352
+        c = max(1, -(-m // 1024))
+        last = m - (c - 1) * 1024
+        return (c - 1) * 16 + max(1, -(-last // 64)) + (c - 1)
+
+    sizes, _, _ = synth.library(0, 50_000, 50_000)
+    sizes = np.asarray(sizes, np.uint64)
+    sizes[:20000] = 5  # a skewed library: small files first, then the mixture
+    costs = np.array([cost(int(s)) for s in sizes])
+    for R in (1, 2, 3, 8, 64):
+        b = shard_plan(sizes, R).astype(np.int64)
+        assert b[0] == 0 and b[-1] == len(sizes) and np.all(np.diff(b) >= 0)
+        per = np.array([costs[b[r]:b[r + 1]].sum() for r in range(R)])
+        assert per.max() - per.min() <= 2 * costs.max(), (R, per.min(), per.max())
+    assert list(shard_plan(np.zeros(0, np.uint64), 3)) == [0, 0, 0, 0]
