@@ -34,15 +34,15 @@
 struct sd_comm {
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0, device = 0;
-    // device scratch, grown on demand: counts[nranks], the partitioned send records, the
-    // all-gather rows (send row + nranks rows)
-    void* d_counts = nullptr;
+    // device scratch, grown on demand: the partitioned send records, the all-gather rows
+    // (send row + nranks rows)
     void* d_send = nullptr;
     size_t send_bytes = 0;
     void* d_rows = nullptr;
-    uint64_t* h_rows = nullptr;  // pinned
+    void* d_part_scratch = nullptr;  // sdk::dedup_partition's scratch; its last u64 = valid records
+    uint64_t* h_rows = nullptr;      // pinned: this rank's row extras, then all rows, then n_valid
     ~sd_comm() {
-        if (d_counts) (void)hipFree(d_counts);
+        if (d_part_scratch) (void)hipFree(d_part_scratch);
         if (d_send) (void)hipFree(d_send);
         if (d_rows) (void)hipFree(d_rows);
         if (h_rows) (void)hipHostFree(h_rows);
@@ -103,9 +103,9 @@ int sd_comm_create(sd_cas_ctx* ctx, const uint8_t* id, int nranks, int rank, sd_
     memcpy(&uid, id, SD_COMM_ID_BYTES);
     NCCL_OK(ncclCommInitRank(&c->comm, nranks, uid, rank));
     const size_t row = (size_t)nranks + ROW_EXTRA;
-    HIP_OK(hipMalloc(&c->d_counts, sizeof(uint64_t) * nranks));
     HIP_OK(hipMalloc(&c->d_rows, sizeof(uint64_t) * row * (nranks + 1)));
-    HIP_OK(hipHostMalloc((void**)&c->h_rows, sizeof(uint64_t) * row * (nranks + 1), hipHostMallocDefault));
+    HIP_OK(hipMalloc(&c->d_part_scratch, sdk::dedup_partition_scratch(nranks)));
+    HIP_OK(hipHostMalloc((void**)&c->h_rows, sizeof(uint64_t) * (row * (nranks + 1) + 1), hipHostMallocDefault));
     *out = c.release();
     return SD_OK;
     SD_GUARD_END
@@ -139,22 +139,26 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
         comm->send_bytes = 16 * (n ? n : 1);
         HIP_OK(hipMalloc(&comm->d_send, comm->send_bytes));
     }
-    uint64_t n_valid = 0;
-    check_rc(sd_dedup_partition(ctx, d_hash32, d_valid, n, global_index_base, R, (uint64_t*)comm->d_counts,
-                                (uint64_t*)comm->d_send, &n_valid, stream));
+    // (the partition counts go straight into this rank's all-gather row; no host sync here)
+    uint64_t* d_row = (uint64_t*)comm->d_rows;
+    uint64_t* d_all = d_row + row;
+    const size_t psb = sdk::dedup_partition_scratch(R);
+    uint64_t* pscratch = (uint64_t*)comm->d_part_scratch;
+    HIP_OK(sdk::dedup_partition(d_hash32, d_valid, n, global_index_base, R, d_row, (uint64_t*)comm->d_send, pscratch,
+                                s));
     // 2. all-gather of (counts, index base, file count, capacity)
     uint64_t* h_row = comm->h_rows;
     h_row[R] = global_index_base;
     h_row[R + 1] = n;
     h_row[R + 2] = capacity;
-    uint64_t* d_row = (uint64_t*)comm->d_rows;
-    uint64_t* d_all = d_row + row;
-    HIP_OK(hipMemcpyAsync(d_row, comm->d_counts, sizeof(uint64_t) * R, hipMemcpyDeviceToDevice, s));
     HIP_OK(hipMemcpyAsync(d_row + R, h_row + R, sizeof(uint64_t) * ROW_EXTRA, hipMemcpyHostToDevice, s));
     NCCL_OK(ncclAllGather(d_row, d_all, row, ncclUint64, comm->comm, s));
     uint64_t* all = comm->h_rows + row;
     HIP_OK(hipMemcpyAsync(all, d_all, sizeof(uint64_t) * row * R, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
+    HIP_OK(hipMemcpyAsync(all + row * R, pscratch + psb / sizeof(uint64_t) - 1, sizeof(uint64_t),
+                          hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));  // the one sync before the exchange: every rank's row
+    const uint64_t n_valid = all[row * R];
     auto cnt = [&](int src, int dst) { return all[(size_t)src * row + dst]; };
     std::vector<uint64_t> recv_total(R, 0);
     for (int src = 0; src < R; src++)
@@ -185,9 +189,8 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
     if (soff != n_valid) throw sd_failure(SD_ERR_INTERNAL, "partition counts disagree with the valid records");
     // 4. group by cas_id and assign Objects (chunk-of-100 rule) on the received records
     uint64_t ng = 0;
-    check_rc(sd_dedup_group(ctx, d_records_out, *m_out, ascending ? SD_DEDUP_INDEX_SORTED : 0, d_rep_out, &ng,
-                            stream));
-    check_rc(sd_dedup_owners(ctx, d_records_out, *m_out, d_rep_out, chunk_size, d_owner_out, stream));
+    dedup_group_owners(ctx, d_records_out, *m_out, ascending ? SD_DEDUP_INDEX_SORTED : 0, d_rep_out, chunk_size,
+                       d_owner_out, &ng, s);
     *n_groups_out = ng;
     return SD_OK;
     SD_GUARD_END

@@ -523,6 +523,46 @@ int32_t cas_overflow(SlotPair& sl, int& cur, Streamer& st, const char* path, uin
 int sd_ctx_device(const sd_cas_ctx* ctx) { return ctx->device; }
 const SplitPlan& sd_split_plan_of(const sd_split_checksum* x) { return x->sp; }
 
+// Grouping, and (owner_chunk > 0) the Object rule on its output, with one host sync: with
+// the LDS-bucket grouping the owners kernel is queued right behind it, before the sync that
+// reads the group count and the overflow flag; on an overflow both run again on the radix
+// path.  Throws sd_failure.
+void dedup_group_owners(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, int flags, uint64_t* d_rep,
+                        uint64_t owner_chunk, uint64_t* d_owner, uint64_t* n_groups, hipStream_t s) {
+    ctx->bind();
+    size_t need = 0;
+    HIP_CHECK(sdk::dedup_group(d_records, m, flags, d_rep, nullptr, nullptr, &need, s));
+    auto slot = ctx->acquire();
+    struct Rel {
+        sd_cas_ctx* c;
+        std::unique_ptr<Slot>* s;
+        ~Rel() { c->release(std::move(*s)); }
+    } rel{ctx, &slot};
+    const bool buckets = tuning_get(SD_TUNE_DEDUP_VARIANT) == 1 && m > 0 && m < (1ull << 31);
+    if (buckets) need = std::max(need, sdk::dedup_group_buckets_scratch(m));
+    slot->staged.ensure(need);
+    slot->hashes.ensure(8 * sizeof(uint64_t));
+    slot->host_hashes.ensure(2 * sizeof(uint64_t));
+    size_t have = slot->staged.bytes;
+    if (buckets) {
+        HIP_CHECK(sdk::dedup_group_buckets(d_records, m, d_rep, slot->hashes.as<uint64_t>(), slot->staged.p, have, s));
+        HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, slot->hashes.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        if (owner_chunk) HIP_CHECK(sdk::dedup_owners(d_records, m, d_rep, owner_chunk, d_owner, s));  // speculative
+        HIP_CHECK(hipStreamSynchronize(s));
+        const uint64_t* st = reinterpret_cast<const uint64_t*>(slot->host_hashes.p);
+        if (st[1] == 0) {
+            *n_groups = st[0];
+            return;
+        }
+        flags &= ~SD_DEDUP_INDEX_SORTED;  // a bucket overflowed: d_records is now a permutation
+    }
+    HIP_CHECK(sdk::dedup_group(d_records, m, flags, d_rep, slot->hashes.as<uint64_t>(), slot->staged.p, &have, s));
+    HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, slot->hashes.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    if (owner_chunk) HIP_CHECK(sdk::dedup_owners(d_records, m, d_rep, owner_chunk, d_owner, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    *n_groups = *reinterpret_cast<uint64_t*>(slot->host_hashes.p);
+}
+
 // ============================================================================ C ABI
 extern "C" {
 
@@ -1227,37 +1267,7 @@ int sd_dedup_group(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, int flags, 
                    uint64_t* n_groups, void* stream) {
     SD_GUARD_BEGIN
     if (!ctx || !n_groups || (m && (!d_records || !d_rep))) throw sd_failure(SD_ERR_INVALID, "null argument");
-    ctx->bind();
-    hipStream_t s = ctx->pick(stream);
-    size_t need = 0;
-    HIP_CHECK(sdk::dedup_group(d_records, m, flags, d_rep, nullptr, nullptr, &need, s));
-    auto slot = ctx->acquire();
-    struct Rel {
-        sd_cas_ctx* c;
-        std::unique_ptr<Slot>* s;
-        ~Rel() { c->release(std::move(*s)); }
-    } rel{ctx, &slot};
-    const bool buckets = tuning_get(SD_TUNE_DEDUP_VARIANT) == 1 && m > 0 && m < (1ull << 31);
-    if (buckets) need = std::max(need, sdk::dedup_group_buckets_scratch(m));
-    slot->staged.ensure(need);
-    slot->hashes.ensure(8 * sizeof(uint64_t));
-    slot->host_hashes.ensure(2 * sizeof(uint64_t));
-    size_t have = slot->staged.bytes;
-    if (buckets) {
-        HIP_CHECK(sdk::dedup_group_buckets(d_records, m, d_rep, slot->hashes.as<uint64_t>(), slot->staged.p, have, s));
-        HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, slot->hashes.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipStreamSynchronize(s));
-        const uint64_t* st = reinterpret_cast<const uint64_t*>(slot->host_hashes.p);
-        if (st[1] == 0) {
-            *n_groups = st[0];
-            return SD_OK;
-        }
-        flags &= ~SD_DEDUP_INDEX_SORTED;  // a bucket overflowed: d_records is now a permutation
-    }
-    HIP_CHECK(sdk::dedup_group(d_records, m, flags, d_rep, slot->hashes.as<uint64_t>(), slot->staged.p, &have, s));
-    HIP_CHECK(hipMemcpyAsync(slot->host_hashes.p, slot->hashes.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    *n_groups = *reinterpret_cast<uint64_t*>(slot->host_hashes.p);
+    dedup_group_owners(ctx, d_records, m, flags, d_rep, 0, nullptr, n_groups, ctx->pick(stream));
     return SD_OK;
     SD_GUARD_END
 }

@@ -8,6 +8,9 @@
 
 // the device a context was created on
 int sd_ctx_device(const sd_cas_ctx* ctx);
+// sd_dedup_group followed by sd_dedup_owners (owner_chunk > 0) with a single host sync
+void dedup_group_owners(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, int flags, uint64_t* d_rep,
+                        uint64_t owner_chunk, uint64_t* d_owner, uint64_t* n_groups, hipStream_t s);
 // the block partition of a split-file checksum object
 const SplitPlan& sd_split_plan_of(const sd_split_checksum* x);
 namespace sdk {
