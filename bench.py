@@ -545,10 +545,22 @@ def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int
         def run():
             sc.leaves(d_slice, cvs, stream)
             sc.root(cvs, out32, stream)
-    else:
-        return {"skipped": "needs libsdcas's RCCL communicator at N > 1 (--dedup rccl, nccl backend)"}
+    else:  # rehearsal transport (gloo): the CV slots gathered through host memory
+        from spacedrive_amd.split import _gather_slots
+        q = sc.cv_bytes // (32 * world)
+
+        def run():
+            sc.leaves(d_slice, cvs, stream)
+            h = cvs.cpu()
+            _gather_slots(h, rank, world, q, None)
+            cvs.copy_(h)
+            sc.root(cvs, out32, stream)
     run()
-    warm(run, stream, warm_ms)
+    if world == 1:
+        warm(run, stream, warm_ms)
+    else:  # run() is a collective: every rank must call it the same number of times
+        for _ in range(3):
+            run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -556,7 +568,7 @@ def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int
     for _ in range(reps):
         run()
     torch.cuda.synchronize()
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev if comm is not None else "cpu")
     if world > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     wall_ms = float(dt.item()) / reps * 1e3
@@ -565,10 +577,11 @@ def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int
            "ms_per_file": wall_ms, "GBps": total / (wall_ms * 1e-3) / 1e9, "scaling": "strong",
            "rank0_leaves_ms": leaves_ms, "rank0_bytes": sc.len,
            "rank0_leaves_GBps": sc.len / (leaves_ms * 1e-3) / 1e9 if sc.len else None,
-           "transport": "rccl" if comm is not None else "none (N=1)",
-           "note": "one file over all ranks: per-rank block CVs, in-place ncclAllGather of the CV slots, "
-                   "reduce on every rank (sd_split_checksum_mgpu); wall time with barriers, max over ranks"}
-    h = out32.clone()
+           "transport": "rccl" if comm is not None else ("none (N=1)" if world == 1 else "gloo via host (rehearsal)"),
+           "note": "one file over all ranks: per-rank block CVs, the CV slots gathered in rank order (in-place "
+                   "ncclAllGather inside sd_split_checksum_mgpu over RCCL), reduce on every rank; wall time with "
+                   "barriers, max over ranks"}
+    h = out32.clone() if comm is not None else out32.cpu()
     if world > 1:  # every rank must hold the same hash
         allh = [torch.zeros_like(h) for _ in range(world)]
         dist.all_gather(allh, h)
@@ -578,7 +591,7 @@ def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int
         ref = torch.zeros(32, dtype=torch.uint8, device=dev)
         cb.run(d_slice, ref, stream)
         torch.cuda.synchronize()
-        res["equal_to_checksum_batch"] = bool(torch.equal(ref, h))
+        res["equal_to_checksum_batch"] = bool(torch.equal(ref.cpu(), h.cpu()))
         cb.close()
     res["hash"] = bytes(h.cpu().numpy()).hex()
     sc.close()
@@ -590,6 +603,9 @@ def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int
 # ------------------------------------------------------------------ main
 def main():
     args = parse()
+    if os.environ.get("SD_BENCH_STACKS_AFTER"):  # debugging a stuck run: dump every thread's stack
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["SD_BENCH_STACKS_AFTER"]), repeat=True)
     # stdout carries exactly one JSON line: anything native libraries print there (RCCL's
     # version banner at communicator init) goes to stderr instead
     json_out = os.fdopen(os.dup(1), "w")
