@@ -71,7 +71,7 @@ void check_rc(int rc) {
 }
 
 // row layout of the all-gather: counts[nranks], index base, local file count, capacity
-constexpr int ROW_EXTRA = 3;
+constexpr int ROW_EXTRA = SD_EXCHANGE_ROW_EXTRA;
 
 }  // namespace
 
@@ -159,37 +159,26 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
                           hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));  // the one sync before the exchange: every rank's row
     const uint64_t n_valid = all[row * R];
-    auto cnt = [&](int src, int dst) { return all[(size_t)src * row + dst]; };
-    std::vector<uint64_t> recv_total(R, 0);
-    for (int src = 0; src < R; src++)
-        for (int dst = 0; dst < R; dst++) recv_total[dst] += cnt(src, dst);
-    bool fits = true, ascending = true;
-    for (int r = 0; r < R; r++) {
-        if (recv_total[r] > all[(size_t)r * row + R + 2]) fits = false;
-        if (r + 1 < R && all[(size_t)r * row + R] + all[(size_t)r * row + R + 1] > all[(size_t)(r + 1) * row + R])
-            ascending = false;
-    }
-    *m_out = recv_total[me];
+    const ExchangePlan plan = exchange_plan(all, R, me);
+    *m_out = plan.recv_total;
     *n_groups_out = 0;
-    if (!fits)  // every rank sees the same matrix, so every rank stops here
+    if (!plan.fits)  // every rank sees the same matrix, so every rank stops here
         throw sd_failure(SD_ERR_CAPACITY, "an output capacity is smaller than the records its rank receives "
                                          "(*m_out = this rank's requirement)");
+    if (plan.send_total != n_valid) throw sd_failure(SD_ERR_INTERNAL, "partition counts disagree with the valid records");
     // 3. the all-to-all of the 16-byte records: one send and one receive per peer
     const uint64_t* send = (const uint64_t*)comm->d_send;
-    uint64_t soff = 0, roff = 0;
     NCCL_OK(ncclGroupStart());
     for (int p = 0; p < R; p++) {
-        const uint64_t sc = cnt(me, p), rc = cnt(p, me);
-        if (sc) NCCL_OK(ncclSend(send + 2 * soff, 2 * sc, ncclUint64, p, comm->comm, s));
-        if (rc) NCCL_OK(ncclRecv(d_records_out + 2 * roff, 2 * rc, ncclUint64, p, comm->comm, s));
-        soff += sc;
-        roff += rc;
+        if (plan.send_cnt[p])
+            NCCL_OK(ncclSend(send + 2 * plan.send_off[p], 2 * plan.send_cnt[p], ncclUint64, p, comm->comm, s));
+        if (plan.recv_cnt[p])
+            NCCL_OK(ncclRecv(d_records_out + 2 * plan.recv_off[p], 2 * plan.recv_cnt[p], ncclUint64, p, comm->comm, s));
     }
     NCCL_OK(ncclGroupEnd());
-    if (soff != n_valid) throw sd_failure(SD_ERR_INTERNAL, "partition counts disagree with the valid records");
     // 4. group by cas_id and assign Objects (chunk-of-100 rule) on the received records
     uint64_t ng = 0;
-    dedup_group_owners(ctx, d_records_out, *m_out, ascending ? SD_DEDUP_INDEX_SORTED : 0, d_rep_out, chunk_size,
+    dedup_group_owners(ctx, d_records_out, *m_out, plan.ascending ? SD_DEDUP_INDEX_SORTED : 0, d_rep_out, chunk_size,
                        d_owner_out, &ng, s);
     *n_groups_out = ng;
     return SD_OK;

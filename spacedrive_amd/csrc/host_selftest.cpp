@@ -377,6 +377,51 @@ void test_coalescer() {
 
 }  // namespace
 
+// ------------------------------------------------------------------ multi-GPU plans
+void test_exchange_plan() {
+    // 3 ranks: rows [to0, to1, to2, base, n, capacity]
+    const int R = 3;
+    std::vector<uint64_t> rows = {5, 1, 0, 0, 10, 100,    // rank 0: files [0, 10)
+                                  2, 0, 7, 10, 10, 100,   // rank 1: files [10, 20)
+                                  0, 3, 4, 20, 10, 100};  // rank 2: files [20, 30)
+    uint64_t sent_to[R][R] = {}, recv_from[R][R] = {};
+    for (int me = 0; me < R; me++) {
+        const ExchangePlan p = exchange_plan(rows.data(), R, me);
+        CHECK(p.fits && p.ascending);
+        uint64_t so = 0, ro = 0;
+        for (int q = 0; q < R; q++) {
+            CHECK(p.send_off[q] == so && p.recv_off[q] == ro);  // destination / source order
+            so += p.send_cnt[q];
+            ro += p.recv_cnt[q];
+            sent_to[me][q] = p.send_cnt[q];
+            recv_from[me][q] = p.recv_cnt[q];
+        }
+        CHECK(p.send_total == so && p.recv_total == ro);
+    }
+    for (int a = 0; a < R; a++)
+        for (int b = 0; b < R; b++) CHECK(sent_to[a][b] == recv_from[b][a]);  // every send has its receive
+    CHECK(exchange_plan(rows.data(), R, 0).recv_total == 7 && exchange_plan(rows.data(), R, 2).recv_total == 11);
+    // rank 2's capacity short: every rank sees it
+    std::vector<uint64_t> tight = rows;
+    tight[2 * 6 + 5] = 10;
+    for (int me = 0; me < R; me++) CHECK(!exchange_plan(tight.data(), R, me).fits);
+    // overlapping index ranges: no ascending fast path, on any rank
+    std::vector<uint64_t> overlap = rows;
+    overlap[1 * 6 + 3] = 5;
+    for (int me = 0; me < R; me++) CHECK(!exchange_plan(overlap.data(), R, me).ascending);
+    // one file over R ranks: contiguous block ranges covering the file
+    for (uint64_t total : {0ull, 1ull, (1ull << 20) + 1, (7ull << 20) + 5})
+        for (int r = 1; r <= 5; r++) {
+            uint64_t end = 0;
+            for (int k = 0; k < r; k++) {
+                const SplitPlan sp = split_plan(total, r, k);
+                CHECK(sp.off == end);
+                end = sp.off + sp.len;
+            }
+            CHECK(end == total);
+        }
+}
+
 int main() {
     char tmpl[] = "/tmp/sd_selftest_XXXXXX";
     if (!mkdtemp(tmpl)) return 2;
@@ -388,6 +433,7 @@ int main() {
     test_pool_growth();
     test_cpu_batches();
     test_coalescer();
+    test_exchange_plan();
     // clean up the scratch directory
     if (DIR* d = opendir(g_dir.c_str())) {
         while (dirent* e = readdir(d))

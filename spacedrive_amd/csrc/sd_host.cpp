@@ -52,6 +52,32 @@ SplitPlan split_plan(uint64_t total, int nranks, int rank) {
     return p;
 }
 
+ExchangePlan exchange_plan(const uint64_t* rows, int R, int me) {
+    const size_t row = (size_t)R + SD_EXCHANGE_ROW_EXTRA;
+    auto cnt = [&](int src, int dst) { return rows[(size_t)src * row + dst]; };
+    ExchangePlan p;
+    p.send_cnt.resize(R);
+    p.send_off.resize(R);
+    p.recv_cnt.resize(R);
+    p.recv_off.resize(R);
+    for (int r = 0; r < R; r++) {
+        uint64_t in = 0;
+        for (int src = 0; src < R; src++) in += cnt(src, r);
+        if (in > rows[(size_t)r * row + R + 2]) p.fits = false;
+        if (r + 1 < R && rows[(size_t)r * row + R] + rows[(size_t)r * row + R + 1] > rows[(size_t)(r + 1) * row + R])
+            p.ascending = false;
+    }
+    for (int q = 0; q < R; q++) {
+        p.send_cnt[q] = cnt(me, q);
+        p.send_off[q] = p.send_total;
+        p.send_total += p.send_cnt[q];
+        p.recv_cnt[q] = cnt(q, me);
+        p.recv_off[q] = p.recv_total;
+        p.recv_total += p.recv_cnt[q];
+    }
+    return p;
+}
+
 extern "C" {
 const char* sd_cas_last_error(void) { return g_err.c_str(); }
 int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }

@@ -139,6 +139,20 @@ struct SplitPlan {
 };
 SplitPlan split_plan(uint64_t total, int nranks, int rank);
 
+// The multi-GPU dedup exchange (sd_cas_dedup_mgpu) as seen by rank `me` from the gathered
+// rows of all R ranks, row r = [count to rank 0 .. count to rank R-1, index base, file
+// count, output capacity].  Every rank derives `fits` and `ascending` from the same matrix,
+// so all ranks take the same branch.  Records go out in destination order (the partition's
+// order) and come in in source-rank order.
+struct ExchangePlan {
+    std::vector<uint64_t> send_cnt, send_off, recv_cnt, recv_off;  // per peer, in records
+    uint64_t send_total = 0, recv_total = 0;
+    bool fits = true;       // every rank's capacity holds what it receives
+    bool ascending = true;  // the ranks' index ranges ascend with the rank
+};
+constexpr int SD_EXCHANGE_ROW_EXTRA = 3;
+ExchangePlan exchange_plan(const uint64_t* rows, int R, int me);
+
 // ------------------------------------------------------------------ file reading
 // Reads one file's cas message into staged + e.msg_offset exactly as generate_cas_id reads
 // it (cas.rs:25-58) and zero-pads it to the next 64-byte boundary.  Returns an
