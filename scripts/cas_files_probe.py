@@ -19,6 +19,9 @@ from spacedrive_amd import synth  # noqa: E402
 from spacedrive_amd._native import check, lib  # noqa: E402
 
 
+REPS = 5
+
+
 def main():
     k = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
     ctx = sd.default_context(0)
@@ -39,11 +42,11 @@ def main():
         buf = ctypes.create_string_buffer(17 * k)
         st = np.zeros(k, np.int32)
         ref = None
-        for mb in (16, 32, 64, 128, 256):
+        for mb in (32, 64):
             check(L.sd_cas_set_tuning(b"files_window_mb", mb))
             for th in (16, 32):
                 best = 1e9
-                for _ in range(3):
+                for _ in range(REPS):
                     t0 = time.perf_counter()
                     check(L.sd_cas_ids_files(ctx.handle, arr, sz.ctypes.data, k, buf, st.ctypes.data, th))
                     best = min(best, time.perf_counter() - t0)
@@ -58,7 +61,7 @@ def main():
         stage = np.zeros(total + 64, np.uint8)
         for th in (16, 32):
             best = 1e9
-            for _ in range(3):
+            for _ in range(REPS):
                 t0 = time.perf_counter()
                 check(L.sd_cas_stage_files(arr, ext2.ctypes.data, k, stage.ctypes.data, st.ctypes.data, th))
                 best = min(best, time.perf_counter() - t0)

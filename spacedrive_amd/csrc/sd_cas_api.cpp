@@ -793,67 +793,114 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
     ctx->bind();
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 64) nthreads = 64;
-    std::shared_ptr<StagePool> pool = ctx->stage_pool(nthreads);
+    // nthreads reader threads stage in the background (start/wait) while this thread plans,
+    // launches and harvests the windows
+    std::shared_ptr<StagePool> pool = ctx->stage_pool(nthreads + 1);
     const uint64_t WINDOW = (uint64_t)std::max(1, tuning_get(SD_TUNE_FILES_WINDOW_MB)) << 20;
     SlotPair slots(ctx);
     sd_cas_batch batches[2];
-    struct Win {
-        std::vector<size_t> files;  // hashed files of the window, in extent order
-        bool busy = false;
+    struct Win {  // the window being staged into a slot's pinned buffer
+        std::vector<sd_extent> ext;
+        std::vector<size_t> idx;  // input index of each extent
+        uint64_t bytes = 0;
     } wins[2];
+    struct Launched {  // the window in flight on a slot's stream
+        std::vector<size_t> files;  // hashed files, in extent order
+        bool busy = false;
+    } launched[2];
+    hipEvent_t copied[2] = {nullptr, nullptr};  // the slot's pinned buffer has been read by its H2D
+    bool copy_pending[2] = {false, false};
+    struct Cleanup {  // on any exit: no reader left writing, no event leaked
+        StagePool* pool;
+        bool staging = false;
+        hipEvent_t* ev;
+        ~Cleanup() {
+            if (staging) pool->wait();
+            for (int k = 0; k < 2; k++)
+                if (ev[k]) (void)hipEventDestroy(ev[k]);
+        }
+    } cleanup{pool.get(), false, copied};
+    for (int k = 0; k < 2; k++) HIP_CHECK(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming));
     auto harvest = [&](int k) {
-        if (!wins[k].busy) return;
+        if (!launched[k].busy) return;
         HIP_CHECK(hipStreamSynchronize(slots[k].stream));
         const uint8_t* h = slots[k].host_hashes.u8();
-        for (size_t q = 0; q < wins[k].files.size(); q++)
-            to_hex(h + q * 32, 8, out_hex17 + wins[k].files[q] * 17);  // cas.rs:61 to_hex()[..16]
-        wins[k].busy = false;
+        for (size_t q = 0; q < launched[k].files.size(); q++)
+            to_hex(h + q * 32, 8, out_hex17 + launched[k].files[q] * 17);  // cas.rs:61 to_hex()[..16]
+        launched[k].busy = false;
     };
-    std::vector<sd_extent> ext;
-    std::vector<size_t> idx, overflow;
+    std::vector<size_t> overflow;
     size_t i = 0;
-    for (int w = 0; i < n; w ^= 1) {
-        // the next window: consecutive files whose messages fit WINDOW bytes
-        ext.clear();
-        idx.clear();
+    // plans the next window (consecutive files whose messages fit WINDOW bytes) into slot w
+    // and starts the readers on it; false when no files are left
+    auto begin_window = [&](int w) -> bool {
+        if (i >= n) return false;
+        Win& W = wins[w];
+        W.ext.clear();
+        W.idx.clear();
         uint64_t off = 0;
         while (i < n) {
             const sd_extent e = plan_extent(sizes[i], off);
             const uint64_t next = align_up(off + e.msg_len, SD_STAGE_ALIGN);
-            if (!ext.empty() && next > WINDOW) break;
-            ext.push_back(e);
-            idx.push_back(i);
+            if (!W.ext.empty() && next > WINDOW) break;
+            W.ext.push_back(e);
+            W.idx.push_back(i);
             off = next;
             i++;
         }
-        harvest(w);  // slot w's previous window is done: its pinned buffer is free
+        W.bytes = off;
+        if (copy_pending[w]) {  // the slot's last H2D must have read its buffer
+            HIP_CHECK(hipEventSynchronize(copied[w]));
+            copy_pending[w] = false;
+        }
+        if (slots[w].window.bytes < off + 64) {
+            harvest(w);  // a reallocation frees the buffer: nothing may still use it
+            slots[w].window.ensure(off + 64);
+        }
+        uint8_t* win = slots[w].window.u8();
+        pool->start(W.ext.size(), [&W, win, paths, status](size_t q) {
+            status[W.idx[q]] = stage_one(paths[W.idx[q]], W.ext[q], win);
+        });
+        cleanup.staging = true;
+        return true;
+    };
+    int w = 0;
+    bool staging = begin_window(w);
+    while (staging) {
+        pool->wait();  // window w is staged
+        cleanup.staging = false;
+        Win& W = wins[w];
         Slot& sl = slots[w];
-        sl.window.ensure(off + 64);
-        uint8_t* win = sl.window.u8();
-        pool->run(ext.size(), [&](size_t q) { status[idx[q]] = stage_one(paths[idx[q]], ext[q], win); });
         // failed files (I/O error, short read) keep their status and leave the window;
         // files longer than their extent are hashed from disk after the windows
         size_t m = 0;
-        for (size_t q = 0; q < ext.size(); q++) {
-            if (status[idx[q]] == SD_FILE_OK) {
-                ext[m] = ext[q];
-                idx[m++] = idx[q];
-            } else if (status[idx[q]] == SD_FILE_CHANGED) {
-                overflow.push_back(idx[q]);
+        for (size_t q = 0; q < W.ext.size(); q++) {
+            if (status[W.idx[q]] == SD_FILE_OK) {
+                W.ext[m] = W.ext[q];
+                W.idx[m++] = W.idx[q];
+            } else if (status[W.idx[q]] == SD_FILE_CHANGED) {
+                overflow.push_back(W.idx[q]);
             }
         }
-        ext.resize(m);
-        idx.resize(m);
-        if (m == 0) continue;
-        plan_cas_batch(&batches[w], ext.data(), m, sl.stream);
-        sl.staged.ensure(off + 64);
-        sl.hashes.ensure(m * 32);
-        sl.host_hashes.ensure(m * 32);
-        HIP_CHECK(hipMemcpyAsync(sl.staged.p, win, off, hipMemcpyHostToDevice, sl.stream));
-        run_cas_batch(&batches[w], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
-        HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, m * 32, hipMemcpyDeviceToHost, sl.stream));
-        wins[w].files = idx;
-        wins[w].busy = true;
+        W.ext.resize(m);
+        W.idx.resize(m);
+        const int next = w ^ 1;
+        staging = begin_window(next);  // the readers go on with the next window...
+        if (m) {                        // ...while this one is planned and launched
+            harvest(w);                 // slot w's previous launch (two windows back)
+            plan_cas_batch(&batches[w], W.ext.data(), m, sl.stream);
+            sl.staged.ensure(W.bytes + 64);
+            sl.hashes.ensure(m * 32);
+            sl.host_hashes.ensure(m * 32);
+            HIP_CHECK(hipMemcpyAsync(sl.staged.p, sl.window.p, W.bytes, hipMemcpyHostToDevice, sl.stream));
+            HIP_CHECK(hipEventRecord(copied[w], sl.stream));
+            copy_pending[w] = true;
+            run_cas_batch(&batches[w], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
+            HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, m * 32, hipMemcpyDeviceToHost, sl.stream));
+            launched[w].files = W.idx;
+            launched[w].busy = true;
+        }
+        w = next;
     }
     harvest(0);
     harvest(1);

@@ -1,6 +1,8 @@
 // stage_pool.h -- persistent host thread pool for the file stager (pread of the byte
 // windows generate_cas_id reads, cas.rs:27-58).  run(n, f) calls f(0..n-1) on the pool
-// and the calling thread and returns when all are done; one run at a time per pool.
+// and the calling thread and returns when all are done; start(n, f) / wait() do the same
+// on the worker threads only while the caller goes on with other work.  One run at a time
+// per pool (a start() holds the pool until its wait()).
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -40,6 +42,30 @@ public:
         fn_ = nullptr;
     }
 
+    void start(size_t n, std::function<void(size_t)> f) {
+        async_lock_ = std::unique_lock<std::mutex>(run_mu_);
+        async_fn_ = std::move(f);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &async_fn_;
+            n_ = n;
+            next_.store(0);
+            busy_ = (int)th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        if (th_.empty()) drain();  // no worker threads: run inline
+    }
+    void wait() {
+        {
+            std::unique_lock<std::mutex> g(mu_);
+            done_.wait(g, [&] { return busy_ == 0; });
+            fn_ = nullptr;
+        }
+        async_fn_ = nullptr;
+        async_lock_.unlock();
+    }
+
 private:
     void drain() {
         for (;;) {
@@ -65,6 +91,8 @@ private:
     std::mutex mu_, run_mu_;
     std::condition_variable cv_, done_;
     const std::function<void(size_t)>* fn_ = nullptr;
+    std::function<void(size_t)> async_fn_;
+    std::unique_lock<std::mutex> async_lock_;
     size_t n_ = 0;
     std::atomic<size_t> next_{0};
     int busy_ = 0;
