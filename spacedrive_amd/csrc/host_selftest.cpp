@@ -294,7 +294,14 @@ void test_pool_growth() {
             for (int r = 0; r < 60; r++) {
                 auto p = get(1 + (t * 60 + r) % 12);
                 std::atomic<uint64_t> s{0};
-                p->run(97, [&](size_t i) { s += i; });
+                if (r % 2) {
+                    p->run(97, [&](size_t i) { s += i; });
+                } else {  // background run (sd_cas_ids_files' readers) while this thread works
+                    p->start(97, [&](size_t i) { s += i; });
+                    volatile uint64_t busy = 0;
+                    for (int k = 0; k < 1000; k++) busy = busy + k;
+                    p->wait();
+                }
                 total += s.load();
             }
         });

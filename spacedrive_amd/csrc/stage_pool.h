@@ -43,7 +43,7 @@ public:
     }
 
     void start(size_t n, std::function<void(size_t)> f) {
-        async_lock_ = std::unique_lock<std::mutex>(run_mu_);
+        run_mu_.lock();  // held until wait(), on this thread
         async_fn_ = std::move(f);
         {
             std::lock_guard<std::mutex> g(mu_);
@@ -63,7 +63,7 @@ public:
             fn_ = nullptr;
         }
         async_fn_ = nullptr;
-        async_lock_.unlock();
+        run_mu_.unlock();
     }
 
 private:
@@ -92,7 +92,6 @@ private:
     std::condition_variable cv_, done_;
     const std::function<void(size_t)>* fn_ = nullptr;
     std::function<void(size_t)> async_fn_;
-    std::unique_lock<std::mutex> async_lock_;
     size_t n_ = 0;
     std::atomic<size_t> next_{0};
     int busy_ = 0;
