@@ -229,6 +229,42 @@ void test_stager() {
     std::vector<uint8_t> buf(128);
     st = stage_one((g_dir + "/missing").c_str(), e, buf.data());
     CHECK((st & 0xFFFF) == SD_FILE_IO_ERROR && (st >> 16) == ENOENT);
+    // a FIFO (whole kind, metadata length 0): fs::read takes what the writer gives until it
+    // closes; with a capture vector stage_one keeps every byte (a pipe cannot be re-read)
+    for (size_t n : {size_t(0), size_t(1), size_t(4000), size_t(200000)}) {
+        const std::string fifo = g_dir + "/fifo" + std::to_string(n);
+        CHECK(mkfifo(fifo.c_str(), 0600) == 0);
+        const auto data = content(900 + (int)n, n);
+        std::thread writer([&] {
+            const int fd = open(fifo.c_str(), O_WRONLY);
+            for (size_t o = 0; o < n;) {  // 4000-byte writes, like test_oracle's FIFO
+                const ssize_t w = write(fd, data.data() + o, std::min<size_t>(4000, n - o));
+                if (w <= 0) break;
+                o += (size_t)w;
+            }
+            close(fd);
+        });
+        sd_extent fe = plan_extent(0, 0);
+        std::vector<uint8_t> fbuf(128, 0xAB), cap;
+        const int32_t fst = stage_one(fifo.c_str(), fe, fbuf.data(), &cap);
+        writer.join();
+        if (n == 0) {
+            CHECK(fst == SD_FILE_OK && fe.msg_len == 8 && cap.empty());
+        } else {
+            CHECK(fst == SD_FILE_CHANGED && cap == data);
+            MsgSource src(-1, MsgSource::READ_TO_EOF);  // the message the caller hashes
+            src.set_prefix_le64(0);
+            src.set_memory(cap.data(), cap.size());
+            std::vector<uint8_t> msg, win(3000);
+            for (;;) {
+                const uint64_t k = src.read(win.data(), win.size());
+                msg.insert(msg.end(), win.begin(), win.begin() + k);
+                if (src.done || src.err) break;
+            }
+            CHECK(msg.size() == n + 8 && std::equal(data.begin(), data.end(), msg.begin() + 8));
+        }
+        unlink(fifo.c_str());
+    }
 }
 
 // ------------------------------------------------------------------ readers

@@ -801,7 +801,8 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
     sd_cas_batch batches[2];
     struct Win {  // the window being staged into a slot's pinned buffer
         std::vector<sd_extent> ext;
-        std::vector<size_t> idx;  // input index of each extent
+        std::vector<size_t> idx;                // input index of each extent
+        std::vector<std::vector<uint8_t>> cap;  // a pipe's / device's whole content (stage_one)
         uint64_t bytes = 0;
     } wins[2];
     struct Launched {  // the window in flight on a slot's stream
@@ -829,7 +830,8 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
             to_hex(h + q * 32, 8, out_hex17 + launched[k].files[q] * 17);  // cas.rs:61 to_hex()[..16]
         launched[k].busy = false;
     };
-    std::vector<size_t> overflow;
+    std::vector<size_t> overflow;                                      // regular files that grew
+    std::vector<std::pair<size_t, std::vector<uint8_t>>> captured;    // pipes / devices, read whole
     size_t i = 0;
     // plans the next window (consecutive files whose messages fit WINDOW bytes) into slot w
     // and starts the readers on it; false when no files are left
@@ -849,6 +851,7 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
             i++;
         }
         W.bytes = off;
+        W.cap.assign(W.ext.size(), {});
         if (copy_pending[w]) {  // the slot's last H2D must have read its buffer
             HIP_CHECK(hipEventSynchronize(copied[w]));
             copy_pending[w] = false;
@@ -859,7 +862,7 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
         }
         uint8_t* win = slots[w].window.u8();
         pool->start(W.ext.size(), [&W, win, paths, status](size_t q) {
-            status[W.idx[q]] = stage_one(paths[W.idx[q]], W.ext[q], win);
+            status[W.idx[q]] = stage_one(paths[W.idx[q]], W.ext[q], win, &W.cap[q]);
         });
         cleanup.staging = true;
         return true;
@@ -879,7 +882,8 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
                 W.ext[m] = W.ext[q];
                 W.idx[m++] = W.idx[q];
             } else if (status[W.idx[q]] == SD_FILE_CHANGED) {
-                overflow.push_back(W.idx[q]);
+                if (W.cap[q].empty()) overflow.push_back(W.idx[q]);
+                else captured.emplace_back(W.idx[q], std::move(W.cap[q]));
             }
         }
         W.ext.resize(m);
@@ -904,10 +908,18 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
     }
     harvest(0);
     harvest(1);
-    if (!overflow.empty()) {
+    if (!overflow.empty() || !captured.empty()) {
         Streamer st([](size_t, const uint8_t*) {});
         int cur = 0;
         for (size_t f : overflow) status[f] = cas_overflow(slots, cur, st, paths[f], sizes[f], out_hex17 + f * 17);
+        for (auto& c : captured) {  // le64(size) || every byte the pipe gave (cas.rs:25,29)
+            MsgSource src(-1, MsgSource::READ_TO_EOF);
+            src.set_prefix_le64(sizes[c.first]);
+            src.set_memory(c.second.data(), c.second.size());
+            uint8_t h[32];
+            status[c.first] = st.hash(slots, cur, src, c.second.size() + 8, h);
+            if (status[c.first] == SD_FILE_OK) to_hex(h, 8, out_hex17 + c.first * 17);
+        }
     }
     return SD_OK;
     SD_GUARD_END

@@ -8,6 +8,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -354,7 +355,7 @@ int64_t pread_full(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
     return (int64_t)got;
 }
 
-int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged) {
+int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged, std::vector<uint8_t>* capture) {
     uint8_t* dst = staged + e.msg_offset;
     const uint64_t size = e.size;
     for (int i = 0; i < 8; i++) dst[i] = (uint8_t)(size >> (8 * i));  // cas.rs:25 le64
@@ -369,7 +370,25 @@ int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged) {
                 uint8_t probe;
                 const ssize_t r = read_once(f.fd, &probe, 1);
                 if (r < 0) return io_status(errno);
-                if (r > 0) return SD_FILE_CHANGED;
+                if (r > 0) {
+                    struct stat st;
+                    if (!capture || (fstat(f.fd, &st) == 0 && S_ISREG(st.st_mode))) return SD_FILE_CHANGED;
+                    // a pipe or device: what was read is gone from it -- keep every byte
+                    capture->assign(dst + 8, dst + 8 + room);
+                    capture->push_back(probe);
+                    uint8_t buf[1 << 16];
+                    for (;;) {
+                        const ssize_t k = read_once(f.fd, buf, sizeof buf);
+                        if (k < 0) {
+                            const int err = errno;
+                            capture->clear();
+                            return io_status(err);
+                        }
+                        if (k == 0) break;
+                        capture->insert(capture->end(), buf, buf + k);
+                    }
+                    return SD_FILE_CHANGED;
+                }
                 break;
             }
             const ssize_t r = read_once(f.fd, dst + 8 + got, room - got);
@@ -428,6 +447,10 @@ uint64_t MsgSource::read_impl(uint8_t* dst, uint64_t n) {
         pend_ += k;
         pend_len_ -= k;
         got += k;
+    }
+    if (mem_only_) {
+        if (pend_len_ == 0 && prefix_pos_ == prefix_len_) done = true;
+        return got;
     }
     if (done || err) return got;
     if (pool_ && mode_ == CHECKSUM_READS && got < n) return got + read_parallel(dst + got, n - got);

@@ -160,10 +160,15 @@ ExchangePlan exchange_plan(const uint64_t* rows, int R, int me);
 //   whole kind: every byte read() returns until EOF (fs::read, cas.rs:29); e.msg_len is
 //     set to 8 + that count.  SD_FILE_CHANGED if the file holds more bytes than the
 //     extent's planned room (e.msg_len - 8 on entry): the reference would hash them all.
+//     With `capture`, a file that is not a regular file (a pipe, a character device: its
+//     bytes cannot be read a second time) is read to its end instead, all its bytes
+//     (the room's, then the rest) going to *capture; the status is still SD_FILE_CHANGED
+//     and the caller hashes le64(size) || *capture.  A regular file that grew is left
+//     for the caller to re-read (it may be large).
 //   sampled kind: read_exact of the head and the samples at their traced offsets
 //     (SHORT_READ past EOF), then the footer at seek(End(-8192)) -- the file's real end,
 //     EINVAL when it is shorter than 8192 bytes.
-int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged);
+int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged, std::vector<uint8_t>* capture = nullptr);
 // pread until n bytes or EOF; returns the count, or -errno
 int64_t pread_full(int fd, uint8_t* dst, uint64_t n, uint64_t off);
 
@@ -178,6 +183,12 @@ public:
     static constexpr uint64_t CHECKSUM_READ = SD_CK_BLOCK;
     MsgSource(int fd, Mode m) : fd_(fd), mode_(m) {}
     void set_prefix_le64(uint64_t v);
+    // a message held in memory: after the prefix, exactly these bytes, then the end
+    void set_memory(const uint8_t* p, uint64_t n) {
+        pend_ = p;
+        pend_len_ = n;
+        mem_only_ = true;
+    }
     // the file's first n bytes, already taken from it (whole 1 MiB reads in CHECKSUM_READS mode)
     void set_pending(const uint8_t* p, uint64_t n) {
         pend_ = p;
@@ -217,6 +228,7 @@ private:
     uint64_t pend_len_ = 0;
     uint64_t eof_hint_ = 0;
     bool has_eof_hint_ = false;
+    bool mem_only_ = false;
 };
 
 // ------------------------------------------------------------------ CPU BLAKE3 (cpu_blake3.cpp)

@@ -182,3 +182,26 @@ def test_cpu_cas_ids_on_restaged_shorter_files(tmp_path):
     got = cpu.cas_ids_staged(staged, ext)
     for i in range(3):
         assert got[i] == cs.generate_cas_id_file(cs.synth_bytes(60 + i, 0, 0, flens[i]), sizes[i])
+
+
+def test_cpu_cas_id_of_a_pipe(tmp_path, oracle_native):
+    """The CPU path reads a pipe as fs::read does (cas.rs:29): every byte until the writer
+    closes, hashed after le64(size) -- here the metadata length 0 of a FIFO."""
+    import threading
+    from spacedrive_amd import cpu
+    data = bytes(range(256)) * 700
+    fifo = str(tmp_path / "pipe")
+    os.mkfifo(fifo)
+
+    def writer():
+        with open(fifo, "wb") as f:
+            for o in range(0, len(data), 4000):
+                f.write(data[o:o + 4000])
+
+    t = threading.Thread(target=writer)
+    t.start()
+    try:
+        got = cpu.generate_cas_id(fifo, 0)
+    finally:
+        t.join()
+    assert got == oracle_native.blake3(bytes(8) + data)[:8].hex()

@@ -879,3 +879,40 @@ def test_split_checksum_mgpu_through_rccl_single_rank(ctx, oracle_native, rccl_c
     with pytest.raises(SdCasError):
         bad.mgpu(comm, d, torch.zeros(bad.cv_bytes, dtype=torch.uint8, device="cuda"), out)
     assert checksum_split(d[:total + 64], total, ctx=ctx) == want
+
+
+@pytest.mark.parametrize("route", ["batch", "single-gpu"])
+def test_pipe_whole_kind_reads_every_byte(ctx, tmp_path, oracle_native, route):
+    """generate_cas_id on a pipe (a metadata length of 0, as non_indexed passes for one):
+    fs::read takes every byte the writer gives until it closes (cas.rs:29).  A pipe cannot
+    be read twice, so the stager keeps its bytes and hashes le64(0) || them from memory."""
+    import threading
+    import spacedrive_amd as sd
+    from spacedrive_amd._native import lib
+    data = cs.synth_bytes(77, 0, 0, 150000)
+    fifo = str(tmp_path / "pipe")
+    os.mkfifo(fifo)
+    plain = tmp_path / "plain"
+    plain.write_bytes(b"x" * 5000)
+
+    def writer():
+        with open(fifo, "wb") as f:
+            for o in range(0, len(data), 4000):
+                f.write(data[o:o + 4000])
+
+    t = threading.Thread(target=writer)
+    t.start()
+    try:
+        if route == "batch":
+            got = sd.generate_cas_ids([str(plain), fifo], [5000, 0])
+        else:
+            assert lib().sd_cas_set_tuning(b"latency_cpu_max", 0) == 0  # the GPU-coalesced route
+            try:
+                got = [sd.generate_cas_id(str(plain), 5000), sd.generate_cas_id(fifo, 0)]
+            finally:
+                lib().sd_cas_set_tuning(b"latency_cpu_max", 16)
+    finally:
+        t.join()
+    le64 = lambda v: int(v).to_bytes(8, "little")  # noqa: E731  (cas.rs:25)
+    assert got[0] == oracle_native.blake3(le64(5000) + b"x" * 5000)[:8].hex()
+    assert got[1] == oracle_native.blake3(le64(0) + data)[:8].hex()
