@@ -218,7 +218,8 @@ def host_staged(ctx, ext, d_staged, k, dev, stream):
         t0 = time.perf_counter()
         check(lib().sd_cas_ids(ctx.handle, host.data_ptr(), nbytes, sub.ctypes.data, k, out, None))
         e2e.append(time.perf_counter() - t0)
-    got = np.frombuffer(bytes.fromhex("".join(out.raw[17 * i:17 * i + 16].decode() for i in range(k))),
+    raw = out.raw  # one copy: each .raw access copies the whole buffer
+    got = np.frombuffer(bytes.fromhex("".join(raw[17 * i:17 * i + 16].decode() for i in range(k))),
                         np.uint8).reshape(k, 8)
     assert np.array_equal(got, want), "sd_cas_ids differs from the device-resident batch"
     e2e_s = min(e2e[1:])
@@ -261,7 +262,8 @@ def checksum_host(ctx, gib: int, dev, stream):
         t0 = time.perf_counter()
         check(lib().sd_checksums(ctx.handle, host.data_ptr(), offs.ctypes.data, lens.ctypes.data, nf, out))
         e2e.append(time.perf_counter() - t0)
-    got = [out.raw[65 * i:65 * i + 64].decode() for i in range(nf)]
+    raw = out.raw
+    got = [raw[65 * i:65 * i + 64].decode() for i in range(nf)]
     assert got == want, "sd_checksums differs from the device-resident batch"
     e2e_s = min(e2e)
     return {"files": nf, "bytes": total, "h2d_ms": h2d_ms, "h2d_GBps": total / (h2d_ms * 1e-3) / 1e9,
@@ -439,7 +441,8 @@ def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool, latency_calls
             check(L.sd_cas_ids_files(ctx.handle, arr, sz.ctypes.data, k, out, st.ctypes.data, threads))
             pipe.append(time.perf_counter() - t0)
         assert (st == 0).all(), np.unique(st)
-        gpu_ids = [out.raw[17 * i:17 * i + 16].decode() for i in range(k)]
+        raw = out.raw
+        gpu_ids = [raw[17 * i:17 * i + 16].decode() for i in range(k)]
         pipe_s = min(pipe[1:])
         res = {"files": k, "dir_fs": _fs_type(d), "write_s": write_s,
                "message_bytes": int(ext["msg_len"][:k].astype(np.int64).sum()),

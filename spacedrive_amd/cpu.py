@@ -83,7 +83,8 @@ def cas_ids_staged(staged: np.ndarray, extents: np.ndarray, status: Optional[np.
     out = ctypes.create_string_buffer(17 * max(n, 1))
     check(lib().sd_cpu_cas_ids(staged.ctypes.data, staged.nbytes, extents.ctypes.data, n, out,
                                None if status is None else status.ctypes.data, nthreads))
-    return [out.raw[17 * i:17 * i + 16].decode() for i in range(n)]
+    raw = out.raw  # one copy: each .raw access copies the whole buffer
+    return [raw[17 * i:17 * i + 16].decode() for i in range(n)]
 
 
 def blake3(data: bytes) -> bytes:

@@ -1,4 +1,5 @@
 // 4-lane instantiation of cpu_b3_lanes.inc (see the Makefile for its ISA flags)
 #define SD_LANES 4
 #define SD_CHUNKS_FN cpu_hash_chunks_x4
+#define SD_PARENTS_FN cpu_hash_parents_x4
 #include "cpu_b3_lanes.inc"

@@ -29,6 +29,9 @@
 void cpu_hash_chunks_x16(const uint8_t* const* in, int n, uint64_t ctr0, uint32_t (*cv)[8]);
 void cpu_hash_chunks_x8(const uint8_t* const* in, int n, uint64_t ctr0, uint32_t (*cv)[8]);
 void cpu_hash_chunks_x4(const uint8_t* const* in, int n, uint64_t ctr0, uint32_t (*cv)[8]);
+void cpu_hash_parents_x16(const uint32_t (*cvs)[8], int n, uint32_t (*out)[8]);
+void cpu_hash_parents_x8(const uint32_t (*cvs)[8], int n, uint32_t (*out)[8]);
+void cpu_hash_parents_x4(const uint32_t (*cvs)[8], int n, uint32_t (*out)[8]);
 
 namespace {
 
@@ -95,22 +98,43 @@ void chunk_cv(const uint8_t* p, uint32_t len, uint64_t counter, bool root, uint3
 }
 
 using chunks_fn = void (*)(const uint8_t* const*, int, uint64_t, uint32_t (*)[8]);
+using parents_fn = void (*)(const uint32_t (*)[8], int, uint32_t (*)[8]);
 struct Simd {
     chunks_fn fn;
     int lanes;
+    parents_fn parents;
 };
 Simd pick_simd() {
     __builtin_cpu_init();
     // SD_CPU_LANES=4/8 caps the width (tests run every width the CPU has)
     const char* cap = getenv("SD_CPU_LANES");
     const int lim = cap ? atoi(cap) : 16;
-    if (lim >= 16 && __builtin_cpu_supports("avx512f")) return {cpu_hash_chunks_x16, 16};
-    if (lim >= 8 && __builtin_cpu_supports("avx2")) return {cpu_hash_chunks_x8, 8};
-    return {cpu_hash_chunks_x4, 4};
+    if (lim >= 16 && __builtin_cpu_supports("avx512f")) return {cpu_hash_chunks_x16, 16, cpu_hash_parents_x16};
+    if (lim >= 8 && __builtin_cpu_supports("avx2")) return {cpu_hash_chunks_x8, 8, cpu_hash_parents_x8};
+    return {cpu_hash_chunks_x4, 4, cpu_hash_parents_x4};
 }
 const Simd& simd() {
     static const Simd s = pick_simd();
     return s;
+}
+
+// n >= 2 CVs merged level-wise (pairs left to right, the odd node carried up: BLAKE3's tree
+// over power-of-two aligned groups), the pairs of a level SIMD_LANES at a time; ROOT on the
+// final parent when `root`.  cv[] is overwritten.
+void merge_levels(uint32_t (*cv)[8], uint64_t n, bool root, uint32_t out[8]) {
+    const Simd& s = simd();
+    uint32_t tmp[16][8];
+    while (n > 2) {
+        const uint64_t P = n / 2;
+        for (uint64_t i = 0; i < P; i += (uint64_t)s.lanes) {
+            const int g = (int)std::min<uint64_t>((uint64_t)s.lanes, P - i);
+            s.parents(cv + 2 * i, g, tmp);  // reads pairs [2i, 2i + 2g) before any write
+            memcpy(cv + i, tmp, 32 * (size_t)g);
+        }
+        if (n & 1) memmove(cv + P, cv + n - 1, 32);
+        n = P + (n & 1);
+    }
+    parent_cv(cv[0], cv[1], root ? ROOT : 0, out);
 }
 
 }  // namespace
@@ -121,10 +145,15 @@ CpuHasher::CpuHasher() {}
 CpuHasher::CpuHasher(uint64_t chunk0) : ctr0_(chunk0) {}
 
 void CpuHasher::push_chunk_cv(const uint32_t cv[8]) {
+    memcpy(blk_[nblk_++], cv, 32);
+    chunks_++;
+    if (nblk_ < BLOCK_CHUNKS) return;
+    // a complete 1 MiB block (never the message's last: its last chunk stays buffered)
     uint32_t cur[8];
-    memcpy(cur, cv, 32);
-    uint64_t total = ++chunks_;
-    while ((total & 1) == 0) {  // this chunk completes a subtree: merge it with its left half
+    merge_levels(blk_.get(), nblk_, false, cur);
+    nblk_ = 0;
+    uint64_t total = ++blocks_;
+    while ((total & 1) == 0) {  // this block completes a subtree: merge it with its left half
         parent_cv(stack_[--sp_], cur, 0, cur);
         total >>= 1;
     }
@@ -163,39 +192,50 @@ void CpuHasher::update(const uint8_t* p, size_t n) {
     }
 }
 
-void CpuHasher::finalize(uint8_t out[32]) const {
+void CpuHasher::finish(uint8_t out[32], bool root) const {
     uint32_t cur[8];
-    if (sp_ == 0) {
-        chunk_cv(buf_, buf_len_, ctr0_ + chunks_, true, cur);
-    } else {
-        chunk_cv(buf_, buf_len_, ctr0_ + chunks_, false, cur);
-        for (int i = sp_ - 1; i >= 1; i--) parent_cv(stack_[i], cur, 0, cur);
-        parent_cv(stack_[0], cur, ROOT, cur);
+    if (chunks_ == 0) {  // one chunk: it is the message (ROOT on its last block)
+        chunk_cv(buf_, buf_len_, ctr0_, root, cur);
+        memcpy(out, cur, 32);  // little-endian words = the hash bytes
+        return;
     }
-    memcpy(out, cur, 32);  // little-endian words = the hash bytes
-}
-
-void CpuHasher::finalize_cv(uint8_t out[32]) const {
-    uint32_t cur[8];
-    chunk_cv(buf_, buf_len_, ctr0_ + chunks_, false, cur);
-    for (int i = sp_ - 1; i >= 0; i--) parent_cv(stack_[i], cur, 0, cur);
+    // the last block: its chunk CVs and the buffered last chunk, merged level-wise
+    uint32_t (*cv)[8] = blk_.get();
+    uint32_t last[8];
+    chunk_cv(buf_, buf_len_, ctr0_ + chunks_, false, last);
+    const bool whole = sp_ == 0;  // the message is this one block
+    if (nblk_ == 0) {
+        memcpy(cur, last, 32);
+    } else {
+        // finish() is const: merge a copy (on the stack for the short messages of cas_ids)
+        uint32_t small[128][8];
+        std::vector<uint32_t> big;
+        uint32_t(*t)[8] = small;
+        if (nblk_ + 1 > 128) {
+            big.resize((size_t)(nblk_ + 1) * 8);
+            t = reinterpret_cast<uint32_t(*)[8]>(big.data());
+        }
+        memcpy(t, cv, 32 * (size_t)nblk_);
+        memcpy(t[nblk_], last, 32);
+        merge_levels(t, nblk_ + 1, root && whole, cur);
+    }
+    if (!whole) {  // then the complete blocks' subtrees, right to left
+        for (int i = sp_ - 1; i >= 1; i--) parent_cv(stack_[i], cur, 0, cur);
+        parent_cv(stack_[0], cur, root ? ROOT : 0, cur);
+    }
     memcpy(out, cur, 32);
 }
 
-// Level-wise pairwise merge with the odd node carried up (= BLAKE3's left-heavy tree over
-// power-of-two aligned blocks), ROOT on the final parent.
+void CpuHasher::finalize(uint8_t out[32]) const { finish(out, true); }
+void CpuHasher::finalize_cv(uint8_t out[32]) const { finish(out, false); }
+
+// BLAKE3 root from nb >= 2 consecutive 1 MiB block CVs (the split checksum)
 void cpu_root_from_cvs(const uint8_t* cvs, uint64_t nb, uint8_t out[32]) {
     std::vector<uint32_t> lvl(nb * 8);
     memcpy(lvl.data(), cvs, nb * 32);
-    uint64_t n = nb;
-    while (n > 1) {
-        const uint64_t pairs = n / 2;
-        for (uint64_t i = 0; i < pairs; i++)
-            parent_cv(&lvl[16 * i], &lvl[16 * i + 8], n == 2 ? ROOT : 0, &lvl[8 * i]);
-        if (n & 1) memmove(&lvl[8 * pairs], &lvl[8 * (n - 1)], 32);
-        n = pairs + (n & 1);
-    }
-    memcpy(out, lvl.data(), 32);
+    uint32_t o[8];
+    merge_levels(reinterpret_cast<uint32_t(*)[8]>(lvl.data()), nb, true, o);
+    memcpy(out, o, 32);
 }
 
 void cpu_blake3(const uint8_t* p, size_t n, uint8_t out[32]) {
@@ -235,21 +275,32 @@ int32_t hash_source(MsgSource& src, uint8_t* buf, uint64_t bufsz, uint8_t out[32
 }
 }  // namespace
 
+// per-thread read buffers, allocated once (a fresh, zeroed 128 KiB or 1 MiB buffer per file
+// costs more than reading a small file)
+static uint8_t* scratch(size_t bytes) {
+    thread_local std::unique_ptr<uint8_t[]> buf;
+    thread_local size_t have = 0;
+    if (have < bytes) {
+        buf.reset(new uint8_t[bytes]);
+        have = bytes;
+    }
+    return buf.get();
+}
+
 int32_t cpu_cas_id_file(const char* path, uint64_t size, char out_hex17[17]) {
     uint8_t h[32];
     if (size > SD_MINIMUM_FILE_SIZE) {  // cas.rs:30-58: the 57 352 B sampled message
-        std::vector<uint8_t> msg(sd_align_up(SD_SAMPLED_MSG_LEN, SD_STAGE_PAD));
+        uint8_t* msg = scratch(sd_align_up(SD_SAMPLED_MSG_LEN, SD_STAGE_PAD));
         sd_extent e = plan_extent(size, 0);
-        const int32_t st = stage_one(path, e, msg.data());
+        const int32_t st = stage_one(path, e, msg);
         if (st != SD_FILE_OK) return st;
-        cpu_blake3(msg.data(), e.msg_len, h);
+        cpu_blake3(msg, e.msg_len, h);
     } else {  // cas.rs:25-29: le64(size) || fs::read
         Fd f{open(path, O_RDONLY | O_CLOEXEC)};
         if (f.fd < 0) return io_status(errno);
         MsgSource src(f.fd, MsgSource::READ_TO_EOF);
         src.set_prefix_le64(size);
-        std::vector<uint8_t> buf(128 << 10);
-        const int32_t st = hash_source(src, buf.data(), buf.size(), h);
+        const int32_t st = hash_source(src, scratch(128 << 10), 128 << 10, h);
         if (st != SD_FILE_OK) return st;
     }
     hex_lower(h, 8, out_hex17);  // cas.rs:61 to_hex()[..16]
@@ -260,9 +311,8 @@ int32_t cpu_checksum_file(const char* path, char out_hex65[65]) {
     Fd f{open(path, O_RDONLY | O_CLOEXEC)};  // hash.rs:11
     if (f.fd < 0) return io_status(errno);
     MsgSource src(f.fd, MsgSource::CHECKSUM_READS);
-    std::unique_ptr<uint8_t[]> buf(new uint8_t[SD_CK_BLOCK]);
     uint8_t h[32];
-    const int32_t st = hash_source(src, buf.get(), SD_CK_BLOCK, h);
+    const int32_t st = hash_source(src, scratch(SD_CK_BLOCK), SD_CK_BLOCK, h);
     if (st != SD_FILE_OK) return st;
     hex_lower(h, 32, out_hex65);  // hash.rs:21-23
     return SD_FILE_OK;

@@ -7,6 +7,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -247,9 +248,16 @@ public:
     void finalize_cv(uint8_t out[32]) const;
 
 private:
+    static constexpr uint32_t BLOCK_CHUNKS = 1024;  // 1 MiB: the unit merged level-wise
     void push_chunk_cv(const uint32_t cv[8]);
-    uint32_t stack_[56][8];
+    void finish(uint8_t out[32], bool root) const;
+    // chunk CVs of the current 1 MiB block, merged level-wise (SIMD parents) when it is
+    // complete; complete blocks' CVs on a stack that merges every completed subtree
+    std::unique_ptr<uint32_t[][8]> blk_{new uint32_t[BLOCK_CHUNKS][8]};
+    uint32_t nblk_ = 0;
+    uint32_t stack_[48][8];
     int sp_ = 0;
+    uint64_t blocks_ = 0;  // complete blocks pushed so far
     uint64_t ctr0_ = 0;    // chunk index of the first chunk
     uint64_t chunks_ = 0;  // complete chunks pushed so far
     uint8_t buf_[1024];

@@ -125,8 +125,9 @@ def test_cas_pattern_goldens_host_staged(ctx, golden):
         staged[o:o + len(msg)] = np.frombuffer(msg, np.uint8)
     out = ctypes.create_string_buffer(17 * len(sizes))
     check(lib().sd_cas_ids(ctx.handle, staged.ctypes.data, total, ext.ctypes.data, len(sizes), out, None))
+    raw = out.raw  # one copy of the buffer
     for i, s in enumerate(cp):
-        assert out.raw[17 * i:17 * i + 16].decode() == cp[s], s
+        assert raw[17 * i:17 * i + 16].decode() == cp[s], s
 
 
 def test_sd_cas_ids_pipelined_windows(ctx):
@@ -715,8 +716,9 @@ def test_long_whole_messages_staged(ctx, oracle_native):
     want = oracle_native.checksums(staged, ext["msg_offset"], ext["msg_len"].astype(np.uint64), nthreads=NT)
     out = ctypes.create_string_buffer(17 * len(lens))
     check(lib().sd_cas_ids(ctx.handle, staged.ctypes.data, len(staged), ext.ctypes.data, len(lens), out, None))
+    raw = out.raw  # one copy of the buffer
     for i in range(len(lens)):
-        assert out.raw[17 * i:17 * i + 16].decode() == want[i, :8].tobytes().hex(), (i, lens[i])
+        assert raw[17 * i:17 * i + 16].decode() == want[i, :8].tobytes().hex(), (i, lens[i])
     b = ctx.cas_batch(ext)
     d_st = torch.from_numpy(staged).cuda()
     h = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
@@ -824,8 +826,9 @@ def test_checksums_from_host_memory(ctx, oracle_native):
     out = ctypes.create_string_buffer(65 * len(lens))
     check(lib().sd_checksums(ctx.handle, host.data_ptr(), arr_o.ctypes.data, arr_l.ctypes.data, len(lens), out))
     want = oracle_native.checksums_simd(host.numpy(), arr_o, arr_l, nthreads=NT)
+    raw = out.raw  # one copy of the buffer
     for i in range(len(lens)):
-        assert out.raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), lens[i]
+        assert raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), lens[i]
 
 
 def test_split_checksum_ranks_on_one_gpu(ctx, oracle_native):
