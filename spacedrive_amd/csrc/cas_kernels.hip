@@ -80,7 +80,7 @@ constexpr int S_F = S_THREADS / S_LANES;  // files per workgroup (16)
 constexpr int S_N0 = S_LANES + 1;         // nodes per file entering the tree (29)
 
 __global__ __launch_bounds__(S_THREADS) void k_cas_sampled(const uint8_t* __restrict__ staged,
-                                                           const sd_extent* __restrict__ ext,
+                                                           const uint64_t* __restrict__ soff,
                                                            const uint32_t* __restrict__ idx, uint32_t n,
                                                            uint32_t* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t cvs[S_F][S_N0][8];
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(S_THREADS) void k_cas_sampled(const uint8_t* __rest
         const uint32_t f = t / S_LANES, j = t % S_LANES;
         const uint32_t g = wg * S_F + f;
         if (g < n) {
-            const uint8_t* msg = staged + ext[idx[g]].msg_offset;
+            const uint8_t* msg = staged + soff[g];  // one load, not idx -> extent -> offset
             uint32_t cv[8];
             full_chunks_cv<S_U>(cv, msg + (size_t)j * S_U * CHUNK_LEN, (uint64_t)j * S_U);
             store_cv(cvs[f][j], cv);
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(S_THREADS) void k_cas_sampled(const uint8_t* __rest
                 const uint32_t gt = wg * S_F + (t - S_F * P);
                 if (t < S_F * P + S_F && gt < n) {
                     ff = t - S_F * P; p = P;
-                    const uint8_t* msg = staged + ext[idx[gt]].msg_offset;
+                    const uint8_t* msg = staged + soff[gt];
                     chunk_cv(res, msg + (size_t)S_FULL * CHUNK_LEN, SD_SAMPLED_MSG_LEN - S_FULL * CHUNK_LEN, S_FULL,
                              false);
                     have = true;
@@ -322,10 +322,10 @@ __global__ __launch_bounds__(256) void k_ck_reduce(const uint32_t* __restrict__ 
 // --------------------------------------------------------------------- launchers
 namespace sdk {
 
-hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const uint32_t* idx, uint32_t n,
+hipError_t launch_cas_sampled(const uint8_t* staged, const uint64_t* soff, const uint32_t* idx, uint32_t n,
                               uint32_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_cas_sampled, dim3((n + S_F - 1) / S_F), dim3(S_THREADS), 0, s, staged, ext, idx, n, out);
+    hipLaunchKernelGGL(k_cas_sampled, dim3((n + S_F - 1) / S_F), dim3(S_THREADS), 0, s, staged, soff, idx, n, out);
     return hipGetLastError();
 }
 

@@ -210,7 +210,7 @@ struct sd_cas_batch {
     uint32_t n_sampled = 0, n_whole = 0, n_long = 0;
     uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0, whole_chunks = 0;
     WholePlan whole;  // work lists (kernel formats in cas_kernels.hip, k_whole_items / _merge8)
-    DevBuf ext, sidx, full_items, tail_items, merge_a, merge_b, cvbuf, cv2;
+    DevBuf ext, sidx, soff, full_items, tail_items, merge_a, merge_b, cvbuf, cv2;
     // whole-file messages longer than SD_WHOLE_ITEMS_MAX: a checksum sub-batch over their
     // byte ranges, its hashes scattered to out[long_idx[i]]
     sd_checksum_batch lng;
@@ -218,6 +218,7 @@ struct sd_cas_batch {
     // host copies backing async uploads
     std::vector<sd_extent> h_ext;
     std::vector<uint32_t> h_sidx, h_long_idx;
+    std::vector<uint64_t> h_soff;
 };
 
 namespace {
@@ -263,6 +264,7 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
     b->n_whole = 0;
     b->compressions = b->msg_bytes = b->whole_chunks = 0;
     b->h_sidx.clear();
+    b->h_soff.clear();
     b->h_long_idx.clear();
     std::vector<uint64_t> loff, llen;
     uint64_t end = 0;
@@ -273,6 +275,7 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
         b->msg_bytes += e.msg_len;
         if (e.kind == SD_KIND_SAMPLED) {
             b->h_sidx.push_back((uint32_t)i);
+            b->h_soff.push_back(e.msg_offset);
             b->compressions += 953;  // 56 x 16 + 1 blocks, 56 parents
         } else if (e.msg_len <= SD_WHOLE_ITEMS_MAX) {
             b->n_whole++;
@@ -291,6 +294,7 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
     b->h_ext.assign(ext, ext + n);
     b->ext.upload(b->h_ext, stream);
     b->sidx.upload(b->h_sidx, stream);
+    b->soff.upload(b->h_soff, stream);
     b->full_items.upload(b->whole.full, stream);
     b->tail_items.upload(b->whole.tail, stream);
     b->merge_a.upload(b->whole.merge_a, stream);
@@ -309,7 +313,7 @@ void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_ha
                    int parts = SD_PART_SAMPLED | SD_PART_WHOLE) {
     uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
     if (parts & SD_PART_SAMPLED)
-        HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->ext.as<sd_extent>(), b->sidx.as<uint32_t>(), b->n_sampled, out,
+        HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->soff.as<uint64_t>(), b->sidx.as<uint32_t>(), b->n_sampled, out,
                                           s));
     if (parts & SD_PART_WHOLE) {
         const WholePlan& w = b->whole;

@@ -14,7 +14,8 @@ void dedup_group_owners(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, int fl
 // the block partition of a split-file checksum object
 const SplitPlan& sd_split_plan_of(const sd_split_checksum* x);
 namespace sdk {
-hipError_t launch_cas_sampled(const uint8_t* staged, const sd_extent* ext, const uint32_t* idx, uint32_t n,
+// soff[i] = msg_offset of sampled file i, idx[i] = its index in the batch (the output slot)
+hipError_t launch_cas_sampled(const uint8_t* staged, const uint64_t* soff, const uint32_t* idx, uint32_t n,
                               uint32_t* out, hipStream_t s);
 // whole-file work lists: full-pair items, cost-sorted tail items, two merge8 passes (cv2 =
 // pass-A output)
