@@ -89,3 +89,41 @@ def checksum_split(slice_data, total_len: int, ctx=None, group=None) -> str:
     if R > 1:
         _gather_slots(cvs, r, R, q, group)
     return cpu_root(cvs.numpy(), total_len).hex()
+
+
+def file_checksum_split(path, ctx=None, group=None) -> str:
+    """file_checksum (hash.rs:10-24) of one file on disk, computed by all ranks of the group:
+    every rank stats the file, preads only its own byte range ``split_range(len, R, r)`` and
+    hashes it (on the device with `ctx`, else on host cores); the block CVs are gathered and
+    every rank returns the 64-hex hash.  For a file that is not being written: the ranks
+    must see the same length (it is checked across the group)."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+    R = dist.get_world_size(group) if dist.is_initialized() else 1
+    r = dist.get_rank(group) if dist.is_initialized() else 0
+    total = os.stat(path).st_size
+    if R > 1:
+        lens = [None] * R
+        dist.all_gather_object(lens, total, group=group)
+        if len(set(lens)) != 1:
+            raise OSError(f"{path}: length differs across ranks {lens} (the file is changing)")
+    off, length, _ = split_range(total, R, r)
+    buf = np.zeros(length + 64, np.uint8)  # zero padding past the slice (the kernels' rule)
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        got = 0
+        mv = memoryview(buf)
+        while got < length:
+            k = os.preadv(fd, [mv[got:length]], off + got)
+            if k == 0:
+                raise OSError(f"{path}: shorter than its length {total} (the file is changing)")
+            got += k
+    finally:
+        os.close(fd)
+    t = torch.from_numpy(buf)
+    if ctx is not None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        t = t.to(dev)
+    return checksum_split(t, total, ctx=ctx, group=group)

@@ -919,3 +919,14 @@ def test_pipe_whole_kind_reads_every_byte(ctx, tmp_path, oracle_native, route):
     le64 = lambda v: int(v).to_bytes(8, "little")  # noqa: E731  (cas.rs:25)
     assert got[0] == oracle_native.blake3(le64(5000) + b"x" * 5000)[:8].hex()
     assert got[1] == oracle_native.blake3(le64(0) + data)[:8].hex()
+
+
+def test_file_checksum_split_on_device(ctx, tmp_path, oracle_native):
+    """split.file_checksum_split: the rank's byte range of a file read from disk and hashed
+    by the device's split leaves + root (one rank here) == the oracle's BLAKE3 of the file."""
+    from spacedrive_amd.split import file_checksum_split
+    n = (9 << 20) + 4321
+    data = cs.synth_bytes(902, 0, 0, n)
+    p = tmp_path / "big.bin"
+    p.write_bytes(data)
+    assert file_checksum_split(str(p), ctx=ctx) == oracle_native.blake3(data).hex()

@@ -14,7 +14,7 @@ import torch.multiprocessing as mp
 
 from oracle import native
 from spacedrive_amd._native import SdCasError
-from spacedrive_amd.split import BLOCK, checksum_split, cpu_leaves, cpu_root, split_range
+from spacedrive_amd.split import BLOCK, checksum_split, cpu_leaves, cpu_root, file_checksum_split, split_range
 
 SIZES = [0, 1, 1023, 1024, 1025, BLOCK - 1, BLOCK, BLOCK + 1, 2 * BLOCK, 5 * BLOCK + 3, 17 * BLOCK,
          33 * BLOCK + 12345]
@@ -81,6 +81,7 @@ def _worker(rank, world, port, outdir):
             d = _data(total, seed=7)
             off, ln, _ = split_range(total, world, rank)
             res.append(checksum_split(torch.from_numpy(d[off:off + ln].copy()), total))
+        res.append(file_checksum_split(os.path.join(outdir, "file.bin")))  # each rank reads its range
         with open(os.path.join(outdir, f"r{rank}.txt"), "w") as f:
             f.write("\n".join(res))
     finally:
@@ -89,8 +90,11 @@ def _worker(rank, world, port, outdir):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_checksum_split_over_gloo(tmp_path, world):
+    fdata = _data(5 * BLOCK + 999, seed=9)[:5 * BLOCK + 999]
+    (tmp_path / "file.bin").write_bytes(fdata.tobytes())
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     want = [_oracle(_data(t, seed=7), t).hex() for t in (3 * BLOCK + 5, 10 * BLOCK, 100)]
+    want.append(_oracle(_data(5 * BLOCK + 999, seed=9), 5 * BLOCK + 999).hex())
     for r in range(world):
         assert open(tmp_path / f"r{r}.txt").read().split("\n") == want, r
