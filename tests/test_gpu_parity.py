@@ -40,13 +40,6 @@ def _rccl_background(ctx):
 
     def make():
         try:
-            # RCCL's first initialisation on a fresh box is mostly reading librccl from disk
-            # (3.7 s cold, 1.0 s warm): warm the page cache first, off the HIP lock
-            import glob
-            for f in glob.glob(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl*.so*")):
-                with open(f, "rb") as fh:
-                    while fh.read(8 << 20):
-                        pass
             box["comm"] = dedup.make_comm(ctx)
         except BaseException as e:  # noqa: BLE001 -- re-raised in the tests that need it
             box["err"] = e
