@@ -151,6 +151,13 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes,
  * status[n] (required) receives each file's sd_file_status. */
 int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n,
                      char* out_hex17, int32_t* status, int nthreads);
+/* The same, with the full 32-byte hashes left in device memory for a multi-GPU library
+ * scan (sd_cas_dedup_mgpu takes them as they are): d_hash32 (device, n x 32 bytes) row i =
+ * file i's hash when status[i] == SD_FILE_OK (other rows untouched); d_valid (device, n
+ * bytes, may be NULL) = 1 for the files the identifier dedups -- hashed and not empty
+ * (file_identifier/mod.rs:80-88).  Returns when the rows are written. */
+int sd_cas_hashes_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n,
+                        uint8_t* d_hash32, uint8_t* d_valid, int32_t* status, int nthreads);
 
 /* Prepared batch for device-resident data: builds the work lists for these extents once
  * (host arithmetic + one upload).  extents are host pointers. */

@@ -62,6 +62,8 @@ extern "C" {
     pub fn sd_cas_stage_plan(sizes: *const u64, n: usize, ext: *mut sd_extent, total: *mut u64) -> c_int;
     pub fn sd_cas_ids_files(ctx: *mut sd_cas_ctx, paths: *const *const c_char, sizes: *const u64, n: usize,
                             out_hex17: *mut c_char, status: *mut i32, nthreads: c_int) -> c_int;
+    pub fn sd_cas_hashes_files(ctx: *mut sd_cas_ctx, paths: *const *const c_char, sizes: *const u64, n: usize,
+                               d_hash32: *mut u8, d_valid: *mut u8, status: *mut i32, nthreads: c_int) -> c_int;
     pub fn sd_cas_id_path(ctx: *mut sd_cas_ctx, path: *const c_char, size: u64, out_hex17: *mut c_char,
                           status: *mut i32) -> c_int;
     pub fn sd_file_checksums(ctx: *mut sd_cas_ctx, paths: *const *const c_char, n: usize,

@@ -504,21 +504,19 @@ inline void to_hex(const uint8_t* h, int nbytes, char* out) { hex_lower(h, nbyte
 
 // Hashes (GPU, streaming) the whole-file cas message of a file that held more bytes than
 // its staged extent could take: le64(size) || every byte fs::read returns (cas.rs:25,29).
-int32_t cas_overflow(SlotPair& sl, int& cur, Streamer& st, const char* path, uint64_t size, char* out_hex17) {
+int32_t cas_overflow(SlotPair& sl, int& cur, Streamer& st, const char* path, uint64_t size, uint8_t out32[32]) {
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) return io_status(errno);
     MsgSource src(fd, MsgSource::READ_TO_EOF);
     src.set_prefix_le64(size);
-    uint8_t h[32];
     int32_t rc;
     try {
-        rc = st.hash(sl, cur, src, size + 8, h);
+        rc = st.hash(sl, cur, src, size + 8, out32);
     } catch (...) {
         close(fd);
         throw;
     }
     close(fd);
-    if (rc == SD_FILE_OK) to_hex(h, 8, out_hex17);  // cas.rs:61 to_hex()[..16]
     return rc;
 }
 
@@ -790,10 +788,11 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
 // kernels and D2H run on the other slot's stream.  A whole-kind file that turns out
 // longer than its planned extent (it grew since the caller's stat) is hashed afterwards
 // from the file itself, streamed (fs::read hashes every byte, cas.rs:29).
-int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n, char* out_hex17,
-                     int32_t* status, int nthreads) {
-    SD_GUARD_BEGIN
-    if (!ctx || (n && (!paths || !sizes || !out_hex17 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
+namespace {
+// The body of sd_cas_ids_files (hex to host memory) and sd_cas_hashes_files (the 32-byte
+// hashes to device memory, for the multi-GPU dedup): out_hex17 xor d_hash32.
+void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n, char* out_hex17,
+               uint8_t* d_hash32, int32_t* status, int nthreads) {
     ctx->bind();
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 64) nthreads = 64;
@@ -830,9 +829,16 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
         if (!launched[k].busy) return;
         HIP_CHECK(hipStreamSynchronize(slots[k].stream));
         const uint8_t* h = slots[k].host_hashes.u8();
-        for (size_t q = 0; q < launched[k].files.size(); q++)
-            to_hex(h + q * 32, 8, out_hex17 + launched[k].files[q] * 17);  // cas.rs:61 to_hex()[..16]
+        if (out_hex17)
+            for (size_t q = 0; q < launched[k].files.size(); q++)
+                to_hex(h + q * 32, 8, out_hex17 + launched[k].files[q] * 17);  // cas.rs:61 to_hex()[..16]
         launched[k].busy = false;
+    };
+    DevBuf dev_idx[2];                          // device output: the launched window's file rows
+    std::vector<uint32_t> dev_idx_h[2];         // (their host copies, alive until the harvest)
+    auto put_hash = [&](size_t f, const uint8_t h[32]) {  // a hash computed off the windows
+        if (out_hex17) to_hex(h, 8, out_hex17 + f * 17);       // cas.rs:61 to_hex()[..16]
+        else HIP_CHECK(hipMemcpy(d_hash32 + 32 * f, h, 32, hipMemcpyHostToDevice));
     };
     std::vector<size_t> overflow;                                      // regular files that grew
     std::vector<std::pair<size_t, std::vector<uint8_t>>> captured;    // pipes / devices, read whole
@@ -904,7 +910,14 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
             HIP_CHECK(hipEventRecord(copied[w], sl.stream));
             copy_pending[w] = true;
             run_cas_batch(&batches[w], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
-            HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, m * 32, hipMemcpyDeviceToHost, sl.stream));
+            if (d_hash32) {  // device output: the window's hashes scattered to their files' rows
+                dev_idx_h[w].assign(W.idx.begin(), W.idx.end());
+                dev_idx[w].upload(dev_idx_h[w], sl.stream);
+                HIP_CHECK(sdk::launch_scatter_hash(sl.hashes.as<uint32_t>(), dev_idx[w].as<uint32_t>(), (uint32_t)m,
+                                                   reinterpret_cast<uint32_t*>(d_hash32), sl.stream));
+            } else {
+                HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, m * 32, hipMemcpyDeviceToHost, sl.stream));
+            }
             launched[w].files = W.idx;
             launched[w].busy = true;
         }
@@ -915,15 +928,41 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
     if (!overflow.empty() || !captured.empty()) {
         Streamer st([](size_t, const uint8_t*) {});
         int cur = 0;
-        for (size_t f : overflow) status[f] = cas_overflow(slots, cur, st, paths[f], sizes[f], out_hex17 + f * 17);
+        for (size_t f : overflow) {
+            uint8_t h[32];
+            status[f] = cas_overflow(slots, cur, st, paths[f], sizes[f], h);
+            if (status[f] == SD_FILE_OK) put_hash(f, h);
+        }
         for (auto& c : captured) {  // le64(size) || every byte the pipe gave (cas.rs:25,29)
             MsgSource src(-1, MsgSource::READ_TO_EOF);
             src.set_prefix_le64(sizes[c.first]);
             src.set_memory(c.second.data(), c.second.size());
             uint8_t h[32];
             status[c.first] = st.hash(slots, cur, src, c.second.size() + 8, h);
-            if (status[c.first] == SD_FILE_OK) to_hex(h, 8, out_hex17 + c.first * 17);
+            if (status[c.first] == SD_FILE_OK) put_hash(c.first, h);
         }
+    }
+}
+}  // namespace
+
+int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n, char* out_hex17,
+                     int32_t* status, int nthreads) {
+    SD_GUARD_BEGIN
+    if (!ctx || (n && (!paths || !sizes || !out_hex17 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    cas_files(ctx, paths, sizes, n, out_hex17, nullptr, status, nthreads);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cas_hashes_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n,
+                        uint8_t* d_hash32, uint8_t* d_valid, int32_t* status, int nthreads) {
+    SD_GUARD_BEGIN
+    if (!ctx || (n && (!paths || !sizes || !d_hash32 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    cas_files(ctx, paths, sizes, n, nullptr, d_hash32, status, nthreads);
+    if (d_valid && n) {  // the records sd_cas_dedup_mgpu takes: hashed, and not empty (mod.rs:80-88)
+        std::vector<uint8_t> v(n);
+        for (size_t i = 0; i < n; i++) v[i] = status[i] == SD_FILE_OK && sizes[i] != 0;
+        HIP_CHECK(hipMemcpy(d_valid, v.data(), n, hipMemcpyHostToDevice));
     }
     return SD_OK;
     SD_GUARD_END

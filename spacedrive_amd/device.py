@@ -73,6 +73,21 @@ class Context:
     def checksum_batch(self, offsets, lens) -> "ChecksumBatch":
         return ChecksumBatch(self, offsets, lens)
 
+    # -------------------------------------------------------------- files -> device hashes
+    def hashes_files(self, paths, sizes, d_hash32, d_valid=None, nthreads: int = 16) -> np.ndarray:
+        """sd_cas_hashes_files: generate_cas_id's messages of these files hashed into
+        d_hash32 (device, n x 32 B; the cas_id is each row's first 8 bytes) and, if given,
+        d_valid (device, n B: hashed and not empty).  Returns the int32 status per file."""
+        import os
+        n = len(paths)
+        status = np.zeros(max(n, 1), np.int32)
+        arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+        sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+        assert d_hash32.numel() >= 32 * n and (d_valid is None or d_valid.numel() >= n)
+        check(lib().sd_cas_hashes_files(self.handle, arr, _ptr(sz), n, _ptr(d_hash32),
+                                        None if d_valid is None else _ptr(d_valid), _ptr(status), nthreads))
+        return status[:n]
+
     # -------------------------------------------------------------- synthetic data
     def synth_stage_cas(self, d_sizes, d_cids, d_twins, d_extents, n, d_staged, stream=None) -> None:
         check(lib().sd_synth_stage_cas(self.handle, _ptr(d_sizes), _ptr(d_cids), _ptr(d_twins),

@@ -930,3 +930,45 @@ def test_file_checksum_split_on_device(ctx, tmp_path, oracle_native):
     p = tmp_path / "big.bin"
     p.write_bytes(data)
     assert file_checksum_split(str(p), ctx=ctx) == oracle_native.blake3(data).hex()
+
+
+def test_hashes_files_to_device_then_rccl_dedup(ctx, tmp_path, oracle_native, rccl_comm):
+    """sd_cas_hashes_files -> sd_cas_dedup_mgpu: a rank's library scan from files with the
+    hashes left on the device.  Rows equal the oracle's full hashes of the reference's
+    messages (including a whole file that outgrew its size and an empty file), d_valid
+    marks hashed non-empty files, and the RCCL dedup over those rows equals the host
+    grouping of the oracle's cas_ids."""
+    import spacedrive_amd as sd  # noqa: F401
+    from spacedrive_amd import synth
+    n = 3000
+    sizes, cids, twins = synth.library(0, n, n, dup_frac=0.3)
+    sizes = np.minimum(sizes, np.uint64(1 << 30))
+    ext, total = sd.stage_plan(sizes)
+    buf = oracle_native.stage_synth(sizes, cids, twins, ext["msg_offset"], total)
+    paths = synth.write_files(str(tmp_path), sizes, buf, ext)
+    plan = sizes.copy()
+    small = [i for i in range(n) if 100 < sizes[i] <= 102400]
+    plan[small[0]] = sizes[small[0]] - 60  # the file is longer than its metadata said: re-read
+    paths[5] = str(tmp_path / "missing")
+    want, wst = oracle_native.cas_ids_files(paths, plan, nthreads=NT)
+    d_hash = torch.zeros((n, 32), dtype=torch.uint8, device="cuda")
+    d_valid = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = ctx.hashes_files(paths, plan, d_hash, d_valid)
+    assert np.array_equal(st != 0, wst != 0) and st[5] != 0
+    h = d_hash.cpu().numpy()
+    ok = st == 0
+    assert np.array_equal(h[ok, :8], want[ok])
+    assert np.array_equal(d_valid.cpu().numpy().astype(bool), ok & (plan != 0))
+    # the rank's dedup over the device rows, as a multi-GPU scan would run it
+    base = 40_000
+    cap = n + 16
+    recs = torch.empty((cap, 2), dtype=torch.int64, device="cuda")
+    rep = torch.empty(cap, dtype=torch.int64, device="cuda")
+    own = torch.empty(cap, dtype=torch.int64, device="cuda")
+    m, ng = ctx.dedup_mgpu(rccl_comm, d_hash, d_valid, n, base, recs, rep, own, cap)
+    torch.cuda.synchronize()
+    valid = ok & (plan != 0)
+    recs_h = np.stack([keys_from_hashes(h)[valid].view(np.int64), np.arange(base, base + n)[valid]], axis=1)
+    gr, grep, gng = group_host(recs_h)
+    assert m == len(gr) and ng == gng
+    assert np.array_equal(recs[:m].cpu().numpy(), gr) and np.array_equal(rep[:m].cpu().numpy(), grep)
