@@ -171,16 +171,24 @@ namespace {
 struct SlotPair {
     sd_cas_ctx* c;
     std::unique_ptr<Slot> s[2];
+    std::unique_ptr<Slot> cp;  // a third queue, for H2D copies issued back to back (copy_stream)
     explicit SlotPair(sd_cas_ctx* ctx) : c(ctx) {
         s[0] = c->acquire();
         s[1] = c->acquire();
     }
     ~SlotPair() {
-        for (auto& x : s)
-            if (x) {
-                (void)hipStreamSynchronize(x->stream);
-                c->release(std::move(x));
+        for (auto* x : {&s[0], &s[1], &cp})
+            if (*x) {
+                (void)hipStreamSynchronize((*x)->stream);
+                c->release(std::move(*x));
             }
+    }
+    // One stream for all of a call's host-to-device copies: they run one after the other on
+    // one DMA queue (two copies in flight on two streams measured 46 instead of 56 GB/s on
+    // some boxes), while the kernels of the two slots overlap them.
+    hipStream_t copy_stream() {
+        if (!cp) cp = c->acquire();
+        return cp->stream;
     }
     Slot& operator[](int k) { return *s[k]; }
     void sync_all() {
@@ -1271,6 +1279,34 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         for (size_t i = pend[k].i0; i < pend[k].i1; i++) to_hex(h + 32 * (i - pend[k].i0), 32, out_hex65 + 65 * i);
         pend[k].busy = false;
     };
+    // copies on one queue (copy_stream), kernels on the two slots' streams, joined by events:
+    // copied[k] = slot k's window has landed; used[k] = slot k's kernels no longer read it
+    hipStream_t cs = slots.copy_stream();
+    hipEvent_t copied[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
+    bool used_set[2] = {false, false};
+    struct Events {
+        hipEvent_t* e[2];
+        ~Events() {
+            for (auto* p : e)
+                for (int k = 0; k < 2; k++)
+                    if (p[k]) (void)hipEventDestroy(p[k]);
+        }
+    } ev_guard{{copied, used}};
+    for (int k = 0; k < 2; k++) {
+        HIP_CHECK(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&used[k], hipEventDisableTiming));
+    }
+    // H2D of `bytes` from `src` into slot k's device window, after its previous kernels
+    auto copy_in = [&](int k, const uint8_t* src, uint64_t bytes) {
+        if (used_set[k]) HIP_CHECK(hipStreamWaitEvent(cs, used[k], 0));
+        HIP_CHECK(hipMemcpyAsync(slots[k].staged.p, src, bytes, hipMemcpyHostToDevice, cs));
+        HIP_CHECK(hipEventRecord(copied[k], cs));
+        HIP_CHECK(hipStreamWaitEvent(slots[k].stream, copied[k], 0));
+    };
+    auto done_with = [&](int k) {
+        HIP_CHECK(hipEventRecord(used[k], slots[k].stream));
+        used_set[k] = true;
+    };
     int cur = 0;
     std::vector<uint64_t> offs, ls;
     for (size_t i = 0; i < n;) {
@@ -1283,15 +1319,14 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
             for (uint64_t pos = 0; pos < L; pos += W) {
                 const int k = cur;
                 cur ^= 1;
-                HIP_CHECK(hipStreamSynchronize(slots[k].stream));
                 const uint64_t here = std::min<uint64_t>(W, L - pos);
-                HIP_CHECK(hipMemcpyAsync(slots[k].staged.p, data + offsets[i] + pos, align_up(here, 64),
-                                         hipMemcpyHostToDevice, slots[k].stream));
+                copy_in(k, data + offsets[i] + pos, align_up(here, 64));
                 const uint32_t wg0 = (uint32_t)(pos / SD_CK_BLOCK);
                 const uint32_t wg1 = (uint32_t)std::min<uint64_t>(nb, wg0 + W / SD_CK_BLOCK);
                 HIP_CHECK(sdk::launch_ck_leaf(slots[k].staged.as<uint8_t>(), pos, 0, big.files.as<ck_file>(),
                                               big.wg_map.as<uint2>() + wg0, wg1 - wg0, big.lvl[0].as<uint32_t>(),
                                               slots[k].hashes.as<uint32_t>(), slots[k].stream));
+                done_with(k);
             }
             slots.sync_all();
             Slot& sl = slots[0];
@@ -1323,9 +1358,9 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         plan_checksum_batch(&batches[k], offs.data(), ls.data(), j - i, sl.stream);
         sl.hashes.ensure((j - i) * 32);
         sl.host_hashes.ensure((j - i) * 32);
-        HIP_CHECK(hipMemcpyAsync(sl.staged.p, data + lo, std::max<uint64_t>(hi - lo, 16), hipMemcpyHostToDevice,
-                                 sl.stream));
+        copy_in(k, data + lo, std::max<uint64_t>(hi - lo, 16));
         run_checksum_batch(&batches[k], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
+        done_with(k);
         HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, (j - i) * 32, hipMemcpyDeviceToHost, sl.stream));
         pend[k] = Pending{i, j, true};
         i = j;
