@@ -972,3 +972,38 @@ def test_hashes_files_to_device_then_rccl_dedup(ctx, tmp_path, oracle_native, rc
     gr, grep, gng = group_host(recs_h)
     assert m == len(gr) and ng == gng
     assert np.array_equal(recs[:m].cpu().numpy(), gr) and np.array_equal(rep[:m].cpu().numpy(), grep)
+
+
+def test_scan_library_from_files(ctx, tmp_path, oracle_native, rccl_comm):
+    """library.scan_library: shard plan -> files hashed into device rows -> RCCL dedup ->
+    Object owners, one rank; equal to the oracle's cas_ids (the reference's reads) and to
+    the host grouping and chunk-of-100 rule over them; the torch.distributed exchange gives
+    the same result."""
+    from spacedrive_amd import synth
+    from spacedrive_amd.identifier import object_owners
+    from spacedrive_amd.library import scan_library
+    n = 2500
+    sizes, cids, twins = synth.library(0, n, n, dup_frac=0.3)
+    sizes = np.minimum(sizes, np.uint64(1 << 30))
+    from spacedrive_amd.device import stage_plan
+    ext, total = stage_plan(sizes)
+    buf = oracle_native.stage_synth(sizes, cids, twins, ext["msg_offset"], total)
+    paths = synth.write_files(str(tmp_path), sizes, buf, ext)
+    paths[11] = str(tmp_path / "missing")
+    want, wst = oracle_native.cas_ids_files(paths, sizes, nthreads=NT)
+    r = scan_library(ctx, paths, sizes, comm=rccl_comm)
+    assert r["shard"] == (0, n)
+    for i in range(n):
+        if wst[i] == 0:
+            assert r["cas_ids"][i] == want[i].tobytes().hex(), i
+        else:
+            assert isinstance(r["cas_ids"][i], OSError), i
+    valid = (wst == 0) & (sizes != 0)
+    keys = want.copy().view(">u8").reshape(-1).astype(np.uint64)
+    gr, grep, gng = group_host(np.stack([keys[valid].view(np.int64), np.arange(n)[valid]], axis=1))
+    assert r["n_groups"] == gng
+    assert np.array_equal(r["records"].cpu().numpy(), gr) and np.array_equal(r["rep"].cpu().numpy(), grep)
+    own = object_owners(torch.from_numpy(gr[:, 1].copy()), torch.from_numpy(grep), 100).numpy()
+    assert np.array_equal(r["owner"].cpu().numpy(), own)
+    t = scan_library(ctx, paths, sizes)  # the torch.distributed statement of the exchange
+    assert t["n_groups"] == gng and np.array_equal(t["records"].cpu().numpy(), gr)
