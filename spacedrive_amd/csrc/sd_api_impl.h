@@ -1,0 +1,227 @@
+// sd_api_impl.h -- the host-side types shared by the C ABI's translation units
+// (sd_cas_api.cpp: context, batches, dedup; sd_files.cpp: the file readers' pipelines and
+// streaming): device / pinned buffers, stream slots, the opaque ABI structs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "sd_host.h"
+#include "sd_internal.h"
+#include "stage_pool.h"
+
+#define HIP_CHECK(expr)                                                                              \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess)                                                                        \
+            throw sd_failure(e_ == hipErrorOutOfMemory ? SD_ERR_NOMEM : SD_ERR_DEVICE,              \
+                             std::string(#expr) + ": " + hipGetErrorString(e_));                    \
+    } while (0)
+
+namespace sdi {
+
+inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+inline void to_hex(const uint8_t* h, int nbytes, char* out) { hex_lower(h, nbytes, out); }
+
+// RAII device buffer
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void alloc(size_t n) {
+        reset();
+        if (n == 0) n = 16;
+        HIP_CHECK(hipMalloc(&p, n));
+        bytes = n;
+    }
+    // grow-only (never frees a buffer that is large enough: hipFree synchronises the device)
+    void ensure(size_t n) {
+        if (n > bytes) alloc(n);
+    }
+    // grow keeping the contents (the caller has synchronised every stream writing it)
+    void grow_preserve(size_t n) {
+        if (n <= bytes) return;
+        void* q = nullptr;
+        HIP_CHECK(hipMalloc(&q, n));
+        if (p) {
+            const hipError_t e = hipMemcpy(q, p, bytes, hipMemcpyDeviceToDevice);
+            if (e != hipSuccess) {
+                (void)hipFree(q);
+                HIP_CHECK(e);
+            }
+            (void)hipFree(p);
+        }
+        p = q;
+        bytes = n;
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+    template <class T>
+    void upload(const std::vector<T>& v, hipStream_t s = nullptr) {
+        ensure(v.size() * sizeof(T));
+        if (v.empty()) return;
+        if (s) HIP_CHECK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+        else HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    }
+};
+
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~PinnedBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void ensure(size_t n) {
+        if (n <= bytes) return;
+        reset();
+        HIP_CHECK(hipHostMalloc(&p, n, hipHostMallocDefault));
+        bytes = n;
+    }
+    uint8_t* u8() const { return reinterpret_cast<uint8_t*>(p); }
+};
+
+// per-call working set of the host drop-in entry points
+struct Slot {
+    hipStream_t stream = nullptr;
+    DevBuf staged, hashes;
+    PinnedBuf host_hashes, window;
+};
+
+}  // namespace sdi
+
+struct sd_cas_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::mutex coal_mu;
+    sd_coalescer* coal = nullptr;  // latency path, created on the first single-file call
+    std::mutex pool_mu;
+    // File stager threads (sd_cas_ids_files).  One pool per context, grown to the largest
+    // thread count any call asked for; a caller holds its shared_ptr while it runs, so a
+    // concurrent call that grows the pool never destroys one in use.
+    std::shared_ptr<StagePool> pool;
+    std::shared_ptr<StagePool> stage_pool(int nthreads) {
+        std::lock_guard<std::mutex> g(pool_mu);
+        if (!pool || pool->threads() < nthreads) pool = std::make_shared<StagePool>(nthreads);
+        return pool;
+    }
+    sd_coalescer* coalescer() {
+        std::lock_guard<std::mutex> g(coal_mu);
+        if (!coal) coal = coalescer_create(this);
+        return coal;
+    }
+    std::vector<std::unique_ptr<sdi::Slot>> free_slots;
+
+    std::unique_ptr<sdi::Slot> acquire() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!free_slots.empty()) {
+                auto s = std::move(free_slots.back());
+                free_slots.pop_back();
+                return s;
+            }
+        }
+        auto s = std::make_unique<sdi::Slot>();
+        HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        return s;
+    }
+    void release(std::unique_ptr<sdi::Slot> s) {
+        std::lock_guard<std::mutex> g(mu);
+        free_slots.push_back(std::move(s));
+    }
+    void bind() { HIP_CHECK(hipSetDevice(device)); }
+    static hipStream_t pick(void* s) { return reinterpret_cast<hipStream_t>(s); }  // NULL = null stream
+};
+
+namespace sdi {
+
+// Two slots held for one call; released (after their streams drain) on scope exit.
+struct SlotPair {
+    sd_cas_ctx* c;
+    std::unique_ptr<Slot> s[2];
+    std::unique_ptr<Slot> cp;  // a third queue, for H2D copies issued back to back (copy_stream)
+    explicit SlotPair(sd_cas_ctx* ctx) : c(ctx) {
+        s[0] = c->acquire();
+        s[1] = c->acquire();
+    }
+    ~SlotPair() {
+        for (auto* x : {&s[0], &s[1], &cp})
+            if (*x) {
+                (void)hipStreamSynchronize((*x)->stream);
+                c->release(std::move(*x));
+            }
+    }
+    // One stream for all of a call's host-to-device copies: they run one after the other on
+    // one DMA queue (two copies in flight on two streams measured 46 instead of 56 GB/s on
+    // some boxes), while the kernels of the two slots overlap them.
+    hipStream_t copy_stream() {
+        if (!cp) cp = c->acquire();
+        return cp->stream;
+    }
+    Slot& operator[](int k) { return *s[k]; }
+    void sync_all() {
+        HIP_CHECK(hipStreamSynchronize(s[0]->stream));
+        HIP_CHECK(hipStreamSynchronize(s[1]->stream));
+    }
+};
+
+}  // namespace sdi
+
+struct sd_checksum_batch {
+    size_t n = 0;
+    CkPlan plan;
+    sdi::DevBuf files, wg_map;
+    sdi::DevBuf lvl[2];
+    std::vector<std::unique_ptr<sdi::DevBuf>> pass_wgs;  // capacity reused across replans
+};
+
+// one file over the ranks of a communicator (include/sd_cas.h, sd_split_range)
+struct sd_split_checksum {
+    SplitPlan sp;
+    sd_checksum_batch plan;  // the whole file as one message: leaf table + reduce passes
+};
+
+struct sd_cas_batch {
+    size_t n = 0;
+    uint32_t n_sampled = 0, n_whole = 0, n_long = 0;
+    uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0, whole_chunks = 0;
+    WholePlan whole;  // work lists (kernel formats in cas_kernels.hip, k_whole_items / _merge8)
+    sdi::DevBuf ext, sidx, soff, full_items, tail_items, merge_a, merge_b, cvbuf, cv2;
+    // whole-file messages longer than SD_WHOLE_ITEMS_MAX: a checksum sub-batch over their
+    // byte ranges, its hashes scattered to out[long_idx[i]]
+    sd_checksum_batch lng;
+    sdi::DevBuf long_idx, long_out;
+    // host copies backing async uploads
+    std::vector<sd_extent> h_ext;
+    std::vector<uint32_t> h_sidx, h_long_idx;
+    std::vector<uint64_t> h_soff;
+};
+
+
+namespace sdi {
+// checksum batches (device): (re)plan reusing the batch's buffers; the reduce passes; leaf + reduce
+void plan_checksum_batch(sd_checksum_batch* b, const uint64_t* offsets, const uint64_t* lens, size_t n,
+                         hipStream_t stream);
+void run_checksum_reduce(const sd_checksum_batch* b, uint32_t* out, hipStream_t s);
+void run_checksum_batch(const sd_checksum_batch* b, const uint8_t* d_data, uint8_t* d_hash32, hipStream_t s);
+// cas batches (device)
+void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t stream);
+void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_hash32, hipStream_t s,
+                   int parts = SD_PART_SAMPLED | SD_PART_WHOLE);
+}  // namespace sdi

@@ -8,6 +8,9 @@
 // streams; prepared batches own their scratch (one run of a batch at a time).  Every
 // entry point catches all C++ exceptions (the reference FFI fences panics with
 // catch_unwind, apps/mobile/modules/sd-core/ios/crate/src/lib.rs:41,60).
+// This file: the context, staging and device batches, the latency path, dedup, synthetic
+// data and device utilities; the file-reading pipelines and the streaming hash are in
+// sd_files.cpp, the types both share in sd_api_impl.h.
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
@@ -28,208 +31,9 @@
 #include <thread>
 #include <vector>
 
-#include "sd_host.h"
-#include "sd_internal.h"
-#include "stage_pool.h"
+#include "sd_api_impl.h"
 
-namespace {
-
-#define HIP_CHECK(expr)                                                                              \
-    do {                                                                                             \
-        hipError_t e_ = (expr);                                                                      \
-        if (e_ != hipSuccess)                                                                        \
-            throw sd_failure(e_ == hipErrorOutOfMemory ? SD_ERR_NOMEM : SD_ERR_DEVICE,              \
-                             std::string(#expr) + ": " + hipGetErrorString(e_));                    \
-    } while (0)
-
-inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
-
-// RAII device buffer
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    DevBuf() = default;
-    DevBuf(const DevBuf&) = delete;
-    DevBuf& operator=(const DevBuf&) = delete;
-    ~DevBuf() { reset(); }
-    void reset() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    void alloc(size_t n) {
-        reset();
-        if (n == 0) n = 16;
-        HIP_CHECK(hipMalloc(&p, n));
-        bytes = n;
-    }
-    // grow-only (never frees a buffer that is large enough: hipFree synchronises the device)
-    void ensure(size_t n) {
-        if (n > bytes) alloc(n);
-    }
-    // grow keeping the contents (the caller has synchronised every stream writing it)
-    void grow_preserve(size_t n) {
-        if (n <= bytes) return;
-        void* q = nullptr;
-        HIP_CHECK(hipMalloc(&q, n));
-        if (p) {
-            const hipError_t e = hipMemcpy(q, p, bytes, hipMemcpyDeviceToDevice);
-            if (e != hipSuccess) {
-                (void)hipFree(q);
-                HIP_CHECK(e);
-            }
-            (void)hipFree(p);
-        }
-        p = q;
-        bytes = n;
-    }
-    template <class T>
-    T* as() const { return reinterpret_cast<T*>(p); }
-    template <class T>
-    void upload(const std::vector<T>& v, hipStream_t s = nullptr) {
-        ensure(v.size() * sizeof(T));
-        if (v.empty()) return;
-        if (s) HIP_CHECK(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
-        else HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
-    }
-};
-
-struct PinnedBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    ~PinnedBuf() { reset(); }
-    void reset() {
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    void ensure(size_t n) {
-        if (n <= bytes) return;
-        reset();
-        HIP_CHECK(hipHostMalloc(&p, n, hipHostMallocDefault));
-        bytes = n;
-    }
-    uint8_t* u8() const { return reinterpret_cast<uint8_t*>(p); }
-};
-
-// per-call working set of the host drop-in entry points
-struct Slot {
-    hipStream_t stream = nullptr;
-    DevBuf staged, hashes;
-    PinnedBuf host_hashes, window;
-};
-
-}  // namespace
-
-struct sd_cas_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    std::mutex mu;
-    std::mutex coal_mu;
-    sd_coalescer* coal = nullptr;  // latency path, created on the first single-file call
-    std::mutex pool_mu;
-    // File stager threads (sd_cas_ids_files).  One pool per context, grown to the largest
-    // thread count any call asked for; a caller holds its shared_ptr while it runs, so a
-    // concurrent call that grows the pool never destroys one in use.
-    std::shared_ptr<StagePool> pool;
-    std::shared_ptr<StagePool> stage_pool(int nthreads) {
-        std::lock_guard<std::mutex> g(pool_mu);
-        if (!pool || pool->threads() < nthreads) pool = std::make_shared<StagePool>(nthreads);
-        return pool;
-    }
-    sd_coalescer* coalescer() {
-        std::lock_guard<std::mutex> g(coal_mu);
-        if (!coal) coal = coalescer_create(this);
-        return coal;
-    }
-    std::vector<std::unique_ptr<Slot>> free_slots;
-
-    std::unique_ptr<Slot> acquire() {
-        {
-            std::lock_guard<std::mutex> g(mu);
-            if (!free_slots.empty()) {
-                auto s = std::move(free_slots.back());
-                free_slots.pop_back();
-                return s;
-            }
-        }
-        auto s = std::make_unique<Slot>();
-        HIP_CHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-        return s;
-    }
-    void release(std::unique_ptr<Slot> s) {
-        std::lock_guard<std::mutex> g(mu);
-        free_slots.push_back(std::move(s));
-    }
-    void bind() { HIP_CHECK(hipSetDevice(device)); }
-    static hipStream_t pick(void* s) { return reinterpret_cast<hipStream_t>(s); }  // NULL = null stream
-};
-
-namespace {
-
-// Two slots held for one call; released (after their streams drain) on scope exit.
-struct SlotPair {
-    sd_cas_ctx* c;
-    std::unique_ptr<Slot> s[2];
-    std::unique_ptr<Slot> cp;  // a third queue, for H2D copies issued back to back (copy_stream)
-    explicit SlotPair(sd_cas_ctx* ctx) : c(ctx) {
-        s[0] = c->acquire();
-        s[1] = c->acquire();
-    }
-    ~SlotPair() {
-        for (auto* x : {&s[0], &s[1], &cp})
-            if (*x) {
-                (void)hipStreamSynchronize((*x)->stream);
-                c->release(std::move(*x));
-            }
-    }
-    // One stream for all of a call's host-to-device copies: they run one after the other on
-    // one DMA queue (two copies in flight on two streams measured 46 instead of 56 GB/s on
-    // some boxes), while the kernels of the two slots overlap them.
-    hipStream_t copy_stream() {
-        if (!cp) cp = c->acquire();
-        return cp->stream;
-    }
-    Slot& operator[](int k) { return *s[k]; }
-    void sync_all() {
-        HIP_CHECK(hipStreamSynchronize(s[0]->stream));
-        HIP_CHECK(hipStreamSynchronize(s[1]->stream));
-    }
-};
-
-}  // namespace
-
-struct sd_checksum_batch {
-    size_t n = 0;
-    CkPlan plan;
-    DevBuf files, wg_map;
-    DevBuf lvl[2];
-    std::vector<std::unique_ptr<DevBuf>> pass_wgs;  // capacity reused across replans
-};
-
-// one file over the ranks of a communicator (include/sd_cas.h, sd_split_range)
-struct sd_split_checksum {
-    SplitPlan sp;
-    sd_checksum_batch plan;  // the whole file as one message: leaf table + reduce passes
-};
-
-struct sd_cas_batch {
-    size_t n = 0;
-    uint32_t n_sampled = 0, n_whole = 0, n_long = 0;
-    uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0, whole_chunks = 0;
-    WholePlan whole;  // work lists (kernel formats in cas_kernels.hip, k_whole_items / _merge8)
-    DevBuf ext, sidx, soff, full_items, tail_items, merge_a, merge_b, cvbuf, cv2;
-    // whole-file messages longer than SD_WHOLE_ITEMS_MAX: a checksum sub-batch over their
-    // byte ranges, its hashes scattered to out[long_idx[i]]
-    sd_checksum_batch lng;
-    DevBuf long_idx, long_out;
-    // host copies backing async uploads
-    std::vector<sd_extent> h_ext;
-    std::vector<uint32_t> h_sidx, h_long_idx;
-    std::vector<uint64_t> h_soff;
-};
-
-namespace {
+namespace sdi {
 
 // ----------------------------------------------------------- checksum batches (device)
 // (Re)plans `b` for these byte ranges reusing its device buffers (grow-only).  With a
@@ -317,8 +121,7 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
     }
 }
 
-void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_hash32, hipStream_t s,
-                   int parts = SD_PART_SAMPLED | SD_PART_WHOLE) {
+void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_hash32, hipStream_t s, int parts) {
     uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
     if (parts & SD_PART_SAMPLED)
         HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->soff.as<uint64_t>(), b->sidx.as<uint32_t>(), b->n_sampled, out,
@@ -338,197 +141,10 @@ void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_ha
     }
 }
 
-// ------------------------------------------------------- streaming (unknown length)
-// Hashes messages read front to back from a MsgSource through 256 MiB windows on the two
-// alternating slots.  A message's length is only known when its source ends, which is all
-// the 1 MiB-block tree needs: a full window (more than 1 MiB) holds 256 complete, non-final
-// blocks whose subtree CVs do not depend on the total, so they are hashed as the windows
-// arrive (a provisional one-message table of unbounded length); the final window then runs
-// with the message's real length, and the reduce passes merge all block CVs.
-//
-// Nothing waits for a message to finish: its final window, reduce and the 32-byte D2H are
-// queued on one slot's stream (after an event wait on the other slot's last window of the
-// same message), and the hash is handed to `done(tag, h32)` the next time that stream is
-// synchronised -- by the Streamer itself before it reuses the slot's window, by the
-// caller's collect(), or by finish().  So the host reads the next file while the GPU
-// finishes the last one.  Two per-message plans alternate; a plan is rebuilt only after
-// the events of the message that last used it have completed.
-struct Streamer {
-    static constexpr uint64_t W = 256ull << 20;  // a multiple of the 1 MiB leaf block
-    static constexpr uint32_t BPW = (uint32_t)(W / SD_CK_BLOCK);
-    static constexpr size_t RING = 16;  // results queued per slot between two syncs of it
-    using Done = std::function<void(size_t tag, const uint8_t* h32)>;
+}  // namespace sdi
 
-    struct Msg {
-        sd_checksum_batch fin;  // the final plan: one message of the final length
-        hipEvent_t ev[2] = {nullptr, nullptr};
-        bool used[2] = {false, false};  // ev[k] recorded since the plan was last rebuilt
-    };
-    Msg msg[2];
-    int next_msg = 0;
-    DevBuf prov_files, prov_map;  // full windows: {0, 2^62, 0} and (0, b) for b < BPW
-    bool prov_ready = false;
-    DevBuf rdev[2];
-    PinnedBuf rhost[2];
-    std::vector<size_t> rtag[2];
-    Done done;
+using namespace sdi;
 
-    explicit Streamer(Done d) : done(std::move(d)) {}
-    Streamer(const Streamer&) = delete;
-    Streamer& operator=(const Streamer&) = delete;
-    ~Streamer() {
-        for (auto& m : msg)
-            for (auto& e : m.ev)
-                if (e) (void)hipEventDestroy(e);
-    }
-
-    static void prepare(SlotPair& sl) {
-        for (int k = 0; k < 2; k++) {
-            sl[k].window.ensure(W + 128);
-            sl[k].staged.ensure(W + 128);
-            sl[k].hashes.ensure(32);
-            sl[k].host_hashes.ensure(32);
-        }
-    }
-    // Hands over the hashes queued on slot k.  The caller has synchronised its stream.
-    void collect(int k) {
-        for (size_t q = 0; q < rtag[k].size(); q++) done(rtag[k][q], rhost[k].u8() + 32 * q);
-        rtag[k].clear();
-    }
-    void sync_collect(SlotPair& sl, int k) {
-        HIP_CHECK(hipStreamSynchronize(sl[k].stream));
-        collect(k);
-    }
-    void finish(SlotPair& sl) {
-        sync_collect(sl, 0);
-        sync_collect(sl, 1);
-    }
-    void record(Msg& m, SlotPair& sl, int k) {
-        if (!m.ev[k]) HIP_CHECK(hipEventCreateWithFlags(&m.ev[k], hipEventDisableTiming));
-        HIP_CHECK(hipEventRecord(m.ev[k], sl[k].stream));
-        m.used[k] = true;
-    }
-    void wait_idle(Msg& m) {  // every launch of the message that last used this plan is done
-        for (int k = 0; k < 2; k++)
-            if (m.used[k]) {
-                HIP_CHECK(hipEventSynchronize(m.ev[k]));
-                m.used[k] = false;
-            }
-    }
-
-    // Queues the hash of one message; SD_FILE_OK means done(tag, ...) will follow, anything
-    // else is the source's I/O status (no result for this tag).
-    int32_t hash_async(SlotPair& sl, int& cur, MsgSource& src, uint64_t size_hint, size_t tag) {
-        prepare(sl);
-        if (!prov_ready) {
-            std::vector<ck_file> f{ck_file{0, 1ull << 62, 0}};
-            std::vector<sd_u32x2> mp(BPW);
-            for (uint32_t b = 0; b < BPW; b++) mp[b] = sd_u32x2{0, b};
-            prov_files.upload(f);
-            prov_map.upload(mp);
-            for (int k = 0; k < 2; k++) {
-                rdev[k].ensure(RING * 32);
-                rhost[k].ensure(RING * 32);
-            }
-            prov_ready = true;
-        }
-        Msg& m = msg[next_msg];
-        next_msg ^= 1;
-        wait_idle(m);
-        sd_checksum_batch& fin = m.fin;
-        const uint64_t cap0 = (uint64_t)std::max<uint64_t>(size_hint / SD_CK_BLOCK + 2, 2 * BPW) * 32;
-        if (cap0 > fin.lvl[0].bytes) fin.lvl[0].grow_preserve(cap0);  // nothing of this plan in flight
-        uint64_t pos = 0;
-        for (;;) {
-            const int k = cur;
-            cur ^= 1;
-            sync_collect(sl, k);  // its window is free again
-            uint8_t* win = sl[k].window.u8();
-            const uint64_t got = src.read(win, W);
-            if (src.err) return io_status(src.err);
-            if (got == W && !src.done) {  // a full window with more to come
-                const uint32_t blk0 = (uint32_t)(pos / SD_CK_BLOCK);
-                if ((uint64_t)(blk0 + BPW) * 32 > fin.lvl[0].bytes) {
-                    sl.sync_all();  // both slots may hold windows of this message
-                    fin.lvl[0].grow_preserve((size_t)(blk0 + BPW) * 64);
-                }
-                HIP_CHECK(hipMemcpyAsync(sl[k].staged.p, win, W, hipMemcpyHostToDevice, sl[k].stream));
-                HIP_CHECK(sdk::launch_ck_leaf(sl[k].staged.as<uint8_t>(), pos, blk0, prov_files.as<ck_file>(),
-                                              prov_map.as<uint2>(), BPW, fin.lvl[0].as<uint32_t>(),
-                                              sl[k].hashes.as<uint32_t>(), sl[k].stream));
-                record(m, sl, k);
-                pos += W;
-                continue;
-            }
-            const uint64_t L = pos + got;
-            const uint64_t nb = L == 0 ? 1 : (L + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
-            if (nb * 32 > fin.lvl[0].bytes) {  // grew past the hint: keep the CVs
-                sl.sync_all();
-                fin.lvl[0].grow_preserve((size_t)nb * 32);
-            }
-            if (m.used[k ^ 1]) HIP_CHECK(hipStreamWaitEvent(sl[k].stream, m.ev[k ^ 1], 0));  // its windows first
-            const uint64_t off0 = 0;
-            // async uploads from fin's host tables: they stay valid until wait_idle(m)
-            plan_checksum_batch(&fin, &off0, &L, 1, sl[k].stream);
-            if (rtag[k].size() == RING) sync_collect(sl, k);
-            const size_t q = rtag[k].size();
-            uint32_t* out = rdev[k].as<uint32_t>() + 8 * q;
-            if (got > 0 || L == 0) {
-                memset(win + got, 0, 64);
-                HIP_CHECK(hipMemcpyAsync(sl[k].staged.p, win, align_up(got, 64) + 64, hipMemcpyHostToDevice,
-                                         sl[k].stream));
-                const uint32_t wg0 = (uint32_t)(pos / SD_CK_BLOCK);
-                HIP_CHECK(sdk::launch_ck_leaf(sl[k].staged.as<uint8_t>(), pos, 0, fin.files.as<ck_file>(),
-                                              fin.wg_map.as<uint2>() + wg0, (uint32_t)(nb - wg0),
-                                              fin.lvl[0].as<uint32_t>(), out, sl[k].stream));
-            }
-            run_checksum_reduce(&fin, out, sl[k].stream);
-            HIP_CHECK(hipMemcpyAsync(rhost[k].u8() + 32 * q, out, 32, hipMemcpyDeviceToHost, sl[k].stream));
-            record(m, sl, k);
-            rtag[k].push_back(tag);
-            return SD_FILE_OK;
-        }
-    }
-
-    // One message, waited for (the rare paths: cas messages that outgrew their extent).
-    int32_t hash(SlotPair& sl, int& cur, MsgSource& src, uint64_t size_hint, uint8_t out32[32]) {
-        finish(sl);  // earlier messages' results go to their own callback
-        Done keep = std::move(done);
-        done = [&](size_t, const uint8_t* h) { memcpy(out32, h, 32); };
-        int32_t rc;
-        try {
-            rc = hash_async(sl, cur, src, size_hint, 0);
-            finish(sl);
-        } catch (...) {
-            done = std::move(keep);
-            throw;
-        }
-        done = std::move(keep);
-        return rc;
-    }
-};
-
-inline void to_hex(const uint8_t* h, int nbytes, char* out) { hex_lower(h, nbytes, out); }
-
-// Hashes (GPU, streaming) the whole-file cas message of a file that held more bytes than
-// its staged extent could take: le64(size) || every byte fs::read returns (cas.rs:25,29).
-int32_t cas_overflow(SlotPair& sl, int& cur, Streamer& st, const char* path, uint64_t size, uint8_t out32[32]) {
-    const int fd = open(path, O_RDONLY | O_CLOEXEC);
-    if (fd < 0) return io_status(errno);
-    MsgSource src(fd, MsgSource::READ_TO_EOF);
-    src.set_prefix_le64(size);
-    int32_t rc;
-    try {
-        rc = st.hash(sl, cur, src, size + 8, out32);
-    } catch (...) {
-        close(fd);
-        throw;
-    }
-    close(fd);
-    return rc;
-}
-
-}  // namespace
 
 int sd_ctx_device(const sd_cas_ctx* ctx) { return ctx->device; }
 const SplitPlan& sd_split_plan_of(const sd_split_checksum* x) { return x->sp; }
@@ -789,193 +405,6 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
     SD_GUARD_END
 }
 
-// Path-based drop-in batch: generate_cas_id (cas.rs:23-62) for n (path, size) pairs,
-// the sizes being the ones the caller's metadata reported (FileMetadata::new,
-// file_identifier/mod.rs:65-97).  Files are planned into windows of consecutive files;
-// the stager pool reads window k+1 into one pinned slot while window k's H2D copy,
-// kernels and D2H run on the other slot's stream.  A whole-kind file that turns out
-// longer than its planned extent (it grew since the caller's stat) is hashed afterwards
-// from the file itself, streamed (fs::read hashes every byte, cas.rs:29).
-namespace {
-// The body of sd_cas_ids_files (hex to host memory) and sd_cas_hashes_files (the 32-byte
-// hashes to device memory, for the multi-GPU dedup): out_hex17 xor d_hash32.
-void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n, char* out_hex17,
-               uint8_t* d_hash32, int32_t* status, int nthreads) {
-    ctx->bind();
-    if (nthreads < 1) nthreads = 1;
-    if (nthreads > 64) nthreads = 64;
-    // nthreads reader threads stage in the background (start/wait) while this thread plans,
-    // launches and harvests the windows
-    std::shared_ptr<StagePool> pool = ctx->stage_pool(nthreads + 1);
-    const uint64_t WINDOW = (uint64_t)std::max(1, tuning_get(SD_TUNE_FILES_WINDOW_MB)) << 20;
-    SlotPair slots(ctx);
-    sd_cas_batch batches[2];
-    struct Win {  // the window being staged into a slot's pinned buffer
-        std::vector<sd_extent> ext;
-        std::vector<size_t> idx;                // input index of each extent
-        std::vector<std::vector<uint8_t>> cap;  // a pipe's / device's whole content (stage_one)
-        uint64_t bytes = 0;
-    } wins[2];
-    struct Launched {  // the window in flight on a slot's stream
-        std::vector<size_t> files;  // hashed files, in extent order
-        bool busy = false;
-    } launched[2];
-    hipEvent_t copied[2] = {nullptr, nullptr};  // the slot's pinned buffer has been read by its H2D
-    bool copy_pending[2] = {false, false};
-    struct Cleanup {  // on any exit: no reader left writing, no event leaked
-        StagePool* pool;
-        bool staging = false;
-        hipEvent_t* ev;
-        ~Cleanup() {
-            if (staging) pool->wait();
-            for (int k = 0; k < 2; k++)
-                if (ev[k]) (void)hipEventDestroy(ev[k]);
-        }
-    } cleanup{pool.get(), false, copied};
-    for (int k = 0; k < 2; k++) HIP_CHECK(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming));
-    auto harvest = [&](int k) {
-        if (!launched[k].busy) return;
-        HIP_CHECK(hipStreamSynchronize(slots[k].stream));
-        const uint8_t* h = slots[k].host_hashes.u8();
-        if (out_hex17)
-            for (size_t q = 0; q < launched[k].files.size(); q++)
-                to_hex(h + q * 32, 8, out_hex17 + launched[k].files[q] * 17);  // cas.rs:61 to_hex()[..16]
-        launched[k].busy = false;
-    };
-    DevBuf dev_idx[2];                          // device output: the launched window's file rows
-    std::vector<uint32_t> dev_idx_h[2];         // (their host copies, alive until the harvest)
-    auto put_hash = [&](size_t f, const uint8_t h[32]) {  // a hash computed off the windows
-        if (out_hex17) to_hex(h, 8, out_hex17 + f * 17);       // cas.rs:61 to_hex()[..16]
-        else HIP_CHECK(hipMemcpy(d_hash32 + 32 * f, h, 32, hipMemcpyHostToDevice));
-    };
-    std::vector<size_t> overflow;                                      // regular files that grew
-    std::vector<std::pair<size_t, std::vector<uint8_t>>> captured;    // pipes / devices, read whole
-    size_t i = 0;
-    // plans the next window (consecutive files whose messages fit WINDOW bytes) into slot w
-    // and starts the readers on it; false when no files are left
-    auto begin_window = [&](int w) -> bool {
-        if (i >= n) return false;
-        Win& W = wins[w];
-        W.ext.clear();
-        W.idx.clear();
-        uint64_t off = 0;
-        while (i < n) {
-            const sd_extent e = plan_extent(sizes[i], off);
-            const uint64_t next = align_up(off + e.msg_len, SD_STAGE_ALIGN);
-            if (!W.ext.empty() && next > WINDOW) break;
-            W.ext.push_back(e);
-            W.idx.push_back(i);
-            off = next;
-            i++;
-        }
-        W.bytes = off;
-        W.cap.assign(W.ext.size(), {});
-        if (copy_pending[w]) {  // the slot's last H2D must have read its buffer
-            HIP_CHECK(hipEventSynchronize(copied[w]));
-            copy_pending[w] = false;
-        }
-        if (slots[w].window.bytes < off + 64) {
-            harvest(w);  // a reallocation frees the buffer: nothing may still use it
-            slots[w].window.ensure(off + 64);
-        }
-        uint8_t* win = slots[w].window.u8();
-        pool->start(W.ext.size(), [&W, win, paths, status](size_t q) {
-            status[W.idx[q]] = stage_one(paths[W.idx[q]], W.ext[q], win, &W.cap[q]);
-        });
-        cleanup.staging = true;
-        return true;
-    };
-    int w = 0;
-    bool staging = begin_window(w);
-    while (staging) {
-        pool->wait();  // window w is staged
-        cleanup.staging = false;
-        Win& W = wins[w];
-        Slot& sl = slots[w];
-        // failed files (I/O error, short read) keep their status and leave the window;
-        // files longer than their extent are hashed from disk after the windows
-        size_t m = 0;
-        for (size_t q = 0; q < W.ext.size(); q++) {
-            if (status[W.idx[q]] == SD_FILE_OK) {
-                W.ext[m] = W.ext[q];
-                W.idx[m++] = W.idx[q];
-            } else if (status[W.idx[q]] == SD_FILE_CHANGED) {
-                if (W.cap[q].empty()) overflow.push_back(W.idx[q]);
-                else captured.emplace_back(W.idx[q], std::move(W.cap[q]));
-            }
-        }
-        W.ext.resize(m);
-        W.idx.resize(m);
-        const int next = w ^ 1;
-        staging = begin_window(next);  // the readers go on with the next window...
-        if (m) {                        // ...while this one is planned and launched
-            harvest(w);                 // slot w's previous launch (two windows back)
-            plan_cas_batch(&batches[w], W.ext.data(), m, sl.stream);
-            sl.staged.ensure(W.bytes + 64);
-            sl.hashes.ensure(m * 32);
-            sl.host_hashes.ensure(m * 32);
-            HIP_CHECK(hipMemcpyAsync(sl.staged.p, sl.window.p, W.bytes, hipMemcpyHostToDevice, sl.stream));
-            HIP_CHECK(hipEventRecord(copied[w], sl.stream));
-            copy_pending[w] = true;
-            run_cas_batch(&batches[w], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
-            if (d_hash32) {  // device output: the window's hashes scattered to their files' rows
-                dev_idx_h[w].assign(W.idx.begin(), W.idx.end());
-                dev_idx[w].upload(dev_idx_h[w], sl.stream);
-                HIP_CHECK(sdk::launch_scatter_hash(sl.hashes.as<uint32_t>(), dev_idx[w].as<uint32_t>(), (uint32_t)m,
-                                                   reinterpret_cast<uint32_t*>(d_hash32), sl.stream));
-            } else {
-                HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, m * 32, hipMemcpyDeviceToHost, sl.stream));
-            }
-            launched[w].files = W.idx;
-            launched[w].busy = true;
-        }
-        w = next;
-    }
-    harvest(0);
-    harvest(1);
-    if (!overflow.empty() || !captured.empty()) {
-        Streamer st([](size_t, const uint8_t*) {});
-        int cur = 0;
-        for (size_t f : overflow) {
-            uint8_t h[32];
-            status[f] = cas_overflow(slots, cur, st, paths[f], sizes[f], h);
-            if (status[f] == SD_FILE_OK) put_hash(f, h);
-        }
-        for (auto& c : captured) {  // le64(size) || every byte the pipe gave (cas.rs:25,29)
-            MsgSource src(-1, MsgSource::READ_TO_EOF);
-            src.set_prefix_le64(sizes[c.first]);
-            src.set_memory(c.second.data(), c.second.size());
-            uint8_t h[32];
-            status[c.first] = st.hash(slots, cur, src, c.second.size() + 8, h);
-            if (status[c.first] == SD_FILE_OK) put_hash(c.first, h);
-        }
-    }
-}
-}  // namespace
-
-int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n, char* out_hex17,
-                     int32_t* status, int nthreads) {
-    SD_GUARD_BEGIN
-    if (!ctx || (n && (!paths || !sizes || !out_hex17 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
-    cas_files(ctx, paths, sizes, n, out_hex17, nullptr, status, nthreads);
-    return SD_OK;
-    SD_GUARD_END
-}
-
-int sd_cas_hashes_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n,
-                        uint8_t* d_hash32, uint8_t* d_valid, int32_t* status, int nthreads) {
-    SD_GUARD_BEGIN
-    if (!ctx || (n && (!paths || !sizes || !d_hash32 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
-    cas_files(ctx, paths, sizes, n, nullptr, d_hash32, status, nthreads);
-    if (d_valid && n) {  // the records sd_cas_dedup_mgpu takes: hashed, and not empty (mod.rs:80-88)
-        std::vector<uint8_t> v(n);
-        for (size_t i = 0; i < n; i++) v[i] = status[i] == SD_FILE_OK && sizes[i] != 0;
-        HIP_CHECK(hipMemcpy(d_valid, v.data(), n, hipMemcpyHostToDevice));
-    }
-    return SD_OK;
-    SD_GUARD_END
-}
-
 // ------------------------------------------------------------------- latency path
 int sd_cas_id_path(sd_cas_ctx* ctx, const char* path, uint64_t size, char* out_hex17, int32_t* status) {
     SD_GUARD_BEGIN
@@ -1098,275 +527,6 @@ int sd_split_checksum_root(sd_cas_ctx* ctx, sd_split_checksum* x, const uint8_t*
         HIP_CHECK(hipMemcpyAsync(x->plan.lvl[0].p, d_cvs, x->sp.nb * 32, hipMemcpyDeviceToDevice, s));
         run_checksum_reduce(&x->plan, reinterpret_cast<uint32_t*>(d_hash32), s);
     }
-    return SD_OK;
-    SD_GUARD_END
-}
-
-// file_checksum (hash.rs:10-24) for n paths.  Each file is read as the reference reads it:
-// hash.rs's 1 MiB read calls until one returns fewer.  For a regular file those reads are
-// exactly its bytes up to EOF, so regular files are read with parallel preads on the
-// context's stager pool ("read_threads"); anything else (a pipe, a device) with the
-// literal sequential loop.  Small regular files are packed (64-B aligned) into the current
-// slot's pinned window by their stat length -- one batch per window, read in parallel,
-// each file probed past its length in case it grew --; while the GPU hashes one slot's
-// window the host reads the next into the other.  Larger files, files that grew, and
-// non-regular files stream window by window (Streamer), whatever their final length.
-int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65, int32_t* status) {
-    SD_GUARD_BEGIN
-    if (!ctx || (n && (!paths || !out_hex65 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
-    ctx->bind();
-    constexpr uint64_t W = Streamer::W;
-    std::shared_ptr<StagePool> pool = ctx->stage_pool(std::max(1, std::min(64, tuning_get(SD_TUNE_READ_THREADS))));
-    SlotPair slots(ctx);
-    Streamer::prepare(slots);
-    // stat every file in parallel: its length picks the route (regular files only)
-    std::vector<uint64_t> hint(n, 0);
-    std::vector<uint8_t> regular(n, 0);
-    pool->run(n, [&](size_t i) {
-        struct stat st;
-        if (stat(paths[i], &st) == 0 && S_ISREG(st.st_mode)) {
-            hint[i] = (uint64_t)st.st_size;
-            regular[i] = 1;
-        }
-    });
-    struct Pending {
-        std::vector<size_t> files;  // files whose hashes land in this slot's host_hashes
-        bool busy = false;
-    } pend[2];
-    sd_checksum_batch pack_batch[2];
-    // streamed files' hashes arrive when their slot is next synchronised
-    Streamer streamer([&](size_t i, const uint8_t* h) { to_hex(h, 32, out_hex65 + i * 65); });  // hash.rs:21-23
-    int cur = 0;
-    auto harvest = [&](int k) {  // slot k idle: its window is free, its results delivered
-        HIP_CHECK(hipStreamSynchronize(slots[k].stream));
-        streamer.collect(k);
-        if (!pend[k].busy) return;
-        const uint8_t* h = slots[k].host_hashes.u8();
-        for (size_t q = 0; q < pend[k].files.size(); q++)
-            to_hex(h + 32 * q, 32, out_hex65 + pend[k].files[q] * 65);  // hash.rs:21-23
-        pend[k].files.clear();
-        pend[k].busy = false;
-    };
-    // one file streamed (sequential reads, or parallel preads for a regular file); its hash
-    // lands in out_hex65 through the streamer's callback, at a later sync of its slot
-    auto stream_file = [&](size_t i) {
-        const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);  // hash.rs:11
-        if (fd < 0) {
-            status[i] = io_status(errno);
-            return;
-        }
-        struct stat st;
-        const bool reg = fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
-        MsgSource src(fd, MsgSource::CHECKSUM_READS);
-        if (reg) {
-            src.set_parallel(pool.get());
-            src.set_eof_hint((uint64_t)st.st_size);  // a window-multiple file ends with its last window
-        }
-        try {
-            status[i] = streamer.hash_async(slots, cur, src, reg ? (uint64_t)st.st_size : 0, i);
-        } catch (...) {
-            close(fd);
-            throw;
-        }
-        close(fd);
-    };
-    // the pack: regular files laid out by their stat lengths in slot `cur`'s window
-    std::vector<size_t> pack, grew;
-    std::vector<uint64_t> pack_off, pack_len;
-    uint64_t pack_end = 0;
-    auto submit_pack = [&]() {
-        if (pack.empty()) return;
-        const int k = cur;
-        harvest(k);  // slot k's previous batch is done: its window is free
-        Slot& sl = slots[k];
-        uint8_t* win = sl.window.u8();
-        pool->run(pack.size(), [&](size_t q) {
-            const size_t i = pack[q];
-            const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
-            if (fd < 0) {
-                status[i] = io_status(errno);
-                return;
-            }
-            const int64_t got = pread_full(fd, win + pack_off[q], hint[i], 0);
-            uint8_t probe;
-            const int64_t more = got == (int64_t)hint[i] ? pread_full(fd, &probe, 1, hint[i]) : 0;
-            close(fd);
-            if (got < 0 || more < 0) {
-                status[i] = io_status((int)-(got < 0 ? got : more));
-            } else if (more > 0) {
-                status[i] = SD_FILE_CHANGED;  // grew since stat: stream it below
-            } else {
-                status[i] = SD_FILE_OK;
-                pack_len[q] = (uint64_t)got;  // shrank: hash.rs stops at EOF
-                memset(win + pack_off[q] + got, 0, align_up(got, 64) - got);
-            }
-        });
-        std::vector<uint64_t> offs, lens;
-        std::vector<size_t> ok;
-        for (size_t q = 0; q < pack.size(); q++) {
-            if (status[pack[q]] == SD_FILE_OK) {
-                ok.push_back(pack[q]);
-                offs.push_back(pack_off[q]);
-                lens.push_back(pack_len[q]);
-            } else if (status[pack[q]] == SD_FILE_CHANGED) {
-                grew.push_back(pack[q]);
-            }
-        }
-        pack.clear();
-        pack_off.clear();
-        pack_len.clear();
-        const uint64_t span = pack_end;
-        pack_end = 0;
-        if (ok.empty()) return;
-        cur ^= 1;
-        plan_checksum_batch(&pack_batch[k], offs.data(), lens.data(), ok.size(), sl.stream);
-        sl.hashes.ensure(ok.size() * 32);
-        sl.host_hashes.ensure(ok.size() * 32);
-        HIP_CHECK(hipMemcpyAsync(sl.staged.p, win, span + 64, hipMemcpyHostToDevice, sl.stream));
-        run_checksum_batch(&pack_batch[k], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
-        HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, ok.size() * 32, hipMemcpyDeviceToHost, sl.stream));
-        pend[k].files = std::move(ok);
-        pend[k].busy = true;
-    };
-    for (size_t i = 0; i < n; i++) {
-        status[i] = SD_FILE_OK;
-        if (!regular[i] || hint[i] + 128 > W / 2) {  // a pipe / device / unreadable path, or large
-            submit_pack();
-            stream_file(i);
-            continue;
-        }
-        if (pack_end + align_up(hint[i], 64) + 64 > W) submit_pack();
-        pack.push_back(i);
-        pack_off.push_back(pack_end);
-        pack_len.push_back(hint[i]);
-        pack_end = align_up(pack_end + hint[i], 64);
-    }
-    submit_pack();
-    for (size_t i : grew) {
-        status[i] = SD_FILE_OK;
-        stream_file(i);
-    }
-    harvest(0);
-    harvest(1);
-    streamer.finish(slots);
-    return SD_OK;
-    SD_GUARD_END
-}
-
-// Full BLAKE3 of n byte ranges of a host buffer (hash.rs:10-24 on data already in memory):
-// consecutive ranges whose span fits a 256 MiB window are copied with one H2D each and
-// hashed as one batch; a larger range streams window by window into its leaf CVs (known
-// length: one plan), then reduces.  Two slots alternate so copies overlap kernels.
-int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
-                 char* out_hex65) {
-    SD_GUARD_BEGIN
-    if (!ctx || (n && (!data || !offsets || !lens || !out_hex65))) throw sd_failure(SD_ERR_INVALID, "null argument");
-    for (size_t i = 0; i < n; i++)
-        if (offsets[i] % 16) throw sd_failure(SD_ERR_INVALID, "range " + std::to_string(i) + " not 16-byte aligned");
-    ctx->bind();
-    constexpr uint64_t W = Streamer::W;
-    SlotPair slots(ctx);
-    Streamer::prepare(slots);
-    sd_checksum_batch batches[2], big;
-    struct Pending {
-        size_t i0 = 0, i1 = 0;
-        bool busy = false;
-    } pend[2];
-    auto harvest = [&](int k) {
-        if (!pend[k].busy) return;
-        HIP_CHECK(hipStreamSynchronize(slots[k].stream));
-        const uint8_t* h = slots[k].host_hashes.u8();
-        for (size_t i = pend[k].i0; i < pend[k].i1; i++) to_hex(h + 32 * (i - pend[k].i0), 32, out_hex65 + 65 * i);
-        pend[k].busy = false;
-    };
-    // copies on one queue (copy_stream), kernels on the two slots' streams, joined by events:
-    // copied[k] = slot k's window has landed; used[k] = slot k's kernels no longer read it
-    hipStream_t cs = slots.copy_stream();
-    hipEvent_t copied[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
-    bool used_set[2] = {false, false};
-    struct Events {
-        hipEvent_t* e[2];
-        ~Events() {
-            for (auto* p : e)
-                for (int k = 0; k < 2; k++)
-                    if (p[k]) (void)hipEventDestroy(p[k]);
-        }
-    } ev_guard{{copied, used}};
-    for (int k = 0; k < 2; k++) {
-        HIP_CHECK(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&used[k], hipEventDisableTiming));
-    }
-    // H2D of `bytes` from `src` into slot k's device window, after its previous kernels
-    auto copy_in = [&](int k, const uint8_t* src, uint64_t bytes) {
-        if (used_set[k]) HIP_CHECK(hipStreamWaitEvent(cs, used[k], 0));
-        HIP_CHECK(hipMemcpyAsync(slots[k].staged.p, src, bytes, hipMemcpyHostToDevice, cs));
-        HIP_CHECK(hipEventRecord(copied[k], cs));
-        HIP_CHECK(hipStreamWaitEvent(slots[k].stream, copied[k], 0));
-    };
-    auto done_with = [&](int k) {
-        HIP_CHECK(hipEventRecord(used[k], slots[k].stream));
-        used_set[k] = true;
-    };
-    int cur = 0;
-    std::vector<uint64_t> offs, ls;
-    for (size_t i = 0; i < n;) {
-        if (lens[i] + 128 > W) {  // one large range, streamed
-            harvest(0);
-            harvest(1);
-            const uint64_t off0 = 0, L = lens[i];
-            plan_checksum_batch(&big, &off0, &L, 1, nullptr);
-            const uint64_t nb = big.plan.wg_map.size();
-            for (uint64_t pos = 0; pos < L; pos += W) {
-                const int k = cur;
-                cur ^= 1;
-                const uint64_t here = std::min<uint64_t>(W, L - pos);
-                copy_in(k, data + offsets[i] + pos, align_up(here, 64));
-                const uint32_t wg0 = (uint32_t)(pos / SD_CK_BLOCK);
-                const uint32_t wg1 = (uint32_t)std::min<uint64_t>(nb, wg0 + W / SD_CK_BLOCK);
-                HIP_CHECK(sdk::launch_ck_leaf(slots[k].staged.as<uint8_t>(), pos, 0, big.files.as<ck_file>(),
-                                              big.wg_map.as<uint2>() + wg0, wg1 - wg0, big.lvl[0].as<uint32_t>(),
-                                              slots[k].hashes.as<uint32_t>(), slots[k].stream));
-                done_with(k);
-            }
-            slots.sync_all();
-            Slot& sl = slots[0];
-            run_checksum_reduce(&big, sl.hashes.as<uint32_t>(), sl.stream);
-            HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, 32, hipMemcpyDeviceToHost, sl.stream));
-            HIP_CHECK(hipStreamSynchronize(sl.stream));
-            to_hex(sl.host_hashes.u8(), 32, out_hex65 + 65 * i);
-            i++;
-            continue;
-        }
-        // the next window: consecutive ranges whose span fits
-        const uint64_t lo = offsets[i] / 16 * 16;
-        uint64_t hi = 0;
-        size_t j = i;
-        while (j < n && lens[j] + 128 <= W) {
-            const uint64_t nlo = std::min(lo, offsets[j] / 16 * 16);
-            const uint64_t nhi = std::max(hi, align_up(offsets[j] + lens[j], 64));
-            if (j > i && (nlo < lo || nhi - lo > W)) break;
-            hi = nhi;
-            j++;
-        }
-        const int k = cur;
-        cur ^= 1;
-        harvest(k);
-        Slot& sl = slots[k];
-        offs.assign(offsets + i, offsets + j);
-        ls.assign(lens + i, lens + j);
-        for (auto& o : offs) o -= lo;
-        plan_checksum_batch(&batches[k], offs.data(), ls.data(), j - i, sl.stream);
-        sl.hashes.ensure((j - i) * 32);
-        sl.host_hashes.ensure((j - i) * 32);
-        copy_in(k, data + lo, std::max<uint64_t>(hi - lo, 16));
-        run_checksum_batch(&batches[k], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
-        done_with(k);
-        HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, (j - i) * 32, hipMemcpyDeviceToHost, sl.stream));
-        pend[k] = Pending{i, j, true};
-        i = j;
-    }
-    harvest(0);
-    harvest(1);
     return SD_OK;
     SD_GUARD_END
 }
