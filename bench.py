@@ -13,7 +13,7 @@ sort + group, Object owners).  Inputs are resident in HBM before timing (generat
 device from the counter-based generator); PCIe-inclusive rates are reported beside
 `value` ("with_h2d"), never as it.
 
-After the timed steps: configs[3] (full-file checksums of 16 x 4 GiB files) on every
+After the timed steps: configs[3] (full-file checksums of 16 x 4 GiB files, then its mixed 2..8 GiB variant) on every
 rank as `checksum`; on rank 0 at N = 1 the configs[1]/[2] kernel legs, the with-H2D legs
 (cas_ids and checksums from pinned host memory), the file-backed legs (cas_ids and
 checksums from tmpfs beside the reference's read schedule on the CPU), single-call
