@@ -405,13 +405,14 @@ int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged, std::vector<u
     const uint64_t H = SD_HEADER_OR_FOOTER_SIZE, S = SD_SAMPLE_SIZE;
     const uint64_t jump = (size - 2 * H) / SD_SAMPLE_COUNT;
     uint8_t* p = dst + 8;
-    int32_t st = pread_exact(f.fd, p, H, 0);  // :35-38
-    p += H;
-    uint64_t current_pos = H;
-    while (st == SD_FILE_OK) {  // :42-51
+    // :35-38 the header, and the first sample that follows it on disk (current_pos = 8192),
+    // in one read: the two are contiguous, and either falling short is the same UnexpectedEof
+    int32_t st = pread_exact(f.fd, p, H + S, 0);
+    p += H + S;
+    uint64_t current_pos = H + jump;
+    for (int k = 1; k < (int)SD_SAMPLE_COUNT && st == SD_FILE_OK; k++) {  // :42-51
         st = pread_exact(f.fd, p, S, current_pos);
         p += S;
-        if (current_pos >= H + jump * (SD_SAMPLE_COUNT - 1)) break;
         current_pos += jump;
     }
     if (st != SD_FILE_OK) return st;
