@@ -802,6 +802,56 @@ def test_dedup_mgpu_through_rccl_single_rank(ctx, rccl_comm):
     assert ng2 == gng and np.array_equal(r2.cpu().numpy(), gr) and np.array_equal(own2.cpu().numpy(), want_owner)
 
 
+def test_dedup_of_one_batch_beside_the_next_batchs_hashing(ctx, rccl_comm):
+    """The pipelined scan (bench.py steps_pipelined): batch k's
+    sd_cas_dedup_mgpu on one stream while batch k+1 hashes on another, two hash buffers
+    alternating.  Every batch's grouping equals the host grouping of its own hashes."""
+    from spacedrive_amd import dedup
+    from spacedrive_amd.identifier import object_owners
+    n, B = 40000, 4
+    libs = [synth.library(k * n, n, B * n, dup_frac=0.2) for k in range(B)]
+    staged = [stage_synth(ctx, *lib) for lib in libs]
+    batches = [ctx.cas_batch(ext) for ext, _, _ in staged]
+    torch.cuda.synchronize()  # staged before the other streams read it
+    valid = [torch.from_numpy((lib[0] != 0).astype(np.uint8)).cuda() for lib in libs]
+    hs, ds = torch.cuda.Stream(), torch.cuda.Stream()
+    bufs = [torch.zeros(n * 32, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    e_hash = [torch.cuda.Event() for _ in range(2)]
+    e_ded = [torch.cuda.Event() for _ in range(2)]
+    runner = dedup.RcclDedup(ctx, rccl_comm, bufs[0].device, capacity=n + 1024)
+    got, hashes = [], []
+
+    def hash_into(k):
+        b = k & 1
+        if k >= 2:
+            hs.wait_event(e_ded[b])
+        batches[k].run(staged[k][2], bufs[b], hs)
+        e_hash[b].record(hs)
+
+    hash_into(0)
+    for k in range(B):
+        b = k & 1
+        if k + 1 < B:
+            hash_into(k + 1)
+        ds.wait_event(e_hash[b])
+        recs, rep, ng, owner = runner(bufs[b].view(n, 32), valid[k], n, k * n, stream=ds)
+        ds.synchronize()
+        got.append((recs.cpu().numpy(), rep.cpu().numpy(), ng, owner.cpu().numpy()))
+        hashes.append(bufs[b].cpu().numpy().reshape(n, 32))  # still batch k's: batch k+2 waits for e_ded
+        e_ded[b].record(ds)
+    torch.cuda.synchronize()
+    for k in range(B):
+        h = hashes[k]
+        assert np.array_equal(h, gpu_cas(ctx, *libs[k]))
+        ok = libs[k][0] != 0
+        gr, grep, gng = group_host(np.stack([keys_from_hashes(h)[ok].view(np.int64),
+                                             np.arange(k * n, (k + 1) * n)[ok]], axis=1))
+        recs, rep, ng, owner = got[k]
+        assert ng == gng and np.array_equal(recs, gr) and np.array_equal(rep, grep)
+        want_owner = object_owners(torch.from_numpy(gr[:, 1].copy()), torch.from_numpy(grep), 100).numpy()
+        assert np.array_equal(owner, want_owner)
+
+
 def test_checksums_from_host_memory(ctx, oracle_native):
     """sd_checksums: ranges of a host buffer (pinned) -> hex, packed windows and a range
     larger than a window (streamed with a known length), against the oracle."""
