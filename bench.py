@@ -50,7 +50,8 @@ PEAK_BASIS = ("3-operand VALU issue bound (probe): 256 CU x 64 lane-ops/clk x 2.
               "v_add3/v_alignbit-heavy; 3-source ops issue at half the 2-source rate (profiles/r1c_valu_probe.txt). "
               "frac_full_rate is against the guide's SIMD-32 full rate, 256 CU x 128 lane-ops/clk x 2.4 GHz = 78.6 T")
 SAMPLED_MSG = 57352
-S_FILES_PER_WG, S_THREADS = 16, 448  # k_cas_sampled launch shape (cas_kernels.hip)
+S_LANES_PER_FILE = 7  # k_cas_sampled_lanes: one 256-lane grid slot per 8-chunk group (cas_kernels.hip)
+SAMPLED_KERNELS = ["k_cas_sampled_lanes", "k_cas_sampled_merge"]
 
 
 def log(*a):
@@ -113,8 +114,18 @@ def pmc_traffic(kernel: str, grid: int):
     return None
 
 
-def sampled_grid(n_sampled: int) -> int:
-    return (n_sampled + S_FILES_PER_WG - 1) // S_FILES_PER_WG * S_THREADS
+def sampled_grids(n_sampled: int) -> list:
+    """work-items of the two sampled launches: lanes (7 per file), merge (1 per file)"""
+    return [(n_sampled * S_LANES_PER_FILE + 255) // 256 * 256, (n_sampled + 255) // 256 * 256]
+
+
+def pmc_traffic_sum(kernels, grids):
+    """pmc_traffic summed over launches that run as one unit; None unless every one is measured"""
+    parts = [pmc_traffic(k, g) for k, g in zip(kernels, grids)]
+    if not all(parts):
+        return None
+    return {"bytes": sum(p["bytes"] for p in parts), "tag": parts[0]["tag"], "grid": list(grids),
+            "fetch_factor": parts[0]["fetch_factor"], "per_kernel": {k: p["bytes"] for k, p in zip(kernels, parts)}}
 
 
 def whole_grid(batch) -> int:
@@ -310,9 +321,12 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
     ms = ev_ms(lambda: b.run(d_staged, h1, stream), stream, reps=reps)
     deterministic = bool(torch.equal(h0, h1))
     roof = valu_roof(b.compressions, ms)
-    kernels = ["k_cas_sampled"] if which == "sampled" else ["k_whole_items", "k_whole_merge8"]
-    grid = sampled_grid(b.n_sampled) if which == "sampled" else whole_grid(b)
-    tr = pmc_traffic(kernels[0], grid)
+    if which == "sampled":
+        kernels, grid = SAMPLED_KERNELS, sampled_grids(b.n_sampled)
+        tr = pmc_traffic_sum(kernels, grid)
+    else:
+        kernels, grid = ["k_whole_items", "k_whole_merge8"], whole_grid(b)
+        tr = pmc_traffic(kernels[0], grid)
     res = {"workload": ("configs[1]: 1M files <= 100 KiB, whole-content cas_id (log-uniform sizes 1..102400)"
                         if which == "small" else
                         "configs[2]: 1M files > 100 KiB, sampled cas_id (log-uniform sizes 102401..4 GiB)"),
@@ -690,7 +704,7 @@ def main():
     def step(k=None):
         if k is not None:
             ev[k][0].record(stream)
-        batch.run_part(1, d_staged, d_hash, stream)  # k_cas_sampled, timed on its own
+        batch.run_part(1, d_staged, d_hash, stream)  # the sampled kernels, timed on their own
         if k is not None:
             ev[k][1].record(stream)
         batch.run_part(2, d_staged, d_hash, stream)  # k_whole_items + 2 x k_whole_merge8
@@ -762,7 +776,7 @@ def main():
                 hs.wait_event(e_ded[b])
             if k is not None:
                 pev[k][0].record(hs)
-            batch.run_part(1, d_staged, d_hash2[b], hs)  # k_cas_sampled, timed on its own
+            batch.run_part(1, d_staged, d_hash2[b], hs)  # the sampled kernels, timed on their own
             if k is not None:
                 pev[k][1].record(hs)
             batch.run_part(2, d_staged, d_hash2[b], hs)
@@ -813,7 +827,8 @@ def main():
         # the roofline comes from the timed region that gives `value`: these steps' own events
         sampled_ms, hash_ms = p_sampled, p_hash
 
-    # roofline of the dominant kernel, k_cas_sampled (81 % of the shard's compressions),
+    # roofline of the dominant kernels, the sampled pair k_cas_sampled_lanes + _merge (81 % of
+    # the shard's compressions, one unit: the merge finishes what the lanes kernel starts),
     # timed on its own with HIP events on its launch stream: 953 compressions x 672 VALU
     # lane-ops per sampled file; bytes = 57 352 B message read + 32 B hash written per file
     valu_peak = ctx.valu_peak()
@@ -823,8 +838,8 @@ def main():
     dom_gbps = dom_bytes / (sampled_ms * 1e-3) / 1e9
     hash_bytes = batch.msg_bytes + 32 * n
     phase_roof = valu_roof(batch.compressions, hash_ms)
-    s_grid, w_grid = sampled_grid(batch.n_sampled), whole_grid(batch)
-    tr = pmc_traffic("k_cas_sampled", s_grid)
+    s_grid, w_grid = sampled_grids(batch.n_sampled), whole_grid(batch)
+    tr = pmc_traffic_sum(SAMPLED_KERNELS, s_grid)
     tr_w = pmc_traffic("k_whole_items", w_grid)
     out = {
         "metric": "cas_id files/sec (10M synthetic files) + checksum GB/s at 1/2/4/8 MI355X",
@@ -839,7 +854,7 @@ def main():
                      "unit": "T int32 VALU lane-ops/s", "frac": dom["frac"], "peak_basis": PEAK_BASIS,
                      "peak_full_rate": VALU_FULL_RATE_TOPS, "frac_full_rate": dom["frac_full_rate"],
                      "traffic": tr["bytes"] if tr else None, "traffic_source": tr,
-                     "kernel": "k_cas_sampled", "kernel_ms": sampled_ms, "launch_grid": s_grid,
+                     "kernel": " + ".join(SAMPLED_KERNELS), "kernel_ms": sampled_ms, "launch_grid": s_grid,
                      "kernel_events": "steps_pipelined" if pipelined else "steps_serial",
                      "algorithmic": {"compressions_per_launch": dom_comp, "lane_ops_per_compression": 672,
                                      "bytes_per_launch": dom_bytes,
@@ -848,7 +863,7 @@ def main():
                      "frac_of_measured_peak": dom["achieved"] * 1e12 / valu_peak if valu_peak else None,
                      "hbm": {"achieved": dom_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                              "frac": dom_gbps / HBM_PEAK_GBPS},
-                     "phase": {"kernels": ["k_cas_sampled", "k_whole_items", "k_whole_merge8"], "ms": hash_ms,
+                     "phase": {"kernels": SAMPLED_KERNELS + ["k_whole_items", "k_whole_merge8"], "ms": hash_ms,
                                "compressions": batch.compressions, "bytes": hash_bytes,
                                "achieved": phase_roof["achieved"], "frac": phase_roof["frac"],
                                "frac_full_rate": phase_roof["frac_full_rate"],

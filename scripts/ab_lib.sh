@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of two builds of libsdcas on the bench step: A = ab/libsdcas_old.so (the
 # previous build), B = the in-tree library, alternated ABABAB so both see the same box and
-# clock history.  Prints k_cas_sampled / whole / step ms per run.
+# clock history.  Prints sampled / whole / step ms per run.
 set -u
 mkdir -p gpurun_out
 for r in 1 2 3; do

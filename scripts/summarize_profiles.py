@@ -94,9 +94,9 @@ def main(tag):
                 if short(r["Kernel_Name"]) == "k_read_probe" and r["Counter_Name"] == "FETCH_SIZE"]
         for pattern, v in zip((0, 1, 2), vals):
             calib[pattern] = CALIB_BYTES / (v * 1024)
-    # k_cas_sampled / k_whole_items full pairs read 2 KiB per lane (probe pattern 2); the
-    # checksum leaf 4 KiB per lane in the same 16 B x 4 per block shape (pattern 2)
-    use = {"k_cas_sampled": 2, "k_whole_items": 2, "k_ck_leaf": 2}
+    # k_cas_sampled_lanes (8 KiB per lane) / k_whole_items full pairs (2 KiB per lane) read in
+    # line pairs (probe pattern 2); the checksum leaf 4 KiB per lane in the same shape
+    use = {"k_cas_sampled_lanes": 2, "k_cas_sampled": 2, "k_whole_items": 2, "k_ck_leaf": 2}
     kern = {}
     for (k, grid), cs in sorted(pmc.items()):
         if "FETCH_SIZE" not in cs:

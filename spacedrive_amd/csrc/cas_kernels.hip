@@ -1,9 +1,9 @@
 // cas_kernels.hip -- gfx950 kernels for Spacedrive's content-addressing hot path.
 //
-//   k_cas_sampled   generate_cas_id, size > 102400 (cas.rs:30-58): every message is the
-//                   same 57 352 B = 56 full chunks + one 8-byte chunk, so a workgroup of
-//                   7 waves hashes 16 files with one lane per aligned chunk pair and merges
-//                   the 16 x 29 chaining values level-wise in LDS.  No work lists.
+//   k_cas_sampled_lanes  generate_cas_id, size > 102400 (cas.rs:30-58): every message is
+//   k_cas_sampled_merge  the same 57 352 B = 56 full chunks + one 8-byte chunk, so one lane
+//                   per aligned 8-chunk group (7 per file) hashes its subtree, and one lane
+//                   per file merges the 7 subtree CVs and the tail chunk.  No work lists.
 //   k_whole_items   generate_cas_id, size <= 102400 (cas.rs:27-29): host-built work lists
 //   k_whole_merge8  of aligned chunk pairs (full pairs of multi-pair messages, then the
 //                   cost-sorted partial / short pairs), then two level-wise merge passes of
@@ -66,77 +66,125 @@ __device__ void lds_reduce(uint32_t (*lds)[8], uint32_t n, bool root) {
 }  // namespace
 
 // ------------------------------------------------------------------------ sampled cas
-// 448 lanes = 7 waves.  Each lane hashes U = 2 consecutive full chunks of one file (an
-// aligned pair, line-pair loads) and merges them in-lane, so a workgroup covers 16 files.
-// Per file the 28 lane CVs plus the 8-byte tail chunk (node 28, message bytes
-// 57344..57351) are merged level-wise in LDS; the tail is hashed during the first level
-// by lanes that have no parent to compute (the first level always has 224 parents, and
-// an odd node count, so the tail is the carried node).
+// Every sampled message is the same 57 352 B = 56 full chunks + one 8-byte chunk (message
+// bytes 57344..57351, chunk 56), so the launch shape needs no work lists:
 constexpr int S_FULL = 56;  // full chunks per sampled message (57344 bytes)
-constexpr int S_THREADS = 448;
-constexpr int S_U = 2;                    // chunks per lane
-constexpr int S_LANES = S_FULL / S_U;     // lanes per file (28)
-constexpr int S_F = S_THREADS / S_LANES;  // files per workgroup (16)
-constexpr int S_N0 = S_LANES + 1;         // nodes per file entering the tree (29)
+#ifndef SD_SAMPLED_LANE_CHUNKS
+#define SD_SAMPLED_LANE_CHUNKS 8  // chunks per lane (2, 4 or 8; scripts/sampled_ab.py)
+#endif
+constexpr int S_U = SD_SAMPLED_LANE_CHUNKS;
+constexpr int S_K = S_FULL / S_U;  // nodes per file after the lanes kernel (7)
+static_assert(S_U == 2 || S_U == 4 || S_U == 8, "chunks per lane");
 
-__global__ __launch_bounds__(S_THREADS) void k_cas_sampled(const uint8_t* __restrict__ staged,
+// Two kernels, and no in-workgroup tree phase (round 2 measured a one-kernel design -- 16
+// files per 7-wave workgroup, the 29 lane CVs of each merged level-wise in LDS -- 3.4%
+// slower: the LDS rounds, barriers and partly-filled waves of its tree phase cost more than
+// a second launch; profiles/r2/r2z_sampled_ab.json):
+//   k_cas_sampled_lanes<U>  one lane per (file, aligned group of U chunks): 56/U lanes per
+//                           file, 256-lane workgroups, no LDS, no barrier; the group's
+//                           subtree CV -> node row j of the file, rows stored node-major
+//                           (row (j, f) at (j * n + f) * 32 B) so the merge reads coalesce;
+//   k_cas_sampled_merge<U>  one lane per file: the 56/U node CVs merged with BLAKE3's CV
+//                           stack, then the 8-byte tail chunk (chunk 56) and the stack folded
+//                           into the root.
+// CvStack: the pending subtree CVs, top first, in registers with static indices only (a
+// push shifts every entry down one slot), so a loop that is not unrolled can drive it.
+template <int D>
+struct CvStack {
+    uint32_t s[D][8];
+    __device__ __forceinline__ void push(const uint32_t (&c)[8]) {
+#pragma unroll
+        for (int d = D - 1; d > 0; d--)
+#pragma unroll
+            for (int i = 0; i < 8; i++) s[d][i] = s[d - 1][i];
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[0][i] = c[i];
+    }
+    // c <- parent(top, c), and the top popped
+    __device__ __forceinline__ void merge_top(uint32_t (&c)[8], uint32_t flags) {
+        uint32_t r[8];
+        parent(r, s[0], c, flags);
+#pragma unroll
+        for (int i = 0; i < 8; i++) c[i] = r[i];
+#pragma unroll
+        for (int d = 0; d + 1 < D; d++)
+#pragma unroll
+            for (int i = 0; i < 8; i++) s[d][i] = s[d + 1][i];
+    }
+};
+
+constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
+
+// CV of U (a power of two) consecutive full non-root chunks c0.. : U = 2 is full_chunks_cv's
+// unrolled pair; larger groups merge each chunk into the stack as it completes.
+template <int U>
+__device__ __forceinline__ void group_cv(uint32_t (&out)[8], const uint8_t* __restrict__ p, uint64_t c0) {
+    if constexpr (U <= 2) {
+        full_chunks_cv<U>(out, p, c0);
+    } else {
+        CvStack<ilog2(U)> st;
+        uint32_t ma[16], mb[16];
+#pragma unroll 1
+        for (uint32_t u = 0; u < (uint32_t)U; u++) {
+            const uint64_t ctr = c0 + u;
+            const uint32_t clo = (uint32_t)ctr, chi = (uint32_t)(ctr >> 32);
+            const uint8_t* q = p + (size_t)u * CHUNK_LEN;
+            set_iv(out);
+#pragma unroll 1
+            for (uint32_t b = 0; b < 16; b += 2) {
+                load_block(ma, q + 64u * b);
+                load_block(mb, q + 64u * (b + 1));
+                compress(out, ma, clo, chi, BLOCK_LEN, b == 0 ? CHUNK_START : 0u);
+                compress(out, mb, clo, chi, BLOCK_LEN, b + 1 == 15 ? CHUNK_END : 0u);
+            }
+#pragma unroll 1
+            for (uint32_t t = u + 1; (t & 1u) == 0; t >>= 1) st.merge_top(out, 0u);
+            if (u + 1 < (uint32_t)U) st.push(out);
+        }
+    }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_cas_sampled_lanes(const uint8_t* __restrict__ staged,
+                                                           const uint64_t* __restrict__ soff, uint32_t n,
+                                                           uint32_t* __restrict__ rows) {
+    constexpr uint32_t K = S_FULL / U;
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (uint64_t)n * K) return;
+    const uint32_t f = (uint32_t)(g / K), j = (uint32_t)(g - (uint64_t)f * K);
+    uint32_t cv[8];
+    group_cv<U>(cv, staged + soff[f] + (size_t)j * U * CHUNK_LEN, (uint64_t)j * U);
+    store_cv(rows + ((size_t)j * n + f) * 8, cv);
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_cas_sampled_merge(const uint8_t* __restrict__ staged,
                                                            const uint64_t* __restrict__ soff,
                                                            const uint32_t* __restrict__ idx, uint32_t n,
-                                                           uint32_t* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint32_t cvs[S_F][S_N0][8];
-    const uint32_t t = threadIdx.x, wg = blockIdx.x;
-    {
-        const uint32_t f = t / S_LANES, j = t % S_LANES;
-        const uint32_t g = wg * S_F + f;
-        if (g < n) {
-            const uint8_t* msg = staged + soff[g];  // one load, not idx -> extent -> offset
-            uint32_t cv[8];
-            full_chunks_cv<S_U>(cv, msg + (size_t)j * S_U * CHUNK_LEN, (uint64_t)j * S_U);
-            store_cv(cvs[f][j], cv);
-        }
-    }
-    __syncthreads();
-    uint32_t nodes = S_N0;
+                                                           const uint32_t* __restrict__ rows, uint32_t* __restrict__ out) {
+    constexpr uint32_t K = S_FULL / U;
+    constexpr int D = ilog2(K + 1);  // after node k the stack holds popcount(k + 1) subtrees
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n) return;
+    CvStack<D> st;
+    uint32_t cur[8], nxt[8];
+    load_cv(nxt, rows + (size_t)f * 8);
 #pragma unroll 1
-    for (int level = 0; nodes > 1; level++) {
-        const uint32_t P = nodes >> 1;
-        const bool carry = nodes & 1u;
-        uint32_t res[8];
-        bool have = false;
-        uint32_t ff = 0, p = 0;
-        if (t < S_F * P) {
-            ff = t / P; p = t % P;
-            uint32_t l[8], r[8];
-            load_cv(l, cvs[ff][2 * p]);
-            load_cv(r, cvs[ff][2 * p + 1]);
-            parent(res, l, r, nodes == 2 ? ROOT : 0u);
-            have = true;
-        } else if (carry) {
-            if (level == 0) {  // lanes [224, 240): the tail chunk (8 bytes, chunk index 56)
-                const uint32_t gt = wg * S_F + (t - S_F * P);
-                if (t < S_F * P + S_F && gt < n) {
-                    ff = t - S_F * P; p = P;
-                    const uint8_t* msg = staged + soff[gt];
-                    chunk_cv(res, msg + (size_t)S_FULL * CHUNK_LEN, SD_SAMPLED_MSG_LEN - S_FULL * CHUNK_LEN, S_FULL,
-                             false);
-                    have = true;
-                }
-            } else if (t >= 256 && t < 256 + S_F) {  // a wave with no parent work carries the odd node
-                ff = t - 256; p = P;
-                load_cv(res, cvs[ff][nodes - 1]);
-                have = true;
-            }
-        }
-        __syncthreads();
-        if (have) store_cv(cvs[ff][p], res);
-        __syncthreads();
-        nodes = P + (carry ? 1u : 0u);
+    for (uint32_t k = 0; k < K; k++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) cur[i] = nxt[i];
+        if (k + 1 < K) load_cv(nxt, rows + ((size_t)(k + 1) * n + f) * 8);  // in flight during the merges
+#pragma unroll 1
+        for (uint32_t t = k + 1; (t & 1u) == 0; t >>= 1) st.merge_top(cur, 0u);
+        st.push(cur);
     }
-    if (t < S_F * 8) {
-        const uint32_t ff = t >> 3, w = t & 7;
-        const uint32_t gg = wg * S_F + ff;
-        if (gg < n) out[(size_t)idx[gg] * 8 + w] = cvs[ff][0][w];
-    }
+    // the tail chunk is the rightmost node; the stack's subtrees fold onto it, ROOT last
+    chunk_cv(cur, staged + soff[f] + (size_t)S_FULL * CHUNK_LEN, SD_SAMPLED_MSG_LEN - S_FULL * CHUNK_LEN, S_FULL,
+             false);
+    constexpr int P = __builtin_popcount(K);  // subtrees on the stack after K nodes
+#pragma unroll 1
+    for (int d = 0; d < P; d++) st.merge_top(cur, d + 1 == P ? ROOT : 0u);
+    store_cv(out + (size_t)idx[f] * 8, cur);
 }
 
 // ------------------------------------------------------------------ whole-file cas
@@ -322,10 +370,15 @@ __global__ __launch_bounds__(256) void k_ck_reduce(const uint32_t* __restrict__ 
 // --------------------------------------------------------------------- launchers
 namespace sdk {
 
+uint64_t cas_sampled_rows_bytes(uint32_t n) { return (uint64_t)n * S_K * 32; }
+
+// rows >= cas_sampled_rows_bytes(n)
 hipError_t launch_cas_sampled(const uint8_t* staged, const uint64_t* soff, const uint32_t* idx, uint32_t n,
-                              uint32_t* out, hipStream_t s) {
+                              uint32_t* rows, uint32_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_cas_sampled, dim3((n + S_F - 1) / S_F), dim3(S_THREADS), 0, s, staged, soff, idx, n, out);
+    const uint32_t lanes_wg = (uint32_t)(((uint64_t)n * S_K + 255) / 256), merge_wg = (n + 255) / 256;
+    hipLaunchKernelGGL(k_cas_sampled_lanes<S_U>, dim3(lanes_wg), dim3(256), 0, s, staged, soff, n, rows);
+    hipLaunchKernelGGL(k_cas_sampled_merge<S_U>, dim3(merge_wg), dim3(256), 0, s, staged, soff, idx, n, rows, out);
     return hipGetLastError();
 }
 

@@ -203,6 +203,7 @@ struct sd_cas_batch {
     uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0, whole_chunks = 0;
     WholePlan whole;  // work lists (kernel formats in cas_kernels.hip, k_whole_items / _merge8)
     sdi::DevBuf ext, sidx, soff, full_items, tail_items, merge_a, merge_b, cvbuf, cv2;
+    sdi::DevBuf srows;  // the sampled files' node CVs between the two sampled kernels
     // whole-file messages longer than SD_WHOLE_ITEMS_MAX: a checksum sub-batch over their
     // byte ranges, its hashes scattered to out[long_idx[i]]
     sd_checksum_batch lng;

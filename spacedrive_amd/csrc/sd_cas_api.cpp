@@ -113,6 +113,7 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
     b->merge_b.upload(b->whole.merge_b, stream);
     b->cvbuf.ensure((size_t)b->whole.n_cv * 32);
     b->cv2.ensure((size_t)b->whole.n_cv2 * 32);
+    b->srows.ensure(sdk::cas_sampled_rows_bytes(b->n_sampled));
     if (b->n_long) {
         plan_checksum_batch(&b->lng, loff.data(), llen.data(), b->n_long, stream);
         b->compressions += b->lng.plan.compressions;
@@ -124,8 +125,8 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
 void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_hash32, hipStream_t s, int parts) {
     uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
     if (parts & SD_PART_SAMPLED)
-        HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->soff.as<uint64_t>(), b->sidx.as<uint32_t>(), b->n_sampled, out,
-                                          s));
+        HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->soff.as<uint64_t>(), b->sidx.as<uint32_t>(), b->n_sampled,
+                                          b->srows.as<uint32_t>(), out, s));
     if (parts & SD_PART_WHOLE) {
         const WholePlan& w = b->whole;
         HIP_CHECK(sdk::launch_whole_items(d_staged, b->full_items.as<uint4>(), (uint32_t)w.full.size(),

@@ -617,7 +617,8 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
                 const int k = cur;
                 cur ^= 1;
                 const uint64_t here = std::min<uint64_t>(W, L - pos);
-                copy_in(k, data + offsets[i] + pos, align_up(here, 64));
+                copy_in(k, data + offsets[i] + pos, here);  // exactly the range's bytes: the
+                // kernels mask past a message's end, so nothing past it is read from `data`
                 const uint32_t wg0 = (uint32_t)(pos / SD_CK_BLOCK);
                 const uint32_t wg1 = (uint32_t)std::min<uint64_t>(nb, wg0 + W / SD_CK_BLOCK);
                 HIP_CHECK(sdk::launch_ck_leaf(slots[k].staged.as<uint8_t>(), pos, 0, big.files.as<ck_file>(),
@@ -635,14 +636,14 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
             continue;
         }
         // the next window: consecutive ranges whose span fits
-        const uint64_t lo = offsets[i] / 16 * 16;
-        uint64_t hi = 0;
+        const uint64_t lo = offsets[i];
+        uint64_t hi = 0, end = lo;  // hi: the window's padded span; end: its last byte + 1
         size_t j = i;
         while (j < n && lens[j] + 128 <= W) {
-            const uint64_t nlo = std::min(lo, offsets[j] / 16 * 16);
             const uint64_t nhi = std::max(hi, align_up(offsets[j] + lens[j], 64));
-            if (j > i && (nlo < lo || nhi - lo > W)) break;
+            if (j > i && (offsets[j] < lo || nhi - lo > W)) break;
             hi = nhi;
+            end = std::max(end, offsets[j] + lens[j]);
             j++;
         }
         const int k = cur;
@@ -655,7 +656,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         plan_checksum_batch(&batches[k], offs.data(), ls.data(), j - i, sl.stream);
         sl.hashes.ensure((j - i) * 32);
         sl.host_hashes.ensure((j - i) * 32);
-        copy_in(k, data + lo, std::max<uint64_t>(hi - lo, 16));
+        copy_in(k, data + lo, end - lo);  // not past the last range: `data` may end there
         run_checksum_batch(&batches[k], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
         done_with(k);
         HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, (j - i) * 32, hipMemcpyDeviceToHost, sl.stream));

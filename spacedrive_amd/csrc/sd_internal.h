@@ -15,8 +15,10 @@ void dedup_group_owners(sd_cas_ctx* ctx, uint64_t* d_records, uint64_t m, int fl
 const SplitPlan& sd_split_plan_of(const sd_split_checksum* x);
 namespace sdk {
 // soff[i] = msg_offset of sampled file i, idx[i] = its index in the batch (the output slot)
+// sampled cas (two kernels: lanes of 8 chunks, then the per-file merge) through `rows`
+uint64_t cas_sampled_rows_bytes(uint32_t n);
 hipError_t launch_cas_sampled(const uint8_t* staged, const uint64_t* soff, const uint32_t* idx, uint32_t n,
-                              uint32_t* out, hipStream_t s);
+                              uint32_t* rows, uint32_t* out, hipStream_t s);
 // whole-file work lists: full-pair items, cost-sorted tail items, two merge8 passes (cv2 =
 // pass-A output)
 hipError_t launch_whole_items(const uint8_t* staged, const uint4* full, uint32_t n_full, const uint4* tail,

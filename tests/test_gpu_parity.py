@@ -189,8 +189,9 @@ def test_cas_configs0_full_size_and_idempotent(ctx, oracle_native):
 
 
 def test_cas_sampled_batch_shapes(ctx, oracle_native):
-    # k_cas_sampled covers 16 files per workgroup: partial last workgroups are bit-exact
-    for n in (1, 7, 15, 16, 17, 31, 32, 33, 65, 1000):
+    # k_cas_sampled_lanes: 7 lanes per file in 256-lane workgroups (files straddle them);
+    # k_cas_sampled_merge: one lane per file -- partial last workgroups of both are bit-exact
+    for n in (1, 7, 15, 16, 17, 31, 32, 33, 36, 37, 65, 255, 256, 257, 1000):
         sizes = np.full(n, 200001, np.uint64) + np.arange(n, dtype=np.uint64) * 4099
         cids = np.arange(n, dtype=np.uint64) + 22
         h = gpu_cas(ctx, sizes, cids, np.zeros(n, np.uint32))
@@ -879,6 +880,47 @@ def test_checksums_from_host_memory(ctx, oracle_native):
     raw = out.raw  # one copy of the buffer
     for i in range(len(lens)):
         assert raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), lens[i]
+
+
+def test_checksums_host_ranges_end_at_a_guard_page(ctx, oracle_native):
+    """sd_checksums reads no byte past a range: pageable buffers whose last range ends at
+    an unreadable (PROT_NONE) page, through the packed window and the streamed (> 256 MiB)
+    route.  The last range starts 16-byte aligned and ends 16 bytes past a 64-byte boundary,
+    so reading up to the next 64-byte boundary (the old window copy) would fault."""
+    import ctypes
+    import mmap
+    from spacedrive_amd._native import check, lib
+    page = mmap.PAGESIZE
+    for lens in ([3, 1000, 4096 + 16], [(300 << 20) + 16]):
+        offs, off = [], 0
+        for L in lens:
+            off = (off + 15) // 16 * 16
+            offs.append(off)
+            off += L
+        span = off
+        npages = (span + page - 1) // page
+        m = mmap.mmap(-1, (npages + 1) * page)  # the data, then the guard page
+        whole = np.frombuffer(m, dtype=np.uint8)
+        base = whole.ctypes.data
+        start = base + npages * page - span     # the last range ends at the guard page
+        assert start % 16 == 0
+        data = whole[npages * page - span:npages * page]
+        rng = np.random.default_rng(len(lens))
+        data[:] = rng.integers(0, 256, span, dtype=np.uint8)
+        padded = np.concatenate([data, np.zeros(128, np.uint8)])  # the oracle's own copy
+        libc = ctypes.CDLL(None, use_errno=True)
+        assert libc.mprotect(ctypes.c_void_p(base + npages * page), page, 0) == 0  # PROT_NONE
+        arr_o = np.array(offs, np.uint64)
+        arr_l = np.array(lens, np.uint64)
+        out = ctypes.create_string_buffer(65 * len(lens))
+        check(lib().sd_checksums(ctx.handle, start, arr_o.ctypes.data, arr_l.ctypes.data, len(lens), out))
+        want = oracle_native.checksums_simd(padded, arr_o, arr_l, nthreads=NT)
+        raw = out.raw
+        for i in range(len(lens)):
+            assert raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), lens[i]
+        assert libc.mprotect(ctypes.c_void_p(base + npages * page), page, 3) == 0  # back to RW
+        del data, whole
+        m.close()
 
 
 def test_split_checksum_ranks_on_one_gpu(ctx, oracle_native):
