@@ -233,8 +233,10 @@ __global__ __launch_bounds__(256) void k_whole_items(const uint8_t* __restrict__
 }
 
 // Item = (first node slot in src, m | root << 31, dst slot or file): merges nodes
-// src[first .. first + m), m in 1..8, an aligned group of one file's node list, level-wise
-// with the odd node carried up; ROOT on the final parent when the group is the whole file.
+// src[first .. first + m), m in 1..8, an aligned group of one file's node list (every node
+// but the last a full subtree of one size), into one CV with BLAKE3's CV stack: each node
+// merges into the stack as it arrives (the next node's load in flight meanwhile), then the
+// stack folds from the top.  ROOT on the final parent when the group is the whole file.
 // Two passes (<= 8 pair nodes, then <= 8 of those) cover messages of up to 128 chunks.
 __global__ __launch_bounds__(256) void k_whole_merge8(const uint4* __restrict__ items, uint32_t n,
                                                       const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
@@ -244,28 +246,27 @@ __global__ __launch_bounds__(256) void k_whole_merge8(const uint4* __restrict__ 
     const uint4 it = items[g];
     const uint32_t m = it.y & 0xFu;
     const bool root = (it.y >> 31) != 0u;
-    uint32_t v[8][8];
+    const bool pow2 = (m & (m - 1u)) == 0u;
+    CvStack<3> st;  // after node i it holds popcount(i + 1) <= 3 subtrees
+    uint32_t cur[8], nxt[8];
+    load_cv(nxt, src + (size_t)it.x * 8);
+    uint32_t depth = 0;
+#pragma unroll 1
+    for (uint32_t i = 0; i < m; i++) {
 #pragma unroll
-    for (int i = 0; i < 8; i++)
-        if ((uint32_t)i < m) load_cv(v[i], src + (size_t)(it.x + i) * 8);
-    uint32_t nn = m;
-#pragma unroll
-    for (int lvl = 0; lvl < 3; lvl++) {
-#pragma unroll
-        for (int q = 0; q < (4 >> lvl); q++) {
-            if ((uint32_t)(2 * q + 1) < nn) {
-                uint32_t t[8];
-                parent(t, v[2 * q], v[2 * q + 1], (root && nn == 2) ? ROOT : 0u);
-#pragma unroll
-                for (int i = 0; i < 8; i++) v[q][i] = t[i];
-            } else if ((uint32_t)(2 * q) < nn) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) v[q][i] = v[2 * q][i];
-            }
+        for (int k = 0; k < 8; k++) cur[k] = nxt[k];
+        if (i + 1 < m) load_cv(nxt, src + (size_t)(it.x + i + 1) * 8);
+#pragma unroll 1
+        for (uint32_t t = i + 1; (t & 1u) == 0; t >>= 1, depth--)  // a power-of-two group ends here
+            st.merge_top(cur, (root && pow2 && i + 1 == m && t == 2) ? ROOT : 0u);
+        if (i + 1 < m) {
+            st.push(cur);
+            depth++;
         }
-        nn = (nn + 1) >> 1;
     }
-    store_cv((root ? out : dst) + (size_t)it.z * 8, v[0]);
+#pragma unroll 1
+    for (; depth > 0; depth--) st.merge_top(cur, (root && depth == 1) ? ROOT : 0u);
+    store_cv((root ? out : dst) + (size_t)it.z * 8, cur);
 }
 
 // 32-byte hash rows src[i] -> out[idx[i]] (whole-file cas messages hashed by the checksum

@@ -84,6 +84,38 @@ def test_tree_shapes_equal():
         assert _blocked_shape(n, 1024) == _level_shape(n), n
 
 
+def _eager_fold(nodes, tail=None):
+    # k_cas_sampled_merge / k_whole_merge8 (cas_kernels.hip): each node merges into a CV
+    # stack as it arrives (while (i + 1) is even), the last node stays out of the stack
+    # unless a tail follows, then the stack folds onto it from the top
+    st, cur = [], None
+    for i, nd in enumerate(nodes):
+        cur, t = nd, i + 1
+        while t % 2 == 0:
+            cur, t = (st.pop(), cur), t // 2
+        if tail is not None or i + 1 < len(nodes):
+            st.append(cur)
+    if tail is not None:
+        cur = tail
+    while st:
+        cur = (st.pop(), cur)
+    return cur
+
+
+def test_kernel_stack_merges_equal_spec_tree():
+    # the sampled pair: 56 full chunks in groups of U (lanes kernel, level-wise in-lane),
+    # then the merge kernel folds the 56/U group CVs and the tail chunk 56
+    for u in (2, 4, 8):
+        groups = [_level_shape_range(s, s + u) for s in range(0, 56, u)]
+        assert _eager_fold(groups, tail=56) == _stack_shape(57), u
+    # whole-file messages of 1..128 chunks: pair nodes, merge8 pass A over aligned groups
+    # of <= 8 pairs, pass B over <= 8 of those
+    for n in range(1, 129):
+        pairs = [_level_shape_range(s, min(s + 2, n)) for s in range(0, n, 2)]
+        a = [_eager_fold(pairs[s:s + 8]) for s in range(0, len(pairs), 8)]
+        assert _eager_fold(a) == _stack_shape(n), n
+
+
 def test_levelwise_hash_matches_spec():
     for n in (0, 1, 64, 65, 1024, 1025, 3 * 1024 + 7, 8 * 1024, 9 * 1024 + 1):
         assert b3.levelwise_hash(pat(n)) == b3.blake3(pat(n)), n
