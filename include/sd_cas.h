@@ -164,12 +164,16 @@ int sd_cas_hashes_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_
 int sd_cas_batch_create(sd_cas_ctx* ctx, const sd_extent* extents, size_t n, sd_cas_batch** out);
 void sd_cas_batch_destroy(sd_cas_batch* batch);
 /* Enqueue the hashing of a prepared batch: d_staged (device, >= staged size) ->
- * d_hash32 (device, n x 32 bytes: the full BLAKE3 hash; the cas_id is its first 8). */
+ * d_hash32 (device, n x 32 bytes: the full BLAKE3 hash; the cas_id is its first 8).
+ * The batch holds the device scratch its kernels pass between them (subtree chaining
+ * values), so runs of ONE batch must be ordered: the same stream, or an event between
+ * streams.  Its sampled and whole parts use separate scratch and may overlap each other
+ * (run_part on two streams).  Separate batches are independent. */
 int sd_cas_batch_run(sd_cas_ctx* ctx, const sd_cas_batch* batch, const uint8_t* d_staged,
                      uint8_t* d_hash32, void* stream);
 /* Same, restricted to one part of the batch (bitmask): SD_PART_SAMPLED runs only the
- * sampled-file kernel, SD_PART_WHOLE only the whole-file kernels (lets a caller time
- * each kernel with events on `stream`). */
+ * sampled-file kernels, SD_PART_WHOLE only the whole-file kernels (lets a caller time
+ * each part with events on `stream`). */
 #define SD_PART_SAMPLED 1
 #define SD_PART_WHOLE 2
 int sd_cas_batch_run_part(sd_cas_ctx* ctx, const sd_cas_batch* batch, int parts, const uint8_t* d_staged,
