@@ -187,6 +187,82 @@ __global__ __launch_bounds__(256) void k_cas_sampled_merge(const uint8_t* __rest
     store_cv(out + (size_t)idx[f] * 8, cur);
 }
 
+// Small batches (latency): the kernels above trade per-file latency for throughput -- one
+// lane walks 8 chunks (135 dependent compressions) and the merge adds 8 more, fine when
+// tens of thousands of files fill the chip, but a watcher event or a 100-file identifier
+// step then waits for that whole chain.  k_cas_sampled_wave: one 64-lane wave per file,
+// one full chunk per lane (lanes 0..55; the next line pair in flight while the current one
+// is compressed), lane 56 the 8-byte tail chunk, then the 57 chunk CVs merged level-wise
+// in LDS (6 levels): 16 + 6 dependent compressions per file.
+// Full 1 KiB non-root chunk, the next line pair in flight while the current one is
+// compressed: latency kernels (one chunk per lane, few waves) that cannot hide the load
+// of each line pair behind other waves.
+__device__ __forceinline__ void full_chunk_cv_prefetch(uint32_t (&cv)[8], const uint8_t* __restrict__ q,
+                                                       uint32_t counter) {
+    set_iv(cv);
+    uint32_t ma[16], mb[16], na[16], nb[16];
+    load_block(ma, q);
+    load_block(mb, q + 64);
+#pragma unroll
+    for (uint32_t b = 0; b < 16; b += 2) {
+        if (b + 2 < 16) {
+            load_block(na, q + 64u * (b + 2));
+            load_block(nb, q + 64u * (b + 3));
+        }
+        compress(cv, ma, counter, 0u, BLOCK_LEN, b == 0 ? CHUNK_START : 0u);
+        compress(cv, mb, counter, 0u, BLOCK_LEN, b + 1 == 15 ? CHUNK_END : 0u);
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            ma[i] = na[i];
+            mb[i] = nb[i];
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_cas_sampled_wave(const uint8_t* __restrict__ staged,
+                                                         const uint64_t* __restrict__ soff,
+                                                         const uint32_t* __restrict__ idx, uint32_t n,
+                                                         uint32_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[64][8];
+    const uint32_t f = blockIdx.x, t = threadIdx.x;
+    const uint8_t* msg = staged + soff[f];
+    uint32_t cv[8];
+    if (t < (uint32_t)S_FULL) {
+        full_chunk_cv_prefetch(cv, msg + (size_t)t * CHUNK_LEN, t);
+        store_cv(lds[t], cv);
+    } else if (t == (uint32_t)S_FULL) {
+        chunk_cv(cv, msg + (size_t)S_FULL * CHUNK_LEN, SD_SAMPLED_MSG_LEN - S_FULL * CHUNK_LEN, S_FULL, false);
+        store_cv(lds[t], cv);
+    }
+    __syncthreads();
+    lds_reduce(lds, S_FULL + 1, true);
+    if (t < 8) out[(size_t)idx[f] * 8 + t] = lds[0][t];
+}
+
+// Small batches of whole-kind messages (latency; see k_cas_sampled_wave): one 128-lane
+// workgroup per message of <= 101 chunks (SD_WHOLE_ITEMS_MAX), lane c hashes chunk c, the
+// chunk CVs merge level-wise in LDS: at most 16 + 7 dependent compressions, against the
+// work-list path's 33 (a chunk pair per lane) + two merge launches.  Row = (u64 message
+// offset, message length, output row).
+__global__ __launch_bounds__(128) void k_whole_wave(const uint8_t* __restrict__ staged, const uint4* __restrict__ rows,
+                                                    uint32_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[128][8];
+    const uint4 r = rows[blockIdx.x];
+    const uint32_t t = threadIdx.x, L = r.z;
+    const uint8_t* msg = staged + ((uint64_t)r.x | ((uint64_t)r.y << 32));
+    const uint32_t C = L == 0 ? 1u : (L + CHUNK_LEN - 1) / CHUNK_LEN;
+    if (t < C) {
+        const uint32_t len = L == 0 ? 0u : (L - t * CHUNK_LEN < CHUNK_LEN ? L - t * CHUNK_LEN : CHUNK_LEN);
+        uint32_t cv[8];
+        if (len == CHUNK_LEN && C > 1) full_chunk_cv_prefetch(cv, msg + (size_t)t * CHUNK_LEN, t);
+        else chunk_cv(cv, msg + (size_t)t * CHUNK_LEN, len, t, C == 1);
+        store_cv(lds[t], cv);
+    }
+    __syncthreads();
+    lds_reduce(lds, C, C > 1);  // one chunk: its last block already carried ROOT
+    if (t < 8) out[(size_t)r.w * 8 + t] = lds[0][t];
+}
+
 // ------------------------------------------------------------------ whole-file cas
 // Work items built on the host (sd_cas_api.cpp, plan_whole_items), 16 bytes each:
 //   full-pair item  (u64 pair offset, CV slot, first chunk index): an aligned chunk pair
@@ -380,6 +456,19 @@ hipError_t launch_cas_sampled(const uint8_t* staged, const uint64_t* soff, const
     const uint32_t lanes_wg = (uint32_t)(((uint64_t)n * S_K + 255) / 256), merge_wg = (n + 255) / 256;
     hipLaunchKernelGGL(k_cas_sampled_lanes<S_U>, dim3(lanes_wg), dim3(256), 0, s, staged, soff, n, rows);
     hipLaunchKernelGGL(k_cas_sampled_merge<S_U>, dim3(merge_wg), dim3(256), 0, s, staged, soff, idx, n, rows, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_whole_wave(const uint8_t* staged, const uint4* rows, uint32_t n, uint32_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_whole_wave, dim3(n), dim3(128), 0, s, staged, rows, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_cas_sampled_wave(const uint8_t* staged, const uint64_t* soff, const uint32_t* idx, uint32_t n,
+                                   uint32_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_cas_sampled_wave, dim3(n), dim3(64), 0, s, staged, soff, idx, n, out);
     return hipGetLastError();
 }
 

@@ -96,11 +96,103 @@ struct PinnedBuf {
     uint8_t* u8() const { return reinterpret_cast<uint8_t*>(p); }
 };
 
-// per-call working set of the host drop-in entry points
+// A plan's host tables packed into one pinned buffer and copied to one device buffer with
+// a single H2D: one DMA the host does not wait on, instead of an allocation and a staged
+// pageable copy per table (those cost ~12 us each, most of a small batch's host time).
+// add() queues a table at a 16-byte aligned offset; upload() packs and copies.  The pinned
+// buffer is read by the async copy: the caller syncs the stream before the next upload
+// (every plan is rebuilt only after its previous run has drained).
+struct Tables {
+    PinnedBuf host;
+    DevBuf dev;
+    std::vector<std::pair<const void*, size_t>> parts;
+    std::vector<size_t> offs;
+    size_t bytes = 0;
+    void begin() {
+        parts.clear();
+        offs.clear();
+        bytes = 0;
+    }
+    template <class T>
+    size_t add(const std::vector<T>& v) {
+        const size_t o = bytes;
+        parts.emplace_back(v.data(), v.size() * sizeof(T));
+        offs.push_back(o);
+        bytes = align_up(o + v.size() * sizeof(T), 16);
+        return o;
+    }
+    void upload(hipStream_t s) {
+        if (bytes == 0) return;
+        host.ensure(bytes);
+        dev.ensure(bytes);
+        for (size_t k = 0; k < parts.size(); k++)
+            if (parts[k].second) memcpy(host.u8() + offs[k], parts[k].first, parts[k].second);
+        if (s) HIP_CHECK(hipMemcpyAsync(dev.p, host.p, bytes, hipMemcpyHostToDevice, s));
+        else HIP_CHECK(hipMemcpy(dev.p, host.p, bytes, hipMemcpyHostToDevice));
+    }
+    template <class T>
+    T* at(size_t off) const { return reinterpret_cast<T*>(reinterpret_cast<uint8_t*>(dev.p) + off); }
+};
+
+}  // namespace sdi
+
+struct sd_checksum_batch {
+    size_t n = 0;
+    CkPlan plan;
+    sdi::Tables tab;  // files, wg_map, then one table per reduce pass
+    size_t o_files = 0, o_map = 0;
+    std::vector<size_t> o_pass;
+    sdi::DevBuf lvl[2];
+    const ck_file* d_files() const { return tab.at<ck_file>(o_files); }
+    const uint2* d_map() const { return tab.at<uint2>(o_map); }
+    const ck_reduce_wg* d_pass(size_t k) const { return tab.at<ck_reduce_wg>(o_pass[k]); }
+};
+
+// one file over the ranks of a communicator (include/sd_cas.h, sd_split_range)
+struct sd_split_checksum {
+    SplitPlan sp;
+    sd_checksum_batch plan;  // the whole file as one message: leaf table + reduce passes
+};
+
+struct sd_cas_batch {
+    size_t n = 0;
+    uint32_t n_sampled = 0, n_whole = 0, n_long = 0;
+    uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0, whole_chunks = 0;
+    WholePlan whole;  // work lists (kernel formats in cas_kernels.hip, k_whole_items / _merge8)
+    sdi::Tables tab;  // the sampled files' rows and offsets, the work lists, the long-message rows
+    size_t o_sidx = 0, o_soff = 0, o_full = 0, o_tail = 0, o_ma = 0, o_mb = 0, o_lidx = 0, o_wrows = 0;
+    bool whole_wave = false;  // n_whole <= "whole_wave_max" at plan time: one workgroup per file
+    sdi::DevBuf cvbuf, cv2;
+    bool sampled_wave = false;  // n_sampled <= "sampled_wave_max" at plan time: one wave per file
+    sdi::DevBuf srows;          // otherwise the sampled files' node CVs between the two kernels
+    // whole-file messages longer than SD_WHOLE_ITEMS_MAX: a checksum sub-batch over their
+    // byte ranges, its hashes scattered to out[long_idx[i]]
+    sd_checksum_batch lng;
+    sdi::DevBuf long_out;
+    // host tables (packed into tab by the plan)
+    std::vector<uint32_t> h_sidx, h_long_idx;
+    std::vector<sd_u32x4> h_wrows;  // whole_wave: (u64 message offset, length, output row)
+    std::vector<uint64_t> h_soff;
+    const uint32_t* d_sidx() const { return tab.at<uint32_t>(o_sidx); }
+    const uint64_t* d_soff() const { return tab.at<uint64_t>(o_soff); }
+    const uint4* d_full() const { return tab.at<uint4>(o_full); }
+    const uint4* d_tail() const { return tab.at<uint4>(o_tail); }
+    const uint4* d_ma() const { return tab.at<uint4>(o_ma); }
+    const uint4* d_mb() const { return tab.at<uint4>(o_mb); }
+    const uint32_t* d_lidx() const { return tab.at<uint32_t>(o_lidx); }
+    const uint4* d_wrows() const { return tab.at<uint4>(o_wrows); }
+};
+
+namespace sdi {
+
+// per-call working set of the host drop-in entry points; its batches persist with the slot
+// in the context's pool, so a call reuses their device and pinned tables
 struct Slot {
     hipStream_t stream = nullptr;
     DevBuf staged, hashes;
     PinnedBuf host_hashes, window;
+    sd_cas_batch cas;
+    sd_checksum_batch ck;
 };
 
 }  // namespace sdi
@@ -182,38 +274,6 @@ struct SlotPair {
 };
 
 }  // namespace sdi
-
-struct sd_checksum_batch {
-    size_t n = 0;
-    CkPlan plan;
-    sdi::DevBuf files, wg_map;
-    sdi::DevBuf lvl[2];
-    std::vector<std::unique_ptr<sdi::DevBuf>> pass_wgs;  // capacity reused across replans
-};
-
-// one file over the ranks of a communicator (include/sd_cas.h, sd_split_range)
-struct sd_split_checksum {
-    SplitPlan sp;
-    sd_checksum_batch plan;  // the whole file as one message: leaf table + reduce passes
-};
-
-struct sd_cas_batch {
-    size_t n = 0;
-    uint32_t n_sampled = 0, n_whole = 0, n_long = 0;
-    uint64_t compressions = 0, msg_bytes = 0, staged_bytes = 0, whole_chunks = 0;
-    WholePlan whole;  // work lists (kernel formats in cas_kernels.hip, k_whole_items / _merge8)
-    sdi::DevBuf ext, sidx, soff, full_items, tail_items, merge_a, merge_b, cvbuf, cv2;
-    sdi::DevBuf srows;  // the sampled files' node CVs between the two sampled kernels
-    // whole-file messages longer than SD_WHOLE_ITEMS_MAX: a checksum sub-batch over their
-    // byte ranges, its hashes scattered to out[long_idx[i]]
-    sd_checksum_batch lng;
-    sdi::DevBuf long_idx, long_out;
-    // host copies backing async uploads
-    std::vector<sd_extent> h_ext;
-    std::vector<uint32_t> h_sidx, h_long_idx;
-    std::vector<uint64_t> h_soff;
-};
-
 
 namespace sdi {
 // checksum batches (device): (re)plan reusing the batch's buffers; the reduce passes; leaf + reduce

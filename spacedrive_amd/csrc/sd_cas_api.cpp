@@ -43,10 +43,12 @@ void plan_checksum_batch(sd_checksum_batch* b, const uint64_t* offsets, const ui
                          hipStream_t stream) {
     plan_checksum(b->plan, offsets, lens, n);
     b->n = n;
-    b->files.upload(b->plan.files, stream);
-    b->wg_map.upload(b->plan.wg_map, stream);
-    while (b->pass_wgs.size() < b->plan.passes.size()) b->pass_wgs.push_back(std::make_unique<DevBuf>());
-    for (size_t k = 0; k < b->plan.passes.size(); k++) b->pass_wgs[k]->upload(b->plan.passes[k], stream);
+    b->tab.begin();
+    b->o_files = b->tab.add(b->plan.files);
+    b->o_map = b->tab.add(b->plan.wg_map);
+    b->o_pass.clear();
+    for (const auto& ps : b->plan.passes) b->o_pass.push_back(b->tab.add(ps));
+    b->tab.upload(stream);
     b->lvl[0].ensure(b->plan.lvl_cap[0] * 32);
     b->lvl[1].ensure(b->plan.lvl_cap[1] * 32);
 }
@@ -55,14 +57,14 @@ void run_checksum_reduce(const sd_checksum_batch* b, uint32_t* out, hipStream_t 
     for (size_t k = 0; k < b->plan.passes.size(); k++) {
         const int src = (int)(k & 1);  // level 0 -> 1 -> 0 ...
         HIP_CHECK(sdk::launch_ck_reduce(b->lvl[src].as<uint32_t>(), b->lvl[1 - src].as<uint32_t>(),
-                                        b->pass_wgs[k]->as<ck_reduce_wg>(), (uint32_t)b->plan.passes[k].size(), out,
+                                        b->d_pass(k), (uint32_t)b->plan.passes[k].size(), out,
                                         s));
     }
 }
 
 void run_checksum_batch(const sd_checksum_batch* b, const uint8_t* d_data, uint8_t* d_hash32, hipStream_t s) {
     uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
-    HIP_CHECK(sdk::launch_ck_leaf(d_data, 0, 0, b->files.as<ck_file>(), b->wg_map.as<uint2>(),
+    HIP_CHECK(sdk::launch_ck_leaf(d_data, 0, 0, b->d_files(), b->d_map(),
                                   (uint32_t)b->plan.wg_map.size(), b->lvl[0].as<uint32_t>(), out, s));
     run_checksum_reduce(b, out, s);
 }
@@ -78,6 +80,7 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
     b->h_sidx.clear();
     b->h_soff.clear();
     b->h_long_idx.clear();
+    b->h_wrows.clear();
     std::vector<uint64_t> loff, llen;
     uint64_t end = 0;
     for (size_t i = 0; i < n; i++) {
@@ -102,41 +105,59 @@ void plan_cas_batch(sd_cas_batch* b, const sd_extent* ext, size_t n, hipStream_t
     b->staged_bytes = end;
     b->n_sampled = (uint32_t)b->h_sidx.size();
     b->n_long = (uint32_t)b->h_long_idx.size();
-    plan_whole_items(b->whole, ext, n);
-    b->h_ext.assign(ext, ext + n);
-    b->ext.upload(b->h_ext, stream);
-    b->sidx.upload(b->h_sidx, stream);
-    b->soff.upload(b->h_soff, stream);
-    b->full_items.upload(b->whole.full, stream);
-    b->tail_items.upload(b->whole.tail, stream);
-    b->merge_a.upload(b->whole.merge_a, stream);
-    b->merge_b.upload(b->whole.merge_b, stream);
+    b->whole_wave = b->n_whole <= (uint32_t)std::max(0, tuning_get(SD_TUNE_WHOLE_WAVE_MAX));
+    if (b->whole_wave) {  // small batch: one workgroup per whole-kind message, no work lists
+        b->whole = WholePlan{};
+        for (size_t i = 0; i < n; i++) {
+            const sd_extent& e = ext[i];
+            if (e.kind != SD_KIND_SAMPLED && e.msg_len <= SD_WHOLE_ITEMS_MAX)
+                b->h_wrows.push_back({(uint32_t)e.msg_offset, (uint32_t)(e.msg_offset >> 32), e.msg_len, (uint32_t)i});
+        }
+    } else {
+        plan_whole_items(b->whole, ext, n);
+    }
+    b->tab.begin();
+    b->o_sidx = b->tab.add(b->h_sidx);
+    b->o_soff = b->tab.add(b->h_soff);
+    b->o_full = b->tab.add(b->whole.full);
+    b->o_tail = b->tab.add(b->whole.tail);
+    b->o_ma = b->tab.add(b->whole.merge_a);
+    b->o_mb = b->tab.add(b->whole.merge_b);
+    b->o_lidx = b->tab.add(b->h_long_idx);
+    b->o_wrows = b->tab.add(b->h_wrows);
+    b->tab.upload(stream);
     b->cvbuf.ensure((size_t)b->whole.n_cv * 32);
     b->cv2.ensure((size_t)b->whole.n_cv2 * 32);
-    b->srows.ensure(sdk::cas_sampled_rows_bytes(b->n_sampled));
+    b->sampled_wave = b->n_sampled <= (uint32_t)std::max(0, tuning_get(SD_TUNE_SAMPLED_WAVE_MAX));
+    if (!b->sampled_wave) b->srows.ensure(sdk::cas_sampled_rows_bytes(b->n_sampled));
     if (b->n_long) {
         plan_checksum_batch(&b->lng, loff.data(), llen.data(), b->n_long, stream);
         b->compressions += b->lng.plan.compressions;
-        b->long_idx.upload(b->h_long_idx, stream);
         b->long_out.ensure((size_t)b->n_long * 32);
     }
 }
 
 void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_hash32, hipStream_t s, int parts) {
     uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
-    if (parts & SD_PART_SAMPLED)
-        HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->soff.as<uint64_t>(), b->sidx.as<uint32_t>(), b->n_sampled,
-                                          b->srows.as<uint32_t>(), out, s));
+    // small batches take the latency kernels (one wave / workgroup per file), large ones the
+    // throughput kernels; the plan chose ("sampled_wave_max", "whole_wave_max")
+    if ((parts & SD_PART_SAMPLED) && b->sampled_wave)
+        HIP_CHECK(sdk::launch_cas_sampled_wave(d_staged, b->d_soff(), b->d_sidx(), b->n_sampled, out, s));
+    else if (parts & SD_PART_SAMPLED)
+        HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->d_soff(), b->d_sidx(), b->n_sampled, b->srows.as<uint32_t>(),
+                                          out, s));
     if (parts & SD_PART_WHOLE) {
         const WholePlan& w = b->whole;
-        HIP_CHECK(sdk::launch_whole_items(d_staged, b->full_items.as<uint4>(), (uint32_t)w.full.size(),
-                                          b->tail_items.as<uint4>(), (uint32_t)w.tail.size(), b->merge_a.as<uint4>(),
-                                          (uint32_t)w.merge_a.size(), b->merge_b.as<uint4>(),
-                                          (uint32_t)w.merge_b.size(), b->cvbuf.as<uint32_t>(),
-                                          b->cv2.as<uint32_t>(), out, s));
+        if (b->whole_wave)
+            HIP_CHECK(sdk::launch_whole_wave(d_staged, b->d_wrows(), (uint32_t)b->h_wrows.size(), out, s));
+        else
+            HIP_CHECK(sdk::launch_whole_items(d_staged, b->d_full(), (uint32_t)w.full.size(), b->d_tail(),
+                                              (uint32_t)w.tail.size(), b->d_ma(), (uint32_t)w.merge_a.size(),
+                                              b->d_mb(), (uint32_t)w.merge_b.size(), b->cvbuf.as<uint32_t>(),
+                                              b->cv2.as<uint32_t>(), out, s));
         if (b->n_long) {
             run_checksum_batch(&b->lng, d_staged, b->long_out.as<uint8_t>(), s);
-            HIP_CHECK(sdk::launch_scatter_hash(b->long_out.as<uint32_t>(), b->long_idx.as<uint32_t>(), b->n_long, out,
+            HIP_CHECK(sdk::launch_scatter_hash(b->long_out.as<uint32_t>(), b->d_lidx(), b->n_long, out,
                                                s));
         }
     }
@@ -355,7 +376,6 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
         bool busy = false;
     };
     SlotPair slots(ctx);
-    sd_cas_batch batches[2];
     Win wins[2];
     auto harvest = [&](int k) {
         if (!wins[k].busy) return;
@@ -390,12 +410,12 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
             ext.push_back(e);
         }
         Slot& sl = slots[w];
-        plan_cas_batch(&batches[w], ext.data(), ext.size(), sl.stream);
+        plan_cas_batch(&sl.cas, ext.data(), ext.size(), sl.stream);
         sl.staged.ensure(hi - lo);
         sl.hashes.ensure(ext.size() * 32);
         sl.host_hashes.ensure(ext.size() * 32);
         HIP_CHECK(hipMemcpyAsync(sl.staged.p, staged + lo, hi - lo, hipMemcpyHostToDevice, sl.stream));
-        run_cas_batch(&batches[w], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
+        run_cas_batch(&sl.cas, sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
         HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, ext.size() * 32, hipMemcpyDeviceToHost, sl.stream));
         wins[w] = Win{gi, gj, true};
         gi = gj;
@@ -508,8 +528,8 @@ int sd_split_checksum_leaves(sd_cas_ctx* ctx, const sd_split_checksum* x, const 
     ctx->bind();
     if (p.b1 > p.b0) {  // a rank past the last block holds nothing
         uint32_t* cvs = reinterpret_cast<uint32_t*>(d_cvs);
-        HIP_CHECK(sdk::launch_ck_leaf(d_slice, p.off, 0, x->plan.files.as<ck_file>(),
-                                      x->plan.wg_map.as<uint2>() + p.b0, (uint32_t)(p.b1 - p.b0), cvs, cvs,
+        HIP_CHECK(sdk::launch_ck_leaf(d_slice, p.off, 0, x->plan.d_files(),
+                                      x->plan.d_map() + p.b0, (uint32_t)(p.b1 - p.b0), cvs, cvs,
                                       ctx->pick(stream)));
     }
     return SD_OK;

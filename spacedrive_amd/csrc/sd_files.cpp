@@ -158,8 +158,8 @@ struct Streamer {
                 HIP_CHECK(hipMemcpyAsync(sl[k].staged.p, win, align_up(got, 64) + 64, hipMemcpyHostToDevice,
                                          sl[k].stream));
                 const uint32_t wg0 = (uint32_t)(pos / SD_CK_BLOCK);
-                HIP_CHECK(sdk::launch_ck_leaf(sl[k].staged.as<uint8_t>(), pos, 0, fin.files.as<ck_file>(),
-                                              fin.wg_map.as<uint2>() + wg0, (uint32_t)(nb - wg0),
+                HIP_CHECK(sdk::launch_ck_leaf(sl[k].staged.as<uint8_t>(), pos, 0, fin.d_files(),
+                                              fin.d_map() + wg0, (uint32_t)(nb - wg0),
                                               fin.lvl[0].as<uint32_t>(), out, sl[k].stream));
             }
             run_checksum_reduce(&fin, out, sl[k].stream);
@@ -232,7 +232,6 @@ void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes,
     std::shared_ptr<StagePool> pool = ctx->stage_pool(nthreads + 1);
     const uint64_t WINDOW = (uint64_t)std::max(1, tuning_get(SD_TUNE_FILES_WINDOW_MB)) << 20;
     SlotPair slots(ctx);
-    sd_cas_batch batches[2];
     struct Win {  // the window being staged into a slot's pinned buffer
         std::vector<sd_extent> ext;
         std::vector<size_t> idx;                // input index of each extent
@@ -333,14 +332,14 @@ void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes,
         staging = begin_window(next);  // the readers go on with the next window...
         if (m) {                        // ...while this one is planned and launched
             harvest(w);                 // slot w's previous launch (two windows back)
-            plan_cas_batch(&batches[w], W.ext.data(), m, sl.stream);
+            plan_cas_batch(&sl.cas, W.ext.data(), m, sl.stream);
             sl.staged.ensure(W.bytes + 64);
             sl.hashes.ensure(m * 32);
             sl.host_hashes.ensure(m * 32);
             HIP_CHECK(hipMemcpyAsync(sl.staged.p, sl.window.p, W.bytes, hipMemcpyHostToDevice, sl.stream));
             HIP_CHECK(hipEventRecord(copied[w], sl.stream));
             copy_pending[w] = true;
-            run_cas_batch(&batches[w], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
+            run_cas_batch(&sl.cas, sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
             if (d_hash32) {  // device output: the window's hashes scattered to their files' rows
                 dev_idx_h[w].assign(W.idx.begin(), W.idx.end());
                 dev_idx[w].upload(dev_idx_h[w], sl.stream);
@@ -430,7 +429,6 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
         std::vector<size_t> files;  // files whose hashes land in this slot's host_hashes
         bool busy = false;
     } pend[2];
-    sd_checksum_batch pack_batch[2];
     // streamed files' hashes arrive when their slot is next synchronised
     Streamer streamer([&](size_t i, const uint8_t* h) { to_hex(h, 32, out_hex65 + i * 65); });  // hash.rs:21-23
     int cur = 0;
@@ -516,11 +514,11 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
         pack_end = 0;
         if (ok.empty()) return;
         cur ^= 1;
-        plan_checksum_batch(&pack_batch[k], offs.data(), lens.data(), ok.size(), sl.stream);
+        plan_checksum_batch(&sl.ck, offs.data(), lens.data(), ok.size(), sl.stream);
         sl.hashes.ensure(ok.size() * 32);
         sl.host_hashes.ensure(ok.size() * 32);
         HIP_CHECK(hipMemcpyAsync(sl.staged.p, win, span + 64, hipMemcpyHostToDevice, sl.stream));
-        run_checksum_batch(&pack_batch[k], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
+        run_checksum_batch(&sl.ck, sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
         HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, ok.size() * 32, hipMemcpyDeviceToHost, sl.stream));
         pend[k].files = std::move(ok);
         pend[k].busy = true;
@@ -564,7 +562,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     constexpr uint64_t W = Streamer::W;
     SlotPair slots(ctx);
     Streamer::prepare(slots);
-    sd_checksum_batch batches[2], big;
+    sd_checksum_batch big;
     struct Pending {
         size_t i0 = 0, i1 = 0;
         bool busy = false;
@@ -621,8 +619,8 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
                 // kernels mask past a message's end, so nothing past it is read from `data`
                 const uint32_t wg0 = (uint32_t)(pos / SD_CK_BLOCK);
                 const uint32_t wg1 = (uint32_t)std::min<uint64_t>(nb, wg0 + W / SD_CK_BLOCK);
-                HIP_CHECK(sdk::launch_ck_leaf(slots[k].staged.as<uint8_t>(), pos, 0, big.files.as<ck_file>(),
-                                              big.wg_map.as<uint2>() + wg0, wg1 - wg0, big.lvl[0].as<uint32_t>(),
+                HIP_CHECK(sdk::launch_ck_leaf(slots[k].staged.as<uint8_t>(), pos, 0, big.d_files(),
+                                              big.d_map() + wg0, wg1 - wg0, big.lvl[0].as<uint32_t>(),
                                               slots[k].hashes.as<uint32_t>(), slots[k].stream));
                 done_with(k);
             }
@@ -653,11 +651,11 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         offs.assign(offsets + i, offsets + j);
         ls.assign(lens + i, lens + j);
         for (auto& o : offs) o -= lo;
-        plan_checksum_batch(&batches[k], offs.data(), ls.data(), j - i, sl.stream);
+        plan_checksum_batch(&sl.ck, offs.data(), ls.data(), j - i, sl.stream);
         sl.hashes.ensure((j - i) * 32);
         sl.host_hashes.ensure((j - i) * 32);
         copy_in(k, data + lo, end - lo);  // not past the last range: `data` may end there
-        run_checksum_batch(&batches[k], sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
+        run_checksum_batch(&sl.ck, sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
         done_with(k);
         HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, (j - i) * 32, hipMemcpyDeviceToHost, sl.stream));
         pend[k] = Pending{i, j, true};

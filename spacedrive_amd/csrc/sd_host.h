@@ -52,7 +52,9 @@ enum sd_tune_key {
     SD_TUNE_DEDUP_VARIANT = 3,    // sd_dedup_group: 0 = radix sort, 1 = LDS buckets (radix on overflow)
     SD_TUNE_LATENCY_CPU_MAX = 4,  // latency path: hash on the CPU while fewer calls are in flight
     SD_TUNE_READ_THREADS = 5,     // sd_file_checksums: parallel preads of regular files
-    SD_TUNE_NKEYS = 6
+    SD_TUNE_SAMPLED_WAVE_MAX = 6, // batches of at most this many sampled files: one wave per file (latency)
+    SD_TUNE_WHOLE_WAVE_MAX = 7,   // batches of at most this many whole-kind files: one workgroup per file
+    SD_TUNE_NKEYS = 8
 };
 int tuning_get(int key);
 

@@ -19,6 +19,12 @@ namespace sdk {
 uint64_t cas_sampled_rows_bytes(uint32_t n);
 hipError_t launch_cas_sampled(const uint8_t* staged, const uint64_t* soff, const uint32_t* idx, uint32_t n,
                               uint32_t* rows, uint32_t* out, hipStream_t s);
+// the same for small batches: one wave per file, 16 + 6 dependent compressions (latency)
+hipError_t launch_cas_sampled_wave(const uint8_t* staged, const uint64_t* soff, const uint32_t* idx, uint32_t n,
+                                   uint32_t* out, hipStream_t s);
+// whole-kind messages of <= 101 chunks, small batches: one workgroup per message (latency);
+// rows = (u64 message offset, length, output row)
+hipError_t launch_whole_wave(const uint8_t* staged, const uint4* rows, uint32_t n, uint32_t* out, hipStream_t s);
 // whole-file work lists: full-pair items, cost-sorted tail items, two merge8 passes (cv2 =
 // pass-A output)
 hipError_t launch_whole_items(const uint8_t* staged, const uint4* full, uint32_t n_full, const uint4* tail,

@@ -153,6 +153,32 @@ def test_sd_cas_ids_pipelined_windows(ctx):
             assert status[i] == 0 and raw[17 * i:17 * i + 16].decode() == h[i, :8].tobytes().hex(), i
 
 
+@pytest.mark.parametrize("mode", ["latency", "throughput"])
+def test_cas_latency_and_throughput_kernels(ctx, oracle_native, mode):
+    # the same batch through the latency kernels (k_cas_sampled_wave, k_whole_wave: one
+    # wave / workgroup per file) and the throughput kernels (lanes + merge, work lists),
+    # forced by the "sampled_wave_max" / "whole_wave_max" thresholds: full 32-byte hashes
+    # of every message length 0..2100, around the whole-file limit, and sampled files
+    from spacedrive_amd._native import lib
+    big = 1 << 30
+    thr = big if mode == "latency" else 0
+    assert lib().sd_cas_set_tuning(b"sampled_wave_max", thr) == 0
+    assert lib().sd_cas_set_tuning(b"whole_wave_max", thr) == 0
+    try:
+        sizes = np.concatenate([np.arange(0, 2100), np.arange(102300, 102401),
+                                np.arange(102401, 102401 + 300 * 4099, 4099)]).astype(np.uint64)
+        np.random.default_rng(9).shuffle(sizes)
+        cids = np.arange(len(sizes), dtype=np.uint64) + 31
+        twins = np.zeros(len(sizes), np.uint32)
+        h, ext, staged = gpu_cas(ctx, sizes, cids, twins, return_staged=True)
+        full = oracle_native.checksums(staged, ext["msg_offset"], ext["msg_len"].astype(np.uint64), nthreads=NT)
+        mism = np.nonzero((h != full).any(axis=1))[0]
+        assert len(mism) == 0, [(int(sizes[i])) for i in mism[:10]]
+    finally:
+        lib().sd_cas_set_tuning(b"sampled_wave_max", 6144)  # the defaults
+        lib().sd_cas_set_tuning(b"whole_wave_max", 512)
+
+
 def test_cas_exhaustive_small_sizes(ctx, oracle_native):
     # every message length across the first three chunks and the whole-file threshold
     sizes = np.concatenate([np.arange(0, 3200), np.arange(101000, 102500), np.arange(20000, 22000, 7)]).astype(np.uint64)
