@@ -1,6 +1,6 @@
 """Per-call cost of the path-based entry points at small batch sizes (the latency path and
-the identifier's 100-file steps): sd_cas_ids_files and sd_file_checksums with n = 1, 16,
-100 files of the bench's file-backed mixture on tmpfs, 200 calls each after a warm-up;
+the identifier's 100-file steps): sd_cas_ids_files and sd_file_checksums (GPU), and the
+library's CPU path on 16 threads beside them, with n = 1, 16, 100 files of the bench's file-backed mixture on tmpfs, 200 calls each after a warm-up;
 median / p90 wall time per call.  Prints one JSON object.
 python scripts/small_batch_probe.py [calls]"""
 import ctypes
@@ -45,7 +45,11 @@ def main():
             for name, fn in (("cas_ids_files", lambda: lib().sd_cas_ids_files(ctx.handle, arr, sz.ctypes.data, k, hex17,
                                                                                 st.ctypes.data, 16)),
                              ("file_checksums", lambda: lib().sd_file_checksums(ctx.handle, arr, k, hex65,
-                                                                                st.ctypes.data))):
+                                                                                st.ctypes.data)),
+                             ("cpu_cas_ids_files_16t", lambda: lib().sd_cpu_cas_ids_files(arr, sz.ctypes.data, k, hex17,
+                                                                                         st.ctypes.data, 16)),
+                             ("cpu_file_checksums_16t", lambda: lib().sd_cpu_file_checksums(arr, k, hex65,
+                                                                                           st.ctypes.data, 16))):
                 for _ in range(10):
                     check(fn())
                 ts = []

@@ -411,7 +411,10 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
     SD_GUARD_BEGIN
     if (!ctx || (n && (!paths || !out_hex65 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
     ctx->bind();
-    constexpr uint64_t W = Streamer::W;
+    // packs of at most 32 MiB: a pack is read whole before its copy starts, so smaller packs
+    // let the next pack's reads overlap this one's H2D and kernels (one 80 MB pack of 100
+    // files took 4.7 ms against 2.3 ms for the CPU path, read-bound alike)
+    constexpr uint64_t PACK = 32ull << 20;
     std::shared_ptr<StagePool> pool = ctx->stage_pool(std::max(1, std::min(64, tuning_get(SD_TUNE_READ_THREADS))));
     SlotPair slots(ctx);
     Streamer::prepare(slots);
@@ -525,12 +528,12 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
     };
     for (size_t i = 0; i < n; i++) {
         status[i] = SD_FILE_OK;
-        if (!regular[i] || hint[i] + 128 > W / 2) {  // a pipe / device / unreadable path, or large
+        if (!regular[i] || hint[i] + 128 > PACK / 2) {  // a pipe / device / unreadable path, or large
             submit_pack();
             stream_file(i);
             continue;
         }
-        if (pack_end + align_up(hint[i], 64) + 64 > W) submit_pack();
+        if (pack_end + align_up(hint[i], 64) + 64 > PACK) submit_pack();
         pack.push_back(i);
         pack_off.push_back(pack_end);
         pack_len.push_back(hint[i]);
