@@ -114,7 +114,11 @@ def test_gpu_entry_points_fail_without_a_device():
 
 def test_unknown_tuning_key_is_rejected():
     assert lib().sd_cas_set_tuning(b"whole_variant", 3) == -1  # the A/B kernel variants are gone
+    assert lib().sd_cas_set_tuning(b"sampled_variant", 0) == -1
     assert lib().sd_cas_set_tuning(b"files_window_mb", 32) == 0
+    # the batch-size policy between the latency and the throughput kernels
+    assert lib().sd_cas_set_tuning(b"sampled_wave_max", 6144) == 0
+    assert lib().sd_cas_set_tuning(b"whole_wave_max", 512) == 0
 
 
 def test_stage_files_threaded_equals_single(tmp_path):

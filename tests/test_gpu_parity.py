@@ -214,14 +214,21 @@ def test_cas_configs0_full_size_and_idempotent(ctx, oracle_native):
     assert np.array_equal(h1[:, :8], ids)
 
 
-def test_cas_sampled_batch_shapes(ctx, oracle_native):
-    # k_cas_sampled_lanes: 7 lanes per file in 256-lane workgroups (files straddle them);
-    # k_cas_sampled_merge: one lane per file -- partial last workgroups of both are bit-exact
-    for n in (1, 7, 15, 16, 17, 31, 32, 33, 36, 37, 65, 255, 256, 257, 1000):
-        sizes = np.full(n, 200001, np.uint64) + np.arange(n, dtype=np.uint64) * 4099
-        cids = np.arange(n, dtype=np.uint64) + 22
-        h = gpu_cas(ctx, sizes, cids, np.zeros(n, np.uint32))
-        assert np.array_equal(h[:, :8], oracle_native.cas_ids_synth(sizes, cids, nthreads=NT)), n
+@pytest.mark.parametrize("wave_max", [0, 6144])
+def test_cas_sampled_batch_shapes(ctx, oracle_native, wave_max):
+    # throughput path (sampled_wave_max 0): k_cas_sampled_lanes, 7 lanes per file in 256-lane
+    # workgroups (files straddle them), and k_cas_sampled_merge, one lane per file; latency
+    # path (the default threshold): one wave per file -- partial last workgroups bit-exact
+    from spacedrive_amd._native import lib
+    assert lib().sd_cas_set_tuning(b"sampled_wave_max", wave_max) == 0
+    try:
+        for n in (1, 7, 15, 16, 17, 31, 32, 33, 36, 37, 65, 255, 256, 257, 1000):
+            sizes = np.full(n, 200001, np.uint64) + np.arange(n, dtype=np.uint64) * 4099
+            cids = np.arange(n, dtype=np.uint64) + 22
+            h = gpu_cas(ctx, sizes, cids, np.zeros(n, np.uint32))
+            assert np.array_equal(h[:, :8], oracle_native.cas_ids_synth(sizes, cids, nthreads=NT)), n
+    finally:
+        lib().sd_cas_set_tuning(b"sampled_wave_max", 6144)
 
 
 def test_sample_twins_and_duplicates(ctx):
