@@ -368,7 +368,10 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * (200), "coalesce_max" (4096) and "latency_cpu_max" (16) of the latency path;
  * "files_window_mb" (32) of sd_cas_ids_files; "read_threads" (16) of sd_file_checksums;
  * "dedup_variant" (sd_dedup_group) 0 =
- * rocPRIM radix sort, 1 = LDS buckets with the radix sort as overflow fallback (default).
+ * rocPRIM radix sort, 1 = LDS buckets with the radix sort as overflow fallback (default);
+ * "sampled_wave_max" (6144) / "whole_wave_max" (512): a cas batch with at most that many
+ * sampled / whole-kind files takes the latency kernels (one wave or workgroup per file),
+ * a larger one the throughput kernels -- read when the batch is planned.
  * Unknown keys fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);
 /* Read-only probe over d_buf[0, bytes) (bytes a multiple of 4096) for calibrating the
