@@ -37,8 +37,29 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
 constexpr int PERM[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
 constexpr int sigma(int r, int i) { return r == 0 ? i : sigma(r - 1, PERM[i]); }
 
+// rotr(d ^ a, 16) as two VOP2-SDWA xors that write the two 16-bit halves crosswise:
+// both are 2-source ops, where xor + v_alignbit pays one 3-source op (half issue rate on
+// gfx950).  scripts/valu_probe4.hip: 39.4 vs 38.5 T baseline lane-ops/s on four
+// independent G columns (profiles/r2/r2z4_valu_probe4.txt).  Not volatile: the compiler
+// still schedules it; the early-clobber output keeps d and a readable by the second xor.
+#ifndef SD_ROTR16_SDWA
+#define SD_ROTR16_SDWA 1
+#endif
+__device__ __forceinline__ uint32_t xor_rotr16(uint32_t d, uint32_t a) {
+#if SD_ROTR16_SDWA
+    uint32_t t;
+    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1\n\t"
+        "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
+        : "=&v"(t)
+        : "v"(d), "v"(a));
+    return t;
+#else
+    return rotr(d ^ a, 16);
+#endif
+}
+
 #define SD_G(a, b, c, d, x, y)            \
-    a = a + b + (x); d = rotr(d ^ a, 16); \
+    a = a + b + (x); d = xor_rotr16(d, a); \
     c = c + d;       b = rotr(b ^ c, 12); \
     a = a + b + (y); d = rotr(d ^ a, 8);  \
     c = c + d;       b = rotr(b ^ c, 7);
