@@ -924,7 +924,7 @@ def main():
                 break
             m_offs.append(pos)
             m_lens.append(ln)
-            pos = (pos + ln + 15) // 16 * 16
+            pos = (pos + ln + 127) // 128 * 128  # SD_STAGE_ALIGN starts (profiles/r2/r2z5_ck_align.json)
         if m_lens:
             cbm = ctx.checksum_batch(m_offs, m_lens)
             d_msum = torch.empty(len(m_lens) * 32, dtype=torch.uint8, device=dev)
@@ -932,7 +932,8 @@ def main():
             mx_ms = ev_ms(lambda: cbm.run(d_data, d_msum, stream), stream, reps=args.checksum_steps)
             mroof = valu_roof(cbm.compressions, mx_ms)
             out["checksum"]["mixed"] = {
-                "workload": f"configs[3] mixed: {len(m_lens)} files of 2..8 GiB, unaligned lengths",
+                "workload": f"configs[3] mixed: {len(m_lens)} files of 2..8 GiB, unaligned lengths, "
+                            f"packed at 128-B (SD_STAGE_ALIGN) starts",
                 "files": len(m_lens), "bytes": cbm.total_bytes, "ms_per_run": mx_ms,
                 "GBps": cbm.total_bytes / (mx_ms * 1e-3) / 1e9, "frac": mroof["frac"],
                 "frac_full_rate": mroof["frac_full_rate"]}

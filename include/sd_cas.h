@@ -186,7 +186,9 @@ int sd_cas_batch_stats(const sd_cas_batch* batch, uint64_t out[8]);
 /* ---------------------------------------------------------------- checksums */
 /* Full-file BLAKE3 (hash.rs:10-24) of n files that are byte ranges of one device
  * buffer.  offsets/lens are HOST arrays; each range must start 16-byte aligned and the
- * buffer must be readable up to the next 64-byte boundary after each range. */
+ * buffer must be readable up to the next 64-byte boundary after each range.  Start ranges
+ * on SD_STAGE_ALIGN (128 B, a whole cache line) for full speed: a range that starts mid-line
+ * hashes about 5% slower (every line-pair load straddles two lines; scripts/ck_align_probe.py). */
 int sd_checksum_batch_create(sd_cas_ctx* ctx, const uint64_t* offsets, const uint64_t* lens,
                              size_t n, sd_checksum_batch** out);
 void sd_checksum_batch_destroy(sd_checksum_batch* batch);
@@ -196,7 +198,8 @@ int sd_checksum_batch_run(sd_cas_ctx* ctx, const sd_checksum_batch* batch, const
 int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
 /* Drop-in over host memory (pinned or pageable; hash.rs:10-24 on data already read):
  * full BLAKE3 of n byte ranges of `data` -> 65-byte hex each.  Ranges start 16-byte
- * aligned; no byte outside the ranges is read (a range may end where `data` ends).  Consecutive
+ * aligned (SD_STAGE_ALIGN for full speed: the windows keep the host layout on the device);
+ * no byte outside the ranges is read (a range may end where `data` ends).  Consecutive
  * ranges are copied 256 MiB window at a time, larger ranges stream; two windows alternate
  * so the H2D copies overlap the kernels. */
 int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,

@@ -402,7 +402,7 @@ int sd_cas_hashes_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_
 // hash.rs's 1 MiB read calls until one returns fewer.  For a regular file those reads are
 // exactly its bytes up to EOF, so regular files are read with parallel preads on the
 // context's stager pool ("read_threads"); anything else (a pipe, a device) with the
-// literal sequential loop.  Small regular files are packed (64-B aligned) into the current
+// literal sequential loop.  Small regular files are packed (128-B aligned) into the current
 // slot's pinned window by their stat length -- one batch per window, read in parallel,
 // each file probed past its length in case it grew --; while the GPU hashes one slot's
 // window the host reads the next into the other.  Larger files, files that grew, and
@@ -533,11 +533,13 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
             stream_file(i);
             continue;
         }
-        if (pack_end + align_up(hint[i], 64) + 64 > PACK) submit_pack();
+        // files start on whole 128-B lines (SD_STAGE_ALIGN): a start mid-line makes every
+        // line-pair load of k_ck_leaf straddle two lines (5% slower, scripts/ck_align_probe.py)
+        if (pack_end + align_up(hint[i], SD_STAGE_ALIGN) + 64 > PACK) submit_pack();
         pack.push_back(i);
         pack_off.push_back(pack_end);
         pack_len.push_back(hint[i]);
-        pack_end = align_up(pack_end + hint[i], 64);
+        pack_end = align_up(pack_end + hint[i], SD_STAGE_ALIGN);
     }
     submit_pack();
     for (size_t i : grew) {
