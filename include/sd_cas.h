@@ -198,8 +198,8 @@ int sd_checksum_batch_run(sd_cas_ctx* ctx, const sd_checksum_batch* batch, const
 int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
 /* Drop-in over host memory (pinned or pageable; hash.rs:10-24 on data already read):
  * full BLAKE3 of n byte ranges of `data` -> 65-byte hex each.  Ranges start 16-byte
- * aligned (SD_STAGE_ALIGN for full speed: the windows keep the host layout on the device);
- * no byte outside the ranges is read (a range may end where `data` ends).  Consecutive
+ * aligned (ranges of 1 MiB or more are placed on 128-B device lines whatever their host
+ * start); no byte outside the ranges is read (a range may end where `data` ends).  Consecutive
  * ranges are copied 256 MiB window at a time, larger ranges stream; two windows alternate
  * so the H2D copies overlap the kernels. */
 int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,

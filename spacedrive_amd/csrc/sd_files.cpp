@@ -596,10 +596,13 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         HIP_CHECK(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&used[k], hipEventDisableTiming));
     }
-    // H2D of `bytes` from `src` into slot k's device window, after its previous kernels
-    auto copy_in = [&](int k, const uint8_t* src, uint64_t bytes) {
-        if (used_set[k]) HIP_CHECK(hipStreamWaitEvent(cs, used[k], 0));
-        HIP_CHECK(hipMemcpyAsync(slots[k].staged.p, src, bytes, hipMemcpyHostToDevice, cs));
+    // H2D of `bytes` from `src` to byte `dst` of slot k's device window, after its previous
+    // kernels (first piece of a window) / before its next kernels (last piece)
+    auto copy_in = [&](int k, const uint8_t* src, uint64_t bytes, uint64_t dst = 0, bool first = true,
+                       bool last = true) {
+        if (first && used_set[k]) HIP_CHECK(hipStreamWaitEvent(cs, used[k], 0));
+        HIP_CHECK(hipMemcpyAsync(slots[k].staged.as<uint8_t>() + dst, src, bytes, hipMemcpyHostToDevice, cs));
+        if (!last) return;
         HIP_CHECK(hipEventRecord(copied[k], cs));
         HIP_CHECK(hipStreamWaitEvent(slots[k].stream, copied[k], 0));
     };
@@ -609,6 +612,10 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     };
     int cur = 0;
     std::vector<uint64_t> offs, ls;
+    struct RunT {  // a piece of a window copied with one H2D
+        uint64_t host_lo, host_end, dev_lo;
+    };
+    std::vector<RunT> runs;
     for (size_t i = 0; i < n;) {
         if (lens[i] + 128 > W) {  // one large range, streamed
             harvest(0);
@@ -638,28 +645,44 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
             i++;
             continue;
         }
-        // the next window: consecutive ranges whose span fits
-        const uint64_t lo = offsets[i];
-        uint64_t hi = 0, end = lo;  // hi: the window's padded span; end: its last byte + 1
+        // the next window: consecutive ranges whose device layout fits W.  Ranges keep their
+        // host-relative offsets, so a run of them is one H2D, except that a range of a leaf
+        // block or more that would start mid-line on the device opens a new run at the next
+        // 128-B line (a mid-line start costs k_ck_leaf 5%); only ascending,
+        // non-overlapping ranges open runs
+        runs.clear();
+        offs.clear();
+        ls.clear();
+        uint64_t dev_hi = 0;  // the device layout's padded end
         size_t j = i;
         while (j < n && lens[j] + 128 <= W) {
-            const uint64_t nhi = std::max(hi, align_up(offsets[j] + lens[j], 64));
-            if (j > i && (offsets[j] < lo || nhi - lo > W)) break;
-            hi = nhi;
-            end = std::max(end, offsets[j] + lens[j]);
+            const uint64_t o = offsets[j], L = lens[j];
+            const RunT* r = runs.empty() ? nullptr : &runs.back();
+            const bool misaligned = r && (r->dev_lo + (o - r->host_lo)) % SD_STAGE_ALIGN != 0;
+            const bool open = !r || (o >= r->host_end && L >= SD_CK_BLOCK && misaligned);
+            if (r && !open && o < r->host_lo) break;  // before its run: the next window takes it
+            const uint64_t dev_lo = open ? (r ? align_up(dev_hi, SD_STAGE_ALIGN) : 0) : r->dev_lo;
+            const uint64_t host_lo = open ? o : r->host_lo;
+            const uint64_t d = dev_lo + (o - host_lo);
+            const uint64_t nhi = std::max(dev_hi, align_up(d + L, 64));
+            if (j > i && nhi > W) break;
+            if (open) runs.push_back(RunT{o, o + L, dev_lo});
+            else runs.back().host_end = std::max(runs.back().host_end, o + L);
+            offs.push_back(d);
+            ls.push_back(L);
+            dev_hi = nhi;
             j++;
         }
         const int k = cur;
         cur ^= 1;
         harvest(k);
         Slot& sl = slots[k];
-        offs.assign(offsets + i, offsets + j);
-        ls.assign(lens + i, lens + j);
-        for (auto& o : offs) o -= lo;
         plan_checksum_batch(&sl.ck, offs.data(), ls.data(), j - i, sl.stream);
         sl.hashes.ensure((j - i) * 32);
         sl.host_hashes.ensure((j - i) * 32);
-        copy_in(k, data + lo, end - lo);  // not past the last range: `data` may end there
+        for (size_t q = 0; q < runs.size(); q++)  // not past a run's last range: `data` may end there
+            copy_in(k, data + runs[q].host_lo, runs[q].host_end - runs[q].host_lo, runs[q].dev_lo, q == 0,
+                    q + 1 == runs.size());
         run_checksum_batch(&sl.ck, sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
         done_with(k);
         HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, (j - i) * 32, hipMemcpyDeviceToHost, sl.stream));

@@ -915,6 +915,37 @@ def test_checksums_from_host_memory(ctx, oracle_native):
         assert raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), lens[i]
 
 
+def test_checksums_host_ranges_any_layout(ctx, oracle_native):
+    """sd_checksums over host ranges laid out every way a caller may: 16-byte starts (leaf-
+    sized ranges then start a new copy run on a 128-B device line), gaps,
+    a range hashed twice (overlap), one that lies before the previous one, small ranges
+    between big ones, and more than one 256 MiB window -- against the oracle."""
+    import ctypes
+    from spacedrive_amd._native import check, lib
+    MiB = 1 << 20
+    rng = np.random.default_rng(355)
+    span = 300 * MiB
+    host = torch.empty(span + 128, dtype=torch.uint8, pin_memory=True)
+    host.numpy()[:] = rng.integers(0, 256, span + 128, dtype=np.uint8)
+    offs, lens, off = [], [], 16
+    for L in [MiB + 16, 7, 3 * MiB + 5, 2 * MiB, 100, 5 * MiB + 1, 64 * MiB + 48, 1025, 130 * MiB + 3,
+              90 * MiB + 16, 2 * MiB + 1]:
+        offs.append(off)
+        lens.append(L)
+        off = (off + L + 16 * int(rng.integers(0, 9)) + 15) // 16 * 16  # gaps of 0..128 bytes
+    assert off <= span
+    offs += [offs[2], offs[1], 48]              # hashed again; before the previous range
+    lens += [lens[2], lens[1], 4 * MiB + 9]
+    arr_o = np.array(offs, np.uint64)
+    arr_l = np.array(lens, np.uint64)
+    out = ctypes.create_string_buffer(65 * len(lens))
+    check(lib().sd_checksums(ctx.handle, host.data_ptr(), arr_o.ctypes.data, arr_l.ctypes.data, len(lens), out))
+    want = oracle_native.checksums_simd(host.numpy(), arr_o, arr_l, nthreads=NT)
+    raw = out.raw
+    for i in range(len(lens)):
+        assert raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), (i, offs[i], lens[i])
+
+
 def test_checksums_host_ranges_end_at_a_guard_page(ctx, oracle_native):
     """sd_checksums reads no byte past a range: pageable buffers whose last range ends at
     an unreadable (PROT_NONE) page, through the packed window and the streamed (> 256 MiB)
@@ -924,7 +955,8 @@ def test_checksums_host_ranges_end_at_a_guard_page(ctx, oracle_native):
     import mmap
     from spacedrive_amd._native import check, lib
     page = mmap.PAGESIZE
-    for lens in ([3, 1000, 4096 + 16], [(300 << 20) + 16]):
+    # the third set: leaf-sized ranges at mid-line starts, each copied as its own run (§3.2b)
+    for lens in ([3, 1000, 4096 + 16], [(300 << 20) + 16], [5, (1 << 20) + 16, 3 * (1 << 20) + 7, (2 << 20) + 16]):
         offs, off = [], 0
         for L in lens:
             off = (off + 15) // 16 * 16
