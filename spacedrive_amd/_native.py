@@ -64,6 +64,7 @@ SIGNATURES = [
     ("sd_cas_stage_files", I32, [P, P, SZ, P, P, I32]),
     ("sd_cas_ids", I32, [P, P, U64, P, SZ, P, P]),
     ("sd_cas_ids_files", I32, [P, P, P, SZ, P, P, I32]),
+    ("sd_cas_ids_files_stats", I32, [P, P]),
     ("sd_cas_hashes_files", I32, [P, P, P, SZ, P, P, P, I32]),
     ("sd_cas_batch_create", I32, [P, P, SZ, ctypes.POINTER(P)]),
     ("sd_cas_batch_destroy", None, [P]),

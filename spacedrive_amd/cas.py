@@ -127,6 +127,15 @@ def file_checksum(path: Union[str, os.PathLike], device: Optional[int] = None) -
     return out.raw[:64].decode()
 
 
+def cas_ids_files_stats(device: Optional[int] = None) -> dict:
+    """Routes taken by generate_cas_ids (sd_cas_ids_files) on the device's default context:
+    calls hashed on the CPU path by the batch-size policy ("batch_cpu_max") and calls that
+    went through the GPU."""
+    v = np.zeros(2, np.uint64)
+    check(lib().sd_cas_ids_files_stats(default_context(device).handle, _ptr(v)))
+    return {"cpu": int(v[0]), "gpu": int(v[1])}
+
+
 def coalescer_stats(device: Optional[int] = None) -> dict:
     """Latency-path counters of the device's default context: single-file requests, the
     GPU batches they were coalesced into, the largest batch, and requests hashed on the

@@ -379,6 +379,14 @@ int sd_cas_ids_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* 
                      int32_t* status, int nthreads) {
     SD_GUARD_BEGIN
     if (!ctx || (n && (!paths || !sizes || !out_hex17 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    // batch-size policy: an identifier step's few files are hashed
+    // sooner on the host than through reads -> H2D -> kernels -> D2H; "batch_cpu_max" = 0
+    // sends every call to the GPU
+    if (n <= (size_t)std::max(0, tuning_get(SD_TUNE_BATCH_CPU_MAX))) {
+        ctx->files_calls_cpu.fetch_add(1, std::memory_order_relaxed);
+        return sd_cpu_cas_ids_files(paths, sizes, n, out_hex17, status, nthreads);
+    }
+    ctx->files_calls_gpu.fetch_add(1, std::memory_order_relaxed);
     cas_files(ctx, paths, sizes, n, out_hex17, nullptr, status, nthreads);
     return SD_OK;
     SD_GUARD_END

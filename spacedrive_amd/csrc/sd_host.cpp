@@ -21,11 +21,13 @@ thread_local std::string g_err;
 // dedup grouping, single-file calls on the CPU while fewer than 16 are in flight, 16 reader
 // threads for sd_file_checksums, the one-wave-per-file sampled kernel up to 6144 files
 // and one workgroup per whole-kind file up to 512 files (profiles/r2/r2z_small_batch_kernels.json:
-// the crossovers lie between 4096 and 8192 sampled files, 256 and 1024 whole-kind files)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}};
+// the crossovers lie between 4096 and 8192 sampled files, 256 and 1024 whole-kind files),
+// sd_cas_ids_files calls of up to 4096 files on the CPU path (profiles/r2/r2z6_batch_sizes.json:
+// from the page cache the host's 16 threads beat the GPU route up to ~8000 files a call)
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
-                                               "sampled_wave_max",   "whole_wave_max"};
+                                               "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max"};
 }  // namespace
 
 void sd_set_err(const char* fmt, ...) {

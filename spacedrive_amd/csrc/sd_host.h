@@ -54,7 +54,8 @@ enum sd_tune_key {
     SD_TUNE_READ_THREADS = 5,     // sd_file_checksums: parallel preads of regular files
     SD_TUNE_SAMPLED_WAVE_MAX = 6, // batches of at most this many sampled files: one wave per file (latency)
     SD_TUNE_WHOLE_WAVE_MAX = 7,   // batches of at most this many whole-kind files: one workgroup per file
-    SD_TUNE_NKEYS = 8
+    SD_TUNE_BATCH_CPU_MAX = 8,    // sd_cas_ids_files: calls of at most this many files take the CPU path
+    SD_TUNE_NKEYS = 9
 };
 int tuning_get(int key);
 

@@ -119,6 +119,8 @@ def test_unknown_tuning_key_is_rejected():
     # the batch-size policy between the latency and the throughput kernels
     assert lib().sd_cas_set_tuning(b"sampled_wave_max", 6144) == 0
     assert lib().sd_cas_set_tuning(b"whole_wave_max", 512) == 0
+    # sd_cas_ids_files' batch-size policy (CPU path at or below it)
+    assert lib().sd_cas_set_tuning(b"batch_cpu_max", 4096) == 0
 
 
 def test_stage_files_threaded_equals_single(tmp_path):

@@ -30,6 +30,17 @@ def ctx():
 
 
 @pytest.fixture(scope="module", autouse=True)
+def _gpu_route_for_batches():
+    """sd_cas_ids_files hashes calls of up to "batch_cpu_max" files on the CPU path; the
+    parity tests below exercise the GPU route, so the module turns the policy off (the
+    policy has its own test) and restores the library default after."""
+    import spacedrive_amd as sd
+    sd.set_tuning("batch_cpu_max", 0)
+    yield
+    sd.set_tuning("batch_cpu_max", 4096)
+
+
+@pytest.fixture(scope="module", autouse=True)
 def _rccl_background(ctx):
     """The one single-rank RCCL communicator (sd_comm_create) the RCCL tests share, created
     on a background thread as the module starts: RCCL's initialisation takes seconds, its
@@ -798,6 +809,44 @@ def test_latency_policy_routes_and_agrees(ctx, tmp_path):
     after = sd.coalescer_stats()
     assert got == want and sums == want_sums
     assert after["cpu"] - before["cpu"] == 2 * len(paths) and after["batches"] == before["batches"]
+
+
+def test_batch_policy_routes_small_calls_to_the_cpu_path(ctx, tmp_path):
+    """SURVEY.md §8(f) rank 4 for batch calls: a generate_cas_ids (sd_cas_ids_files) call of
+    at most "batch_cpu_max" files is hashed on the CPU path (counted in
+    cas_ids_files_stats()["cpu"]) and returns exactly the GPU route's ids and statuses,
+    including a file shorter than its size and a missing path."""
+    import spacedrive_amd as sd
+    sizes = [0, 1, 1016, 102400, 102401, 300000, 5 << 20, 4000, 200000]
+    paths = []
+    for i, s in enumerate(sizes):
+        p = tmp_path / f"bp{i}"
+        p.write_bytes(cs.synth_bytes(700 + i, 0, 0, s if i < 7 else s // 2))  # the last two shrank
+        paths.append(str(p))
+    paths.append(str(tmp_path / "missing"))
+    sizes.append(5000)
+
+    def ids():  # an id, or the error's type and errno
+        return [r if isinstance(r, str) else (type(r).__name__, r.errno) for r in sd.generate_cas_ids(paths, sizes)]
+
+    want = ids()
+    assert sum(isinstance(r, str) for r in want) == len(paths) - 2, want  # the shrunk sampled file, the missing one
+    s0 = sd.cas_ids_files_stats()
+    sd.set_tuning("batch_cpu_max", len(paths))
+    try:
+        got = ids()
+    finally:
+        sd.set_tuning("batch_cpu_max", 0)
+    s1 = sd.cas_ids_files_stats()
+    assert got == want
+    assert s1["cpu"] - s0["cpu"] == 1 and s1["gpu"] - s0["gpu"] == 0
+    sd.set_tuning("batch_cpu_max", len(paths) - 1)  # one file more than the threshold: the GPU
+    try:
+        assert ids() == want
+    finally:
+        sd.set_tuning("batch_cpu_max", 0)
+    s2 = sd.cas_ids_files_stats()
+    assert s2["gpu"] - s1["gpu"] == 1 and s2["cpu"] == s1["cpu"]
 
 
 def test_dedup_mgpu_through_rccl_single_rank(ctx, rccl_comm):
