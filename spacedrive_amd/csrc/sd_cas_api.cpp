@@ -702,7 +702,7 @@ int sd_valu_peak(sd_cas_ctx* ctx, double* lane_ops_per_s) {
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, ctx->device));
     const uint32_t grid = (uint32_t)prop.multiProcessorCount * 8;  // 8 x 256 threads per CU
-    const uint32_t iters = 512;
+    const uint32_t iters = 1024;  // ~5 ms a launch: the launch ramp is < 1%
     DevBuf sink;
     sink.alloc((size_t)grid * 256 * 4);
     hipStream_t s = ctx->stream;
@@ -719,7 +719,7 @@ int sd_valu_peak(sd_cas_ctx* ctx, double* lane_ops_per_s) {
     HIP_CHECK(hipEventElapsedTime(&ms, a, b));
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
-    const double ops = (double)reps * grid * 256.0 * iters * 96.0;  // 8 G-mixes x 12 ops per iteration
+    const double ops = (double)reps * grid * 256.0 * iters * sdk::VALU_PEAK_OPS_PER_ITER;
     *lane_ops_per_s = ops / (ms * 1e-3);
     return SD_OK;
     SD_GUARD_END

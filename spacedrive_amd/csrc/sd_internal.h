@@ -40,6 +40,7 @@ hipError_t launch_synth_stage_cas(const uint64_t* sizes, const uint64_t* cids, c
 hipError_t launch_synth_fill(uint64_t cid, uint32_t twin, uint64_t offset, uint64_t len, uint8_t* out,
                              hipStream_t s);
 hipError_t launch_read_probe(const uint8_t* buf, uint64_t bytes, int pattern, hipStream_t s);
+constexpr uint32_t VALU_PEAK_OPS_PER_ITER = 384;  // k_valu_peak: VALU instructions per wave per iteration
 hipError_t launch_valu_peak(uint32_t* sink, uint32_t iters, uint32_t grid, hipStream_t s);
 // dedup
 hipError_t dedup_partition(const uint8_t* hash32, const uint8_t* valid, uint64_t n, uint64_t base, int nparts,

@@ -86,27 +86,57 @@ __global__ __launch_bounds__(256) void k_synth_fill(uint64_t key, uint32_t twin,
     }
 }
 
-// VALU integer microbenchmark: 4 independent BLAKE3-style ARX chains per lane; each
-// iteration is 12 ops x 4 chains (add3, add, xor, alignbit mix like one G function).
+// VALU ceiling of BLAKE3's G as the kernels issue it (blake3_device.h: 2x v_add3_u32,
+// rotr16 as two crosswise v_xor_b32_sdwa, 2x v_add_u32, 3x v_xor_b32, 3x v_alignbit_b32),
+// written in asm on hard-named VGPRs (v8..v35: <= 64 allocated, so 8 waves per SIMD fit)
+// with no memory operation: 4 independent G columns per lane, interleaved op by op, the
+// state fed back round after round.  scripts/valu_probe7.hip runs the same block beside
+// per-op controls (profiles/r3/r3c_valu_probe7.txt).
+#define VR(n) "v" #n
+#define G_ADD3(a, b, m) "v_add3_u32 " VR(a) ", " VR(a) ", " VR(b) ", " VR(m) "\n"
+#define G_R16A(t, d, a) "v_xor_b32_sdwa " VR(t) ", " VR(d) ", " VR(a) " dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1\n"
+#define G_R16B(t, d, a) "v_xor_b32_sdwa " VR(t) ", " VR(d) ", " VR(a) " dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n"
+#define G_ADD(c, d) "v_add_u32 " VR(c) ", " VR(c) ", " VR(d) "\n"
+#define G_XOR(x, y, z) "v_xor_b32 " VR(x) ", " VR(y) ", " VR(z) "\n"
+#define G_ROT(x, n) "v_alignbit_b32 " VR(x) ", " VR(x) ", " VR(x) ", " #n "\n"
+// column k: a = v(8+k), b = v(12+k), c = v(16+k), d = v(20+k), m0 = v(24+k), m1 = v(28+k), t = v(32+k)
+#define G_COLS(OP, ...) OP(8, 12, 16, 20, 24, 28, 32) OP(9, 13, 17, 21, 25, 29, 33) OP(10, 14, 18, 22, 26, 30, 34) \
+    OP(11, 15, 19, 23, 27, 31, 35)
+#define S1(a, b, c, d, m0, m1, t) G_ADD3(a, b, m0)
+#define S2(a, b, c, d, m0, m1, t) G_R16A(t, d, a)
+#define S3(a, b, c, d, m0, m1, t) G_R16B(t, d, a)
+#define S4(a, b, c, d, m0, m1, t) G_ADD(c, t)
+#define S5(a, b, c, d, m0, m1, t) G_XOR(b, b, c)
+#define S6(a, b, c, d, m0, m1, t) G_ROT(b, 12)
+#define S7(a, b, c, d, m0, m1, t) G_ADD3(a, b, m1)
+#define S8(a, b, c, d, m0, m1, t) G_XOR(d, t, a)
+#define S9(a, b, c, d, m0, m1, t) G_ROT(d, 8)
+#define S10(a, b, c, d, m0, m1, t) G_ADD(c, d)
+#define S11(a, b, c, d, m0, m1, t) G_XOR(b, b, c)
+#define S12(a, b, c, d, m0, m1, t) G_ROT(b, 7)
+#define G_BLOCK                                                                                              \
+    G_COLS(S1) G_COLS(S2) G_COLS(S3) G_COLS(S4) G_COLS(S5) G_COLS(S6) G_COLS(S7) G_COLS(S8) G_COLS(S9) \
+        G_COLS(S10) G_COLS(S11) G_COLS(S12)
+#define G_CLOB                                                                                                 \
+    "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", \
+        "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35"
+static_assert(sdk::VALU_PEAK_OPS_PER_ITER == 8 * 48, "8 G blocks of 4 columns x 12 ops per iteration");
 __global__ __launch_bounds__(256) void k_valu_peak(uint32_t* sink, uint32_t iters) {
-    uint32_t a0 = threadIdx.x, b0 = blockIdx.x, c0 = 0x6A09E667u, d0 = 0xBB67AE85u;
-    uint32_t a1 = a0 ^ 1, b1 = b0 ^ 3, c1 = c0 ^ 5, d1 = d0 ^ 7;
-    uint32_t a2 = a0 ^ 11, b2 = b0 ^ 13, c2 = c0 ^ 17, d2 = d0 ^ 19;
-    uint32_t a3 = a0 ^ 23, b3 = b0 ^ 29, c3 = c0 ^ 31, d3 = d0 ^ 37;
-    const uint32_t mx = iters * 7u, my = iters * 13u;
-#define VG(a, b, c, d)                                                          \
-    a = a + b + mx; d = __builtin_amdgcn_alignbit(d ^ a, d ^ a, 16);            \
-    c = c + d;      b = __builtin_amdgcn_alignbit(b ^ c, b ^ c, 12);            \
-    a = a + b + my; d = __builtin_amdgcn_alignbit(d ^ a, d ^ a, 8);             \
-    c = c + d;      b = __builtin_amdgcn_alignbit(b ^ c, b ^ c, 7);
+    asm volatile(
+        "v_mov_b32 v8, 1\nv_mov_b32 v9, 2\nv_mov_b32 v10, 3\nv_mov_b32 v11, 4\nv_mov_b32 v12, 5\nv_mov_b32 v13, 6\n"
+        "v_mov_b32 v14, 7\nv_mov_b32 v15, 8\nv_mov_b32 v16, 9\nv_mov_b32 v17, 10\nv_mov_b32 v18, 11\nv_mov_b32 v19, 12\n"
+        "v_mov_b32 v20, 13\nv_mov_b32 v21, 14\nv_mov_b32 v22, 15\nv_mov_b32 v23, 16\nv_mov_b32 v24, 17\nv_mov_b32 v25, 18\n"
+        "v_mov_b32 v26, 19\nv_mov_b32 v27, 20\nv_mov_b32 v28, 21\nv_mov_b32 v29, 22\nv_mov_b32 v30, 23\nv_mov_b32 v31, 24\n"
+        "v_mov_b32 v32, 0\nv_mov_b32 v33, 0\nv_mov_b32 v34, 0\nv_mov_b32 v35, 0" ::: G_CLOB);
     for (uint32_t i = 0; i < iters; i++) {
-        VG(a0, b0, c0, d0) VG(a1, b1, c1, d1) VG(a2, b2, c2, d2) VG(a3, b3, c3, d3)
-        VG(a0, b0, c0, d0) VG(a1, b1, c1, d1) VG(a2, b2, c2, d2) VG(a3, b3, c3, d3)
+        asm volatile(G_BLOCK G_BLOCK G_BLOCK G_BLOCK ::: G_CLOB);
+        asm volatile(G_BLOCK G_BLOCK G_BLOCK G_BLOCK ::: G_CLOB);
     }
-#undef VG
-    const uint32_t r = a0 ^ b0 ^ c0 ^ d0 ^ a1 ^ b1 ^ c1 ^ d1 ^ a2 ^ b2 ^ c2 ^ d2 ^ a3 ^ b3 ^ c3 ^ d3;
-    if (r == 0x12345678u) sink[blockIdx.x * blockDim.x + threadIdx.x] = r;
+    uint32_t r;
+    asm volatile("v_xor_b32 %0, v8, v20" : "=v"(r));
+    if (r == 0x12345678u && iters == 7) sink[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
+#undef G_BLOCK
 
 // Read probe: XOR-reduces the buffer so nothing is dead-code eliminated; writes one word
 // per workgroup only if the reduction hits a sentinel (never, in practice).
