@@ -304,12 +304,24 @@ void sd_comm_destroy(sd_comm* comm);
  * Outputs hold `capacity` entries: d_records_out 2 x u64 each (sorted by (cas_id,
  * index)), d_rep_out and d_owner_out u64 each; *m_out = the records this rank owns,
  * *n_groups_out = its groups.  If any rank's capacity is too small, every rank returns
- * SD_ERR_CAPACITY before the record exchange, with *m_out = its own requirement.  Runs on
+ * SD_ERR_CAPACITY before the record exchange, with *m_out = its own requirement (and
+ * SD_ERR_INTERNAL together if any rank's partition counts disagree with its valid records:
+ * the gathered rows carry both, so no rank is left waiting in the exchange).  Runs on
  * `stream`; returns after the group counts are known (host sync). */
 int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, const uint8_t* d_valid, uint64_t n,
                       uint64_t global_index_base, uint64_t chunk_size, uint64_t* d_records_out, uint64_t* d_rep_out,
                       uint64_t* d_owner_out, uint64_t capacity, uint64_t* m_out, uint64_t* n_groups_out,
                       void* stream);
+/* Phase timing of sd_cas_dedup_mgpu (diagnostics): with timing on, each call records HIP
+ * events on its stream at the phase boundaries; sd_comm_last_phases waits for the last
+ * call's events and returns the SD_DEDUP_PHASES durations in ms, in order:
+ *   [0] partition (kernels), [1] all-gather of the rows + their copy to the host,
+ *   [2] host turnaround: the stream idles from the rows' arrival until the host, having read
+ *       them, has queued the exchange (the call's one mid-call sync),
+ *   [3] grouped ncclSend / ncclRecv of the records, [4] group + Object owners. */
+#define SD_DEDUP_PHASES 5
+int sd_comm_set_timing(sd_comm* comm, int on);
+int sd_comm_last_phases(sd_comm* comm, float* ms_out /* SD_DEDUP_PHASES */);
 
 /* ---------------------------------------------------------------- one file over many GPUs */
 /* file_checksum (hash.rs:10-24) of ONE file whose bytes are spread over the ranks of a
@@ -389,7 +401,8 @@ int sd_cas_set_tuning(const char* key, int value);
  * 16 B/lane streaming, pattern 1 = one lane per 1 KiB chunk reading 4 x 16 B per 64-byte
  * block (the hashing kernels' pattern), pattern 2 = pattern 1 with 2 chunks per lane. */
 int sd_read_probe(sd_cas_ctx* ctx, const uint8_t* d_buf, uint64_t bytes, int pattern, void* stream);
-/* VALU integer-throughput microbenchmark: returns measured lane-ops/s (BLAKE3 ARX mix). */
+/* VALU ceiling of the kernels' BLAKE3 G instruction mix (asm, registers only, 8 waves per SIMD):
+ * measured lane-ops/s on this device. */
 int sd_valu_peak(sd_cas_ctx* ctx, double* lane_ops_per_s);
 
 #ifdef __cplusplus

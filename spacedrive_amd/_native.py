@@ -93,6 +93,8 @@ SIGNATURES = [
     ("sd_comm_id", I32, [P]),
     ("sd_comm_create", I32, [P, P, I32, I32, ctypes.POINTER(P)]),
     ("sd_comm_destroy", None, [P]),
+    ("sd_comm_set_timing", I32, [P, I32]),
+    ("sd_comm_last_phases", I32, [P, P]),
     ("sd_cas_dedup_mgpu", I32, [P, P, P, P, U64, U64, U64, P, P, P, U64, PU64, PU64, P]),
     ("sd_split_range", I32, [U64, I32, I32, PU64, PU64, PU64]),
     ("sd_shard_plan", I32, [P, SZ, I32, P]),

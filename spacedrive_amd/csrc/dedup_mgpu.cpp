@@ -40,8 +40,14 @@ struct sd_comm {
     size_t send_bytes = 0;
     void* d_rows = nullptr;
     void* d_part_scratch = nullptr;  // sdk::dedup_partition's scratch; its last u64 = valid records
-    uint64_t* h_rows = nullptr;      // pinned: this rank's row extras, then all rows, then n_valid
+    uint64_t* h_rows = nullptr;      // pinned: this rank's row extras, then all rows
+    // sd_comm_set_timing: events around the phases of the last sd_cas_dedup_mgpu call
+    bool timing = false;
+    bool timed = false;  // the last call recorded all of ev[]
+    hipEvent_t ev[SD_DEDUP_PHASES + 1] = {};
     ~sd_comm() {
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
         if (d_part_scratch) (void)hipFree(d_part_scratch);
         if (d_send) (void)hipFree(d_send);
         if (d_rows) (void)hipFree(d_rows);
@@ -70,8 +76,17 @@ void check_rc(int rc) {
     if (rc != SD_OK) throw sd_failure(rc, sd_cas_last_error());
 }
 
-// row layout of the all-gather: counts[nranks], index base, local file count, capacity
+// row layout of the all-gather: counts[nranks], index base, local file count, capacity,
+// valid records (the partition's own total, so the consistency check is collective)
 constexpr int ROW_EXTRA = SD_EXCHANGE_ROW_EXTRA;
+static_assert(ROW_EXTRA == 4, "row = counts, base, n, capacity, valid");
+
+// phase boundary k of the current call, when timing is on
+void mark(sd_comm* c, int k, hipStream_t s) {
+    if (!c->timing) return;
+    if (!c->ev[k]) HIP_OK(hipEventCreate(&c->ev[k]));
+    HIP_OK(hipEventRecord(c->ev[k], s));
+}
 
 }  // namespace
 
@@ -144,29 +159,35 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
     uint64_t* d_all = d_row + row;
     const size_t psb = sdk::dedup_partition_scratch(R);
     uint64_t* pscratch = (uint64_t*)comm->d_part_scratch;
+    comm->timed = false;
+    mark(comm, 0, s);
     HIP_OK(sdk::dedup_partition(d_hash32, d_valid, n, global_index_base, R, d_row, (uint64_t*)comm->d_send, pscratch,
                                 s));
-    // 2. all-gather of (counts, index base, file count, capacity)
+    mark(comm, 1, s);
+    // 2. all-gather of (counts, index base, file count, capacity, valid records)
     uint64_t* h_row = comm->h_rows;
     h_row[R] = global_index_base;
     h_row[R + 1] = n;
     h_row[R + 2] = capacity;
-    HIP_OK(hipMemcpyAsync(d_row + R, h_row + R, sizeof(uint64_t) * ROW_EXTRA, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(d_row + R, h_row + R, sizeof(uint64_t) * 3, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(d_row + R + 3, pscratch + psb / sizeof(uint64_t) - 1, sizeof(uint64_t),
+                          hipMemcpyDeviceToDevice, s));
     NCCL_OK(ncclAllGather(d_row, d_all, row, ncclUint64, comm->comm, s));
     uint64_t* all = comm->h_rows + row;
     HIP_OK(hipMemcpyAsync(all, d_all, sizeof(uint64_t) * row * R, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipMemcpyAsync(all + row * R, pscratch + psb / sizeof(uint64_t) - 1, sizeof(uint64_t),
-                          hipMemcpyDeviceToHost, s));
+    mark(comm, 2, s);
     HIP_OK(hipStreamSynchronize(s));  // the one sync before the exchange: every rank's row
-    const uint64_t n_valid = all[row * R];
     const ExchangePlan plan = exchange_plan(all, R, me);
     *m_out = plan.recv_total;
     *n_groups_out = 0;
-    if (!plan.fits)  // every rank sees the same matrix, so every rank stops here
+    // every rank sees the same matrix, so every rank stops here together, before any record
+    // moves (a rank that stopped alone would leave its peers waiting in the send/receive)
+    if (!plan.fits)
         throw sd_failure(SD_ERR_CAPACITY, "an output capacity is smaller than the records its rank receives "
                                          "(*m_out = this rank's requirement)");
-    if (plan.send_total != n_valid) throw sd_failure(SD_ERR_INTERNAL, "partition counts disagree with the valid records");
+    if (!plan.consistent) throw sd_failure(SD_ERR_INTERNAL, "a rank's partition counts disagree with its valid records");
     // 3. the all-to-all of the 16-byte records: one send and one receive per peer
+    mark(comm, 3, s);
     const uint64_t* send = (const uint64_t*)comm->d_send;
     NCCL_OK(ncclGroupStart());
     for (int p = 0; p < R; p++) {
@@ -176,11 +197,34 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
             NCCL_OK(ncclRecv(d_records_out + 2 * plan.recv_off[p], 2 * plan.recv_cnt[p], ncclUint64, p, comm->comm, s));
     }
     NCCL_OK(ncclGroupEnd());
+    mark(comm, 4, s);
     // 4. group by cas_id and assign Objects (chunk-of-100 rule) on the received records
     uint64_t ng = 0;
     dedup_group_owners(ctx, d_records_out, *m_out, plan.ascending ? SD_DEDUP_INDEX_SORTED : 0, d_rep_out, chunk_size,
                        d_owner_out, &ng, s);
+    mark(comm, 5, s);
+    comm->timed = comm->timing;
     *n_groups_out = ng;
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_comm_set_timing(sd_comm* comm, int on) {
+    SD_GUARD_BEGIN
+    if (!comm) throw sd_failure(SD_ERR_INVALID, "null argument");
+    comm->timing = on != 0;
+    comm->timed = false;
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_comm_last_phases(sd_comm* comm, float* ms_out) {
+    SD_GUARD_BEGIN
+    if (!comm || !ms_out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (!comm->timed) throw sd_failure(SD_ERR_INVALID, "no timed sd_cas_dedup_mgpu call (sd_comm_set_timing)");
+    HIP_OK(hipSetDevice(comm->device));
+    HIP_OK(hipEventSynchronize(comm->ev[SD_DEDUP_PHASES]));
+    for (int k = 0; k < SD_DEDUP_PHASES; k++) HIP_OK(hipEventElapsedTime(&ms_out[k], comm->ev[k], comm->ev[k + 1]));
     return SD_OK;
     SD_GUARD_END
 }

@@ -422,15 +422,15 @@ void test_coalescer() {
 
 // ------------------------------------------------------------------ multi-GPU plans
 void test_exchange_plan() {
-    // 3 ranks: rows [to0, to1, to2, base, n, capacity]
-    const int R = 3;
-    std::vector<uint64_t> rows = {5, 1, 0, 0, 10, 100,    // rank 0: files [0, 10)
-                                  2, 0, 7, 10, 10, 100,   // rank 1: files [10, 20)
-                                  0, 3, 4, 20, 10, 100};  // rank 2: files [20, 30)
+    // 3 ranks: rows [to0, to1, to2, base, n, capacity, valid]
+    const int R = 3, W = R + SD_EXCHANGE_ROW_EXTRA;
+    std::vector<uint64_t> rows = {5, 1, 0, 0, 10, 100, 6,     // rank 0: files [0, 10)
+                                  2, 0, 7, 10, 10, 100, 9,    // rank 1: files [10, 20)
+                                  0, 3, 4, 20, 10, 100, 7};   // rank 2: files [20, 30)
     uint64_t sent_to[R][R] = {}, recv_from[R][R] = {};
     for (int me = 0; me < R; me++) {
         const ExchangePlan p = exchange_plan(rows.data(), R, me);
-        CHECK(p.fits && p.ascending);
+        CHECK(p.fits && p.ascending && p.consistent);
         uint64_t so = 0, ro = 0;
         for (int q = 0; q < R; q++) {
             CHECK(p.send_off[q] == so && p.recv_off[q] == ro);  // destination / source order
@@ -446,11 +446,16 @@ void test_exchange_plan() {
     CHECK(exchange_plan(rows.data(), R, 0).recv_total == 7 && exchange_plan(rows.data(), R, 2).recv_total == 11);
     // rank 2's capacity short: every rank sees it
     std::vector<uint64_t> tight = rows;
-    tight[2 * 6 + 5] = 10;
+    tight[2 * W + 5] = 10;
     for (int me = 0; me < R; me++) CHECK(!exchange_plan(tight.data(), R, me).fits);
+    // rank 1's counts disagree with its valid records: every rank sees it (and stops before
+    // the record exchange, so no peer is left waiting in a send or receive)
+    std::vector<uint64_t> bad = rows;
+    bad[1 * W + 6] = 8;
+    for (int me = 0; me < R; me++) CHECK(!exchange_plan(bad.data(), R, me).consistent);
     // overlapping index ranges: no ascending fast path, on any rank
     std::vector<uint64_t> overlap = rows;
-    overlap[1 * 6 + 3] = 5;
+    overlap[1 * W + 3] = 5;
     for (int me = 0; me < R; me++) CHECK(!exchange_plan(overlap.data(), R, me).ascending);
     // one file over R ranks: contiguous block ranges covering the file
     for (uint64_t total : {0ull, 1ull, (1ull << 20) + 1, (7ull << 20) + 5})

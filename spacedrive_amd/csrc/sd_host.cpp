@@ -24,10 +24,11 @@ thread_local std::string g_err;
 // the crossovers lie between 4096 and 8192 sampled files, 256 and 1024 whole-kind files),
 // sd_cas_ids_files calls of up to 4096 files on the CPU path (profiles/r2/r2z6_batch_sizes.json:
 // from the page cache the host's 16 threads beat the GPU route up to ~8000 files a call)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}};
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
-                                               "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max"};
+                                               "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",
+                                               "files_ring"};
 }  // namespace
 
 void sd_set_err(const char* fmt, ...) {
@@ -67,9 +68,11 @@ ExchangePlan exchange_plan(const uint64_t* rows, int R, int me) {
     p.recv_cnt.resize(R);
     p.recv_off.resize(R);
     for (int r = 0; r < R; r++) {
-        uint64_t in = 0;
+        uint64_t in = 0, out = 0;
         for (int src = 0; src < R; src++) in += cnt(src, r);
+        for (int dst = 0; dst < R; dst++) out += cnt(r, dst);
         if (in > rows[(size_t)r * row + R + 2]) p.fits = false;
+        if (out != rows[(size_t)r * row + R + 3]) p.consistent = false;
         if (r + 1 < R && rows[(size_t)r * row + R] + rows[(size_t)r * row + R + 1] > rows[(size_t)(r + 1) * row + R])
             p.ascending = false;
     }

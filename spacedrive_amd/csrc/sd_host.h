@@ -55,7 +55,8 @@ enum sd_tune_key {
     SD_TUNE_SAMPLED_WAVE_MAX = 6, // batches of at most this many sampled files: one wave per file (latency)
     SD_TUNE_WHOLE_WAVE_MAX = 7,   // batches of at most this many whole-kind files: one workgroup per file
     SD_TUNE_BATCH_CPU_MAX = 8,    // sd_cas_ids_files: calls of at most this many files take the CPU path
-    SD_TUNE_NKEYS = 9
+    SD_TUNE_FILES_RING = 9,       // sd_cas_ids_files: pinned window buffers the readers may fill ahead
+    SD_TUNE_NKEYS = 10
 };
 int tuning_get(int key);
 
@@ -145,16 +146,17 @@ SplitPlan split_plan(uint64_t total, int nranks, int rank);
 
 // The multi-GPU dedup exchange (sd_cas_dedup_mgpu) as seen by rank `me` from the gathered
 // rows of all R ranks, row r = [count to rank 0 .. count to rank R-1, index base, file
-// count, output capacity].  Every rank derives `fits` and `ascending` from the same matrix,
-// so all ranks take the same branch.  Records go out in destination order (the partition's
+// count, output capacity, valid records].  Every rank derives `fits`, `consistent` and
+// `ascending` from the same matrix, so all ranks take the same branch.  Records go out in destination order (the partition's
 // order) and come in in source-rank order.
 struct ExchangePlan {
     std::vector<uint64_t> send_cnt, send_off, recv_cnt, recv_off;  // per peer, in records
     uint64_t send_total = 0, recv_total = 0;
-    bool fits = true;       // every rank's capacity holds what it receives
-    bool ascending = true;  // the ranks' index ranges ascend with the rank
+    bool fits = true;        // every rank's capacity holds what it receives
+    bool consistent = true;  // every rank's counts add up to its valid records
+    bool ascending = true;   // the ranks' index ranges ascend with the rank
 };
-constexpr int SD_EXCHANGE_ROW_EXTRA = 3;
+constexpr int SD_EXCHANGE_ROW_EXTRA = 4;
 ExchangePlan exchange_plan(const uint64_t* rows, int R, int me);
 
 // ------------------------------------------------------------------ file reading

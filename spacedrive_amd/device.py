@@ -155,6 +155,18 @@ class Comm:
         check(lib().sd_comm_create(ctx.handle, uid, nranks, rank, ctypes.byref(h)))
         self.handle, self.nranks, self.rank = h, nranks, rank
 
+    PHASES = ("partition", "allgather_rows", "host_turnaround", "sendrecv", "group_owners")  # SD_DEDUP_PHASES
+
+    def set_timing(self, on: bool) -> None:
+        """sd_comm_set_timing: record HIP events at the phases of each sd_cas_dedup_mgpu call."""
+        check(lib().sd_comm_set_timing(self.handle, 1 if on else 0))
+
+    def last_phases(self) -> dict:
+        """sd_comm_last_phases: the last timed call's phase durations (ms), by name."""
+        ms = (ctypes.c_float * len(Comm.PHASES))()
+        check(lib().sd_comm_last_phases(self.handle, ms))
+        return {k: float(v) for k, v in zip(Comm.PHASES, ms)}
+
     def close(self) -> None:
         if self.handle:
             lib().sd_comm_destroy(self.handle)
