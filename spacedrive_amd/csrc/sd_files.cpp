@@ -10,7 +10,14 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <functional>
+#include <mutex>
 
 #include "sd_api_impl.h"
 
@@ -214,47 +221,117 @@ extern "C" {
 
 // Path-based drop-in batch: generate_cas_id (cas.rs:23-62) for n (path, size) pairs,
 // the sizes being the ones the caller's metadata reported (FileMetadata::new,
-// file_identifier/mod.rs:65-97).  Files are planned into windows of consecutive files;
-// the stager pool reads window k+1 into one pinned slot while window k's H2D copy,
-// kernels and D2H run on the other slot's stream.  A whole-kind file that turns out
-// longer than its planned extent (it grew since the caller's stat) is hashed afterwards
-// from the file itself, streamed (fs::read hashes every byte, cas.rs:29).
+// file_identifier/mod.rs:65-97).  A whole-kind file that turns out longer than its
+// planned extent (it grew since the caller's stat) is hashed afterwards from the file
+// itself, streamed (fs::read hashes every byte, cas.rs:29).
 namespace {
 // The body of sd_cas_ids_files (hex to host memory) and sd_cas_hashes_files (the 32-byte
 // hashes to device memory, for the multi-GPU dedup): out_hex17 xor d_hash32.
+//
+// The pipeline.  Every file's message is planned up front into windows of consecutive
+// files (messages at 128-B starts, at most "files_window_mb" per window).  The stager
+// pool's threads take the files in order from ONE cursor for the whole call and read each
+// into its window's buffer in a ring of "files_ring" pinned buffers, so no reader waits at
+// a window boundary for the window's slowest file or for this thread.  The reader that
+// completes a window's last file wakes this thread, which copies the window to the device
+// and queues its kernels and D2H on one of two device slots, then hands the previous
+// window's buffer (its copy done) back to the readers.  A reader waits only when it is a
+// whole ring ahead of the copies.  (Round 2 read one window at a time with a barrier
+// after each: 0.70 M files/s from tmpfs against 1.06 M for the same reads into one
+// buffer, profiles/r3/r3d_stager_probe.txt.)
 void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes, size_t n, char* out_hex17,
                uint8_t* d_hash32, int32_t* status, int nthreads) {
     ctx->bind();
+    if (n == 0) return;
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 64) nthreads = 64;
     // nthreads reader threads stage in the background (start/wait) while this thread plans,
     // launches and harvests the windows
     std::shared_ptr<StagePool> pool = ctx->stage_pool(nthreads + 1);
     const uint64_t WINDOW = (uint64_t)std::max(1, tuning_get(SD_TUNE_FILES_WINDOW_MB)) << 20;
+    const int RING = std::max(2, std::min(16, tuning_get(SD_TUNE_FILES_RING)));
+    // ---- the plan: extents relative to their window's start, windows of consecutive files
+    std::vector<sd_extent> ext(n);
+    std::vector<size_t> win_first;
+    std::vector<uint64_t> win_bytes;
+    {
+        uint64_t off = 0;
+        for (size_t i = 0; i < n; i++) {
+            sd_extent e = plan_extent(sizes[i], off);
+            uint64_t next = align_up(off + e.msg_len, SD_STAGE_ALIGN);
+            if (win_first.empty() || (i > win_first.back() && next > WINDOW)) {
+                if (!win_first.empty()) win_bytes.push_back(off);
+                win_first.push_back(i);
+                e = plan_extent(sizes[i], 0);
+                next = align_up(e.msg_len, SD_STAGE_ALIGN);
+            }
+            ext[i] = e;
+            off = next;
+        }
+        win_bytes.push_back(off);
+    }
+    const size_t nw = win_first.size();
+    win_first.push_back(n);
+    std::vector<uint32_t> win_of(n);
+    uint64_t max_win = 0;
+    for (size_t w = 0; w < nw; w++) {
+        for (size_t i = win_first[w]; i < win_first[w + 1]; i++) win_of[i] = (uint32_t)w;
+        max_win = std::max(max_win, win_bytes[w]);
+    }
+    // ---- the ring of pinned buffers (persistent: borrowed from the context's slot pool)
+    struct Ring {
+        sd_cas_ctx* c;
+        std::vector<std::unique_ptr<Slot>> s;
+        ~Ring() {
+            for (auto& x : s)
+                if (x) c->release(std::move(x));
+        }
+    } ring{ctx, {}};
+    for (int r = 0; r < RING; r++) {
+        ring.s.push_back(ctx->acquire());
+        ring.s.back()->window.ensure(max_win + 64);
+    }
     SlotPair slots(ctx);
-    struct Win {  // the window being staged into a slot's pinned buffer
-        std::vector<sd_extent> ext;
-        std::vector<size_t> idx;                // input index of each extent
-        std::vector<std::vector<uint8_t>> cap;  // a pipe's / device's whole content (stage_one)
-        uint64_t bytes = 0;
-    } wins[2];
-    struct Launched {  // the window in flight on a slot's stream
+    // ---- reader / launcher handshake
+    struct Shared {
+        std::mutex mu;
+        std::condition_variable to_main, to_readers;
+        std::unique_ptr<std::atomic<uint32_t>[]> left;      // files of window w not yet staged
+        std::unique_ptr<std::atomic<int64_t>[]> ring_win;   // the window ring buffer r may take
+        std::atomic<bool> abort{false};
+        std::vector<std::pair<size_t, std::vector<uint8_t>>> captured;  // pipes / devices, read whole
+    } sh;
+    sh.left.reset(new std::atomic<uint32_t>[nw]);
+    for (size_t w = 0; w < nw; w++) sh.left[w].store((uint32_t)(win_first[w + 1] - win_first[w]));
+    sh.ring_win.reset(new std::atomic<int64_t>[RING]);
+    for (int r = 0; r < RING; r++) sh.ring_win[r].store(r);
+    std::vector<uint8_t*> ring_buf(RING);
+    for (int r = 0; r < RING; r++) ring_buf[r] = ring.s[r]->window.u8();
+    hipEvent_t copied[16] = {};          // ring buffer r's H2D (events on the device slots' streams)
+    bool copy_pending[16] = {};
+    struct Launched {  // the window in flight on a device slot's stream
         std::vector<size_t> files;  // hashed files, in extent order
         bool busy = false;
     } launched[2];
-    hipEvent_t copied[2] = {nullptr, nullptr};  // the slot's pinned buffer has been read by its H2D
-    bool copy_pending[2] = {false, false};
-    struct Cleanup {  // on any exit: no reader left writing, no event leaked
+    struct Cleanup {  // on any exit: no reader left writing or waiting, no event leaked
         StagePool* pool;
+        Shared* sh;
         bool staging = false;
         hipEvent_t* ev;
         ~Cleanup() {
-            if (staging) pool->wait();
-            for (int k = 0; k < 2; k++)
+            if (staging) {
+                {
+                    std::lock_guard<std::mutex> g(sh->mu);
+                    sh->abort = true;
+                }
+                sh->to_readers.notify_all();
+                pool->wait();
+            }
+            for (int k = 0; k < 16; k++)
                 if (ev[k]) (void)hipEventDestroy(ev[k]);
         }
-    } cleanup{pool.get(), false, copied};
-    for (int k = 0; k < 2; k++) HIP_CHECK(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming));
+    } cleanup{pool.get(), &sh, false, copied};
+    for (int r = 0; r < RING; r++) HIP_CHECK(hipEventCreateWithFlags(&copied[r], hipEventDisableTiming));
     auto harvest = [&](int k) {
         if (!launched[k].busy) return;
         HIP_CHECK(hipStreamSynchronize(slots[k].stream));
@@ -270,91 +347,108 @@ void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes,
         if (out_hex17) to_hex(h, 8, out_hex17 + f * 17);       // cas.rs:61 to_hex()[..16]
         else HIP_CHECK(hipMemcpy(d_hash32 + 32 * f, h, 32, hipMemcpyHostToDevice));
     };
-    std::vector<size_t> overflow;                                      // regular files that grew
-    std::vector<std::pair<size_t, std::vector<uint8_t>>> captured;    // pipes / devices, read whole
-    size_t i = 0;
-    // plans the next window (consecutive files whose messages fit WINDOW bytes) into slot w
-    // and starts the readers on it; false when no files are left
-    auto begin_window = [&](int w) -> bool {
-        if (i >= n) return false;
-        Win& W = wins[w];
-        W.ext.clear();
-        W.idx.clear();
-        uint64_t off = 0;
-        while (i < n) {
-            const sd_extent e = plan_extent(sizes[i], off);
-            const uint64_t next = align_up(off + e.msg_len, SD_STAGE_ALIGN);
-            if (!W.ext.empty() && next > WINDOW) break;
-            W.ext.push_back(e);
-            W.idx.push_back(i);
-            off = next;
-            i++;
+    // ---- the readers: file i into its window's ring buffer
+    pool->start(n, [&](size_t i) {
+        const uint32_t w = win_of[i];
+        const int r = (int)(w % (uint32_t)RING);
+        if (sh.ring_win[r].load(std::memory_order_acquire) != (int64_t)w) {  // a whole ring ahead
+            std::unique_lock<std::mutex> g(sh.mu);
+            sh.to_readers.wait(g, [&] { return sh.abort.load() || sh.ring_win[r].load() == (int64_t)w; });
         }
-        W.bytes = off;
-        W.cap.assign(W.ext.size(), {});
-        if (copy_pending[w]) {  // the slot's last H2D must have read its buffer
-            HIP_CHECK(hipEventSynchronize(copied[w]));
-            copy_pending[w] = false;
+        if (sh.abort.load(std::memory_order_relaxed)) return;
+        std::vector<uint8_t> cap;
+        status[i] = stage_one(paths[i], ext[i], ring_buf[r], &cap);
+        if (!cap.empty()) {
+            std::lock_guard<std::mutex> g(sh.mu);
+            sh.captured.emplace_back(i, std::move(cap));
         }
-        if (slots[w].window.bytes < off + 64) {
-            harvest(w);  // a reallocation frees the buffer: nothing may still use it
-            slots[w].window.ensure(off + 64);
+        if (sh.left[w].fetch_sub(1, std::memory_order_acq_rel) == 1) {  // the window's last file
+            std::lock_guard<std::mutex> g(sh.mu);
+            sh.to_main.notify_one();
         }
-        uint8_t* win = slots[w].window.u8();
-        pool->start(W.ext.size(), [&W, win, paths, status](size_t q) {
-            status[W.idx[q]] = stage_one(paths[W.idx[q]], W.ext[q], win, &W.cap[q]);
-        });
-        cleanup.staging = true;
-        return true;
-    };
-    int w = 0;
-    bool staging = begin_window(w);
-    while (staging) {
-        pool->wait();  // window w is staged
-        cleanup.staging = false;
-        Win& W = wins[w];
-        Slot& sl = slots[w];
+    });
+    cleanup.staging = true;
+    // SD_PROFILE_FILES=1: one stderr line per call (where this thread's time goes)
+    static const bool prof = getenv("SD_PROFILE_FILES") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto t_call = clk::now();
+    double wait_s = 0, copy_wait_s = 0;
+    std::vector<sd_extent> wext;
+    std::vector<size_t> widx;
+    for (size_t w = 0; w < nw; w++) {
+        const auto tw = clk::now();
+        if (sh.left[w].load(std::memory_order_acquire) != 0) {
+            std::unique_lock<std::mutex> g(sh.mu);
+            sh.to_main.wait(g, [&] { return sh.left[w].load(std::memory_order_acquire) == 0; });
+        }
+        wait_s += std::chrono::duration<double>(clk::now() - tw).count();
+        const int r = (int)(w % (size_t)RING), k = (int)(w & 1);
+        Slot& sl = slots[k];
         // failed files (I/O error, short read) keep their status and leave the window;
         // files longer than their extent are hashed from disk after the windows
-        size_t m = 0;
-        for (size_t q = 0; q < W.ext.size(); q++) {
-            if (status[W.idx[q]] == SD_FILE_OK) {
-                W.ext[m] = W.ext[q];
-                W.idx[m++] = W.idx[q];
-            } else if (status[W.idx[q]] == SD_FILE_CHANGED) {
-                if (W.cap[q].empty()) overflow.push_back(W.idx[q]);
-                else captured.emplace_back(W.idx[q], std::move(W.cap[q]));
+        wext.clear();
+        widx.clear();
+        for (size_t i = win_first[w]; i < win_first[w + 1]; i++)
+            if (status[i] == SD_FILE_OK) {
+                wext.push_back(ext[i]);
+                widx.push_back(i);
             }
-        }
-        W.ext.resize(m);
-        W.idx.resize(m);
-        const int next = w ^ 1;
-        staging = begin_window(next);  // the readers go on with the next window...
-        if (m) {                        // ...while this one is planned and launched
-            harvest(w);                 // slot w's previous launch (two windows back)
-            plan_cas_batch(&sl.cas, W.ext.data(), m, sl.stream);
-            sl.staged.ensure(W.bytes + 64);
+        const size_t m = wext.size();
+        if (m) {
+            harvest(k);  // device slot k's previous launch (two windows back)
+            plan_cas_batch(&sl.cas, wext.data(), m, sl.stream);
+            sl.staged.ensure(win_bytes[w] + 64);
             sl.hashes.ensure(m * 32);
             sl.host_hashes.ensure(m * 32);
-            HIP_CHECK(hipMemcpyAsync(sl.staged.p, sl.window.p, W.bytes, hipMemcpyHostToDevice, sl.stream));
-            HIP_CHECK(hipEventRecord(copied[w], sl.stream));
-            copy_pending[w] = true;
+            HIP_CHECK(hipMemcpyAsync(sl.staged.p, ring_buf[r], win_bytes[w], hipMemcpyHostToDevice, sl.stream));
+            HIP_CHECK(hipEventRecord(copied[r], sl.stream));
+            copy_pending[r] = true;
             run_cas_batch(&sl.cas, sl.staged.as<uint8_t>(), sl.hashes.as<uint8_t>(), sl.stream);
             if (d_hash32) {  // device output: the window's hashes scattered to their files' rows
-                dev_idx_h[w].assign(W.idx.begin(), W.idx.end());
-                dev_idx[w].upload(dev_idx_h[w], sl.stream);
-                HIP_CHECK(sdk::launch_scatter_hash(sl.hashes.as<uint32_t>(), dev_idx[w].as<uint32_t>(), (uint32_t)m,
+                dev_idx_h[k].assign(widx.begin(), widx.end());
+                dev_idx[k].upload(dev_idx_h[k], sl.stream);
+                HIP_CHECK(sdk::launch_scatter_hash(sl.hashes.as<uint32_t>(), dev_idx[k].as<uint32_t>(), (uint32_t)m,
                                                    reinterpret_cast<uint32_t*>(d_hash32), sl.stream));
             } else {
                 HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, m * 32, hipMemcpyDeviceToHost, sl.stream));
             }
-            launched[w].files = W.idx;
-            launched[w].busy = true;
+            launched[k].files = widx;
+            launched[k].busy = true;
         }
-        w = next;
+        // the previous window's buffer goes back to the readers once its copy has read it
+        if (w >= 1 && w - 1 + RING < nw) {
+            const int rp = (int)((w - 1) % (size_t)RING);
+            const auto tc = clk::now();
+            if (copy_pending[rp]) HIP_CHECK(hipEventSynchronize(copied[rp]));
+            copy_pending[rp] = false;
+            copy_wait_s += std::chrono::duration<double>(clk::now() - tc).count();
+            {
+                std::lock_guard<std::mutex> g(sh.mu);
+                sh.ring_win[rp].store((int64_t)(w - 1 + RING), std::memory_order_release);
+            }
+            sh.to_readers.notify_all();
+        }
     }
+    pool->wait();  // every reader has returned (all windows are complete)
+    cleanup.staging = false;
+    const auto th = clk::now();
     harvest(0);
     harvest(1);
+    if (prof)
+        fprintf(stderr,
+                "[sd_files] cas_files n=%zu windows=%zu ring=%d window_mb=%d wall=%.3f ms wait=%.3f ms "
+                "copy_wait=%.3f ms tail=%.3f ms\n",
+                n, nw, RING, (int)(WINDOW >> 20), std::chrono::duration<double>(clk::now() - t_call).count() * 1e3,
+                wait_s * 1e3, copy_wait_s * 1e3, std::chrono::duration<double>(clk::now() - th).count() * 1e3);
+    // regular files that grew: SD_FILE_CHANGED and not captured by the reader
+    std::vector<std::pair<size_t, std::vector<uint8_t>>>& captured = sh.captured;
+    std::vector<size_t> overflow;
+    {
+        std::vector<uint8_t> cap_flag(n, 0);
+        for (auto& c : captured) cap_flag[c.first] = 1;
+        for (size_t i = 0; i < n; i++)
+            if (status[i] == SD_FILE_CHANGED && !cap_flag[i]) overflow.push_back(i);
+    }
     if (!overflow.empty() || !captured.empty()) {
         Streamer st([](size_t, const uint8_t*) {});
         int cur = 0;
