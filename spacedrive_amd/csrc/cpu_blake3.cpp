@@ -15,6 +15,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <stdlib.h>
+#include <sys/stat.h>
 #include <string.h>
 #include <unistd.h>
 
@@ -398,10 +399,97 @@ int sd_cpu_checksums(const uint8_t* data, const uint64_t* offsets, const uint64_
     SD_GUARD_END
 }
 
+// file_checksum (hash.rs:10-24) for n paths on the host.  A regular file of at least
+// CPU_SPLIT_MIN bytes is hashed block-parallel: its 1 MiB blocks are tasks of their own
+// (a block's chaining value depends only on its bytes and its chunk counter), so a batch
+// of a few large files keeps every thread busy; its root is merged from the block CVs.
+// For a regular file the 1 MiB reads of hash.rs are exactly its bytes up to EOF; if the
+// file turns out shorter or longer than its stat length while it is read, it is hashed
+// again with the sequential read loop.  Other files: one task each, the read loop.
+constexpr uint64_t CPU_SPLIT_MIN = 8ull << 20;
+
 int sd_cpu_file_checksums(const char* const* paths, size_t n, char* out_hex65, int32_t* status, int nthreads) {
     SD_GUARD_BEGIN
     if (n && (!paths || !out_hex65 || !status)) throw sd_failure(SD_ERR_INVALID, "null argument");
-    parallel_for(n, nthreads, [&](size_t i) { status[i] = cpu_checksum_file(paths[i], out_hex65 + 65 * i); });
+    struct Big {
+        size_t file;
+        uint64_t len, nb;
+        int fd;
+        std::vector<uint8_t> cvs;
+        std::atomic<bool> failed{false};
+    };
+    std::vector<uint64_t> len(n, 0);
+    std::vector<uint8_t> split(n, 0);
+    if (nthreads > 1)
+        parallel_for(n, nthreads, [&](size_t i) {
+            struct stat st;
+            if (stat(paths[i], &st) == 0 && S_ISREG(st.st_mode) && (uint64_t)st.st_size >= CPU_SPLIT_MIN) {
+                len[i] = (uint64_t)st.st_size;
+                split[i] = 1;
+            }
+        });
+    std::vector<std::unique_ptr<Big>> big;
+    struct Task {
+        size_t file;    // a whole file (block == UINT64_MAX) ...
+        uint64_t block; // ... or one 1 MiB block of big[file]
+    };
+    std::vector<Task> tasks;
+    for (size_t i = 0; i < n; i++) {
+        if (!split[i]) {
+            tasks.push_back({i, UINT64_MAX});
+            continue;
+        }
+        const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);  // hash.rs:11
+        if (fd < 0) {
+            tasks.push_back({i, UINT64_MAX});  // the read loop reports the error
+            continue;
+        }
+        auto b = std::make_unique<Big>();
+        b->file = i;
+        b->len = len[i];
+        b->nb = (len[i] + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
+        b->fd = fd;
+        b->cvs.resize(b->nb * 32);
+        for (uint64_t k = 0; k < b->nb; k++) tasks.push_back({big.size(), k});
+        big.push_back(std::move(b));
+    }
+    struct Close {
+        std::vector<std::unique_ptr<Big>>& b;
+        ~Close() {
+            for (auto& x : b) close(x->fd);
+        }
+    } closer{big};
+    parallel_for(tasks.size(), nthreads, [&](size_t t) {
+        const Task& task = tasks[t];
+        if (task.block == UINT64_MAX) {
+            status[task.file] = cpu_checksum_file(paths[task.file], out_hex65 + 65 * task.file);
+            return;
+        }
+        Big& b = *big[task.file];
+        if (b.failed.load(std::memory_order_relaxed)) return;
+        const uint64_t off = task.block * SD_CK_BLOCK;
+        const uint64_t want = std::min<uint64_t>(SD_CK_BLOCK, b.len - off);
+        uint8_t* buf = scratch(SD_CK_BLOCK);
+        if (pread_full(b.fd, buf, want, off) != (int64_t)want) {  // shrank (or an error): read loop below
+            b.failed.store(true, std::memory_order_relaxed);
+            return;
+        }
+        CpuHasher h(task.block * (SD_CK_BLOCK / 1024));
+        h.update(buf, want);
+        h.finalize_cv(b.cvs.data() + 32 * task.block);
+    });
+    for (auto& bp : big) {
+        Big& b = *bp;
+        uint8_t probe;
+        if (!b.failed.load() && pread_full(b.fd, &probe, 1, b.len) == 0) {  // nothing past the stat length
+            uint8_t h[32];
+            cpu_root_from_cvs(b.cvs.data(), b.nb, h);
+            hex_lower(h, 32, out_hex65 + 65 * b.file);  // hash.rs:21-23
+            status[b.file] = SD_FILE_OK;
+        } else {  // the file changed while it was read: hash.rs's sequential loop, to EOF
+            status[b.file] = cpu_checksum_file(paths[b.file], out_hex65 + 65 * b.file);
+        }
+    }
     return SD_OK;
     SD_GUARD_END
 }
