@@ -25,6 +25,36 @@ from typing import List, Optional, Sequence, Tuple
 CHUNK_SIZE = 100
 
 
+def _assign_step(chunk, cas_of, objects, obj_cas, out):
+    """mod.rs:136-333 for one step's rows (their cas_ids known): link to existing Objects,
+    create the rest.  Returns (created, linked)."""
+    unique = {cas_of[i] for i in chunk if cas_of[i] is not None}
+    existing = [o for o in range(len(objects)) if obj_cas[o] & unique]
+    existing_cas = set()
+    for o in existing:
+        existing_cas |= obj_cas[o]
+    linked = 0
+    for i in chunk:
+        c = cas_of[i]
+        if c is None:
+            continue
+        o = next((o for o in existing if c in obj_cas[o]), None)
+        if o is not None:
+            out[i] = o
+            objects[o].append(i)
+            linked += 1
+    created = 0
+    for i in chunk:
+        c = cas_of[i]
+        if c is None or c not in existing_cas:
+            o = len(objects)
+            objects.append([i])
+            obj_cas.append({c} if c is not None else set())
+            out[i] = o
+            created += 1
+    return created, linked
+
+
 def identifier_replay(cas_ids: Sequence[Optional[str]], chunk_size: int = CHUNK_SIZE
                       ) -> Tuple[List[int], List[Tuple[int, int]]]:
     """cas_ids in file_path.id order -> (object id per file, [(created, linked)] per chunk)."""
@@ -34,31 +64,44 @@ def identifier_replay(cas_ids: Sequence[Optional[str]], chunk_size: int = CHUNK_
     out: List[int] = [-1] * n
     stats = []
     for start in range(0, n, chunk_size):
-        chunk = range(start, min(n, start + chunk_size))
-        unique = {cas_ids[i] for i in chunk if cas_ids[i] is not None}
-        existing = [o for o in range(len(objects)) if obj_cas[o] & unique]
-        existing_cas = set()
-        for o in existing:
-            existing_cas |= obj_cas[o]
-        linked = 0
-        for i in chunk:
-            c = cas_ids[i]
-            if c is None:
-                continue
-            o = next((o for o in existing if c in obj_cas[o]), None)
-            if o is not None:
-                out[i] = o
-                objects[o].append(i)
-                linked += 1
-        created = 0
-        for i in chunk:
-            c = cas_ids[i]
-            if c is None or c not in existing_cas:
-                o = len(objects)
-                objects.append([i])
-                obj_cas.append({c} if c is not None else set())
-                out[i] = o
-                created += 1
-        stats.append((created, linked))
+        stats.append(_assign_step(range(start, min(n, start + chunk_size)), cas_ids, objects, obj_cas, out))
     # name every object by the file that created it
     return [objects[o][0] for o in out], stats
+
+
+ERR = object()  # a file whose FileMetadata::new failed (mod.rs:127-128: logged, dropped)
+
+
+def identifier_job_replay(results: Sequence, chunk_size: int = CHUNK_SIZE):
+    """The whole identifier JOB over orphan file_paths 0..n-1 (their ids), with per-file
+    hashing outcomes `results[i]` = cas_id str, None (empty file, no cas_id) or ERR:
+      * init: task_count = ceil(orphans / 100) steps, cursor = the first orphan's id
+        (file_identifier_job.rs:120-171);
+      * each step: orphans (no Object yet) with id >= cursor, in id order, at most 100
+        (get_orphan_file_paths, :286-309; orphan_path_filters :245-268); none -> EarlyFinish
+        (:196-203);
+      * a file whose metadata failed is dropped from the step and stays an orphan
+        (mod.rs:119-134); the rest link or create (mod.rs:136-333);
+      * cursor = the id of the step's last row (mod.rs:384-392) -- so a dropped file that
+        was its step's last row is queried (and hashed) again by the next step.
+    Returns (owner file index per file or None if never assigned, [(created, linked)] per
+    step, [rows queried per step])."""
+    n = len(results)
+    objects: List[List[int]] = []
+    obj_cas: List[set] = []
+    out: List[int] = [-1] * n
+    stats, queried = [], []
+    if n == 0:
+        return [], [], []
+    steps = (n + chunk_size - 1) // chunk_size
+    cursor = 0
+    for _ in range(steps):
+        rows = [i for i in range(cursor, n) if out[i] < 0][:chunk_size]
+        if not rows:
+            break  # EarlyFinish
+        queried.append(rows)
+        ok = [i for i in rows if results[i] is not ERR]
+        cas_of = {i: results[i] for i in ok}
+        stats.append(_assign_step(ok, cas_of, objects, obj_cas, out))
+        cursor = rows[-1]
+    return [objects[o][0] if o >= 0 else None for o in out], stats, queried

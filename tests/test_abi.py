@@ -225,5 +225,12 @@ def test_rust_step_excerpts_use_the_shim():
     assert 'error!("Failed to extract file metadata' in ident  # log and drop (mod.rs:127-128)
     assert "md.len() != 0" in ident  # empty files are not hashed (mod.rs:80-88)
     assert "CHUNK_SIZE stays" in ident
+    # the identifier reaches the GPU by looking ahead, K orphans per hashing call
+    # (spacedrive_amd/identifier.py IdentifierJob is the tested statement of it)
+    assert "pub const LOOKAHEAD: i64 = 32_768;" in ident and ".take(LOOKAHEAD)" in ident
+    assert "#[serde(skip)]" in ident and "lookahead.take(file_paths)" in ident
+    assert ".order_by(file_path::id::order(SortOrder::Asc))" in ident  # the reference's query order
+    from spacedrive_amd.identifier import LOOKAHEAD
+    assert LOOKAHEAD == 32768
     assert "file_checksums(full_paths.clone()).await" in valid
     assert "ValidatorError::FileIO(FileIOError::from((full_path, e))))?" in valid  # `?` per file (:147-149)
