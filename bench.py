@@ -38,17 +38,25 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
-# The int32 VALU roof.  BLAKE3's G function is 2x v_add3_u32 + 2x v_add_u32 + 4x v_xor_b32
-# + 4x v_alignbit_b32; the 3-source ops (add3, alignbit) issue at half the rate of 2-source
-# VOP2 ops (measured: profiles/r1c_valu_probe.txt), so the mix is bounded by one wave64 op
-# per 4 cycles per SIMD: 256 CU x 64 lane-ops/clk x 2.4 GHz = 39.3 T lane-ops/s.
+# The int32 VALU roof of BLAKE3.  Its G function is 2x v_add3_u32 + 2x v_add_u32 + 4x
+# v_xor_b32 + 4x v_alignbit_b32 (rotr16 as two v_xor_b32_sdwa).  Measured per op and per mix
+# (scripts/valu_probe7.hip, profiles/r3/r3c_valu_probe7.txt; 8 waves/SIMD): the 2-source
+# ops and -- the control -- v_fma_f32 and v_bitop3_b32 issue at the SIMD-32 full rate (68-70 T
+# at 2.38 GHz), while v_add3 / v_alignbit / v_perm / SDWA / v_xad / v_mad_u32_u24 / v_addc
+# issue at about half of it (37.4 T), and fp32 ops overlap those slow integer ops completely
+# (v_fma_f32 : v_add3 1:1 runs at the full rate) -- the slow integer ops are a separate, half-
+# rate datapath, not a harness limit.  BLAKE3's G mix written in asm, registers only, issues
+# at 39.5 T = 64.7 lane-ops/clk/CU (the in-library k_valu_peak is the same block: 39.3-39.5 T,
+# profiles/r3/r3d_valu_peak.txt).  So the roof is 64 lane-ops/clk/CU x 256 CU x 2.4 GHz:
 VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
 # The guide's full VALU rate (MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 op in 2
 # cycles): 256 x 128 x 2.4 GHz = 78.6 T lane-ops/s -- reported as frac_full_rate.
 VALU_FULL_RATE_TOPS = 256 * 128 * 2.4e9 / 1e12
-PEAK_BASIS = ("3-operand VALU issue bound (probe): 256 CU x 64 lane-ops/clk x 2.4 GHz. BLAKE3's G is "
-              "v_add3/v_alignbit-heavy; 3-source ops issue at half the 2-source rate (profiles/r1c_valu_probe.txt). "
-              "frac_full_rate is against the guide's SIMD-32 full rate, 256 CU x 128 lane-ops/clk x 2.4 GHz = 78.6 T")
+PEAK_BASIS = ("BLAKE3 G-mix issue ceiling: 256 CU x 64 lane-ops/clk x 2.4 GHz = 39.3 T.  Measured (scripts/valu_probe7.hip, "
+              "profiles/r3/r3c_valu_probe7.txt, 8 waves/SIMD): v_xor/v_add and the control v_fma_f32 issue at the full rate "
+              "(68-70 T), v_add3/v_alignbit/SDWA at about half (37.4 T), fp32 ops overlap them fully; the kernels' G mix in "
+              "asm from registers reaches 39.5 T (64.7 lane-ops/clk/CU) -- measured_valu_peak is that block in-library. "
+              "frac_full_rate is against the SIMD-32 full rate, 256 CU x 128 lane-ops/clk x 2.4 GHz = 78.6 T")
 SAMPLED_MSG = 57352
 S_LANES_PER_FILE = 7  # k_cas_sampled_lanes: one 256-lane grid slot per 8-chunk group (cas_kernels.hip)
 SAMPLED_KERNELS = ["k_cas_sampled_lanes", "k_cas_sampled_merge"]
@@ -81,14 +89,18 @@ def parse():
     p.add_argument("--warm-ms", type=float, default=150.0,
                    help="side legs: run a kernel this long before timing it (the clock ramps up from idle: "
                         "profiles/r2/r2b_whole_ab.json)")
-    p.add_argument("--file-backed-files", type=int, default=20000,
+    p.add_argument("--file-backed-files", type=int, default=200_000,
                    help="N=1 only: time the drop-in from files on disk (pread stager + sd_cas_ids) on this many "
                         "files of the shard, beside the reference's read schedule on the CPU; 0 = skip")
+    p.add_argument("--identifier-files", type=int, default=100_000,
+                   help="N=1 only: the identifier job (100-row steps) over this many of the file-backed files, "
+                        "look-ahead GPU hashing vs per-step CPU path; 0 = skip")
     p.add_argument("--host-staged-files", type=int, default=300_000,
-                   help="N=1 only: with-H2D leg, sd_cas_ids over this many files from pinned host memory; 0 = skip")
+                   help="with-H2D leg, sd_cas_ids over this many files from pinned host memory on every rank "
+                        "(at most 150 000 per rank at N > 1); 0 = skip")
     p.add_argument("--host-checksum-gib", type=int, default=4,
                    help="N=1 only: with-H2D checksum leg, sd_checksums over this many GiB of pinned memory; 0 = skip")
-    p.add_argument("--file-checksum-mib", type=int, default=2048,
+    p.add_argument("--file-checksum-mib", type=int, default=8192,
                    help="N=1 only: file-backed checksum leg on tmpfs (MiB, 256 MiB files); 0 = skip")
     p.add_argument("--latency-calls", type=int, default=400, help="N=1 only: single-call latency legs; 0 = skip")
     p.add_argument("--no-extras", action="store_true", help="skip every N=1 side leg (profiling passes)")
@@ -155,7 +167,19 @@ def host_cpu() -> dict:
                 model = line.split(":", 1)[1].strip()
     except (OSError, subprocess.SubprocessError):
         pass
-    return {"model": model, "cpus_online": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    quota = None
+    try:  # the cgroup's CPU bandwidth limit, if any ("max" = none)
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q[0] == "max" else float(q[0]) / float(q[1])
+    except (OSError, ValueError, IndexError):
+        pass
+    return {"model": model, "cpus_online": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "cgroup_cpu_quota": quota}
+
+
+def all_cores() -> int:
+    """nproc: every CPU this process may run on (SURVEY.md 8(d) configs[0](ii))."""
+    return len(os.sched_getaffinity(0))
 
 
 def cpu_baseline(sizes, cids, twins, seconds: float):
@@ -163,7 +187,9 @@ def cpu_baseline(sizes, cids, twins, seconds: float):
 
     Uses the SIMD multi-chunk hasher (oracle/sd_oracle_simd.c: AVX-512 16-way / AVX2 8-way
     hash_many, the strategy of the reference's blake3 crate), so the baseline is the
-    reference's arithmetic at its own CPU speed, not a scalar strawman."""
+    reference's arithmetic at its own CPU speed, not a scalar strawman.  Rows: 16 threads
+    (the host's share per GPU of an 8-GPU node), 1 thread (the reference's one hashing task
+    per step), and all cores (nproc)."""
     from oracle import native
     from spacedrive_amd.device import stage_plan
     threads = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share for one GPU
@@ -184,6 +210,8 @@ def cpu_baseline(sizes, cids, twins, seconds: float):
 
     n1, dt1, b1 = rate(1, 2000)
     nT, dtT, bT = rate(threads, 20000)
+    nA = all_cores()
+    nN, dtN, bN = rate(nA, 100000)
     simd = {0: "scalar", 1: "AVX2 8-way", 2: "AVX-512 16-way"}[level]
     return {
         "value": nT / dtT, "unit": "files/s", "cores": threads, "kind": "port",
@@ -192,8 +220,102 @@ def cpu_baseline(sizes, cids, twins, seconds: float):
                   f"on {threads} threads; {bT / dtT / 1e9:.2f} GB/s of message bytes",
         "single_thread": {"value": n1 / dt1, "unit": "files/s", "cores": 1, "sample_files": n1,
                           "GBps": b1 / dt1 / 1e9},
+        "all_cores": {"value": nN / dtN, "unit": "files/s", "cores": nA, "sample_files": nN, "GBps": bN / dtN / 1e9,
+                      "cgroup_cpu_quota": host_cpu().get("cgroup_cpu_quota"),
+                      "note": "the same hash-only leg on nproc threads; where the container's cgroup caps CPU time "
+                              "(cgroup_cpu_quota CPUs), nproc threads share that quota and are throttled"},
         "simd": simd, "host_cpu": host_cpu(),
     }
+
+
+# ------------------------------------------------------------------ parity of the timed steps
+def parity_sample(sizes, cids, twins, d_hash, start: int, k: int = 4096) -> dict:
+    """The timed steps' own output checked against the oracle (outside the timed region):
+    a fixed sample of this rank's shard -- k files at an even stride, plus the shard's first
+    32 (the edge sizes of SURVEY.md 8(d) on rank 0) -- has its cas messages built by the C
+    oracle from the same generator and hashed by the oracle's BLAKE3 (oracle/sd_oracle.c);
+    every sampled file's full 32-byte hash in d_hash must be equal."""
+    from oracle import native
+    from spacedrive_amd.device import stage_plan
+    n = len(sizes)
+    idx = np.unique(np.concatenate([np.arange(min(32, n)), np.linspace(0, n - 1, min(k, n)).astype(np.int64)]))
+    s, c, t = sizes[idx], cids[idx], twins[idx]
+    ext, total = stage_plan(s)
+    buf = native.stage_synth(s, c, t, ext["msg_offset"], total)
+    want = native.checksums(buf, ext["msg_offset"], ext["msg_len"], nthreads=16)
+    got = d_hash.view(-1, 32)[torch.from_numpy(idx).to(d_hash.device)].cpu().numpy()
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    return {"files": int(len(idx)), "mismatches": int(len(bad)),
+            "first_bad_global_index": int(start + idx[bad[0]]) if len(bad) else None,
+            "sampled_kind": int((s > 102400).sum()),
+            "note": "full 32-byte hashes of the timed steps' output vs the C oracle (oracle/sd_oracle.c) on the "
+                    "same generator: the shard's first 32 files + an even-stride sample"}
+
+
+def _gather_rows(t: torch.Tensor, world: int, dev) -> list:
+    """all_gather of a [m, w] int64 tensor whose m differs per rank (padded to the max)."""
+    if world == 1:
+        return [t]
+    m = torch.tensor([t.shape[0]], dtype=torch.int64, device=dev)
+    ms = [torch.zeros_like(m) for _ in range(world)]
+    dist.all_gather(ms, m)
+    mx = max(int(x.item()) for x in ms)
+    pad = torch.zeros((mx, t.shape[1]), dtype=t.dtype, device=dev)
+    pad[:t.shape[0]] = t.to(dev)
+    outs = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad)
+    return [o[:int(k.item())] for o, k in zip(outs, ms)]
+
+
+def dedup_parity(d_hash, d_valid, n: int, start: int, recs, rep, owners, world: int, dev) -> dict:
+    """The multi-rank exchange checked end to end on a slice of the key space: every record
+    whose cas_id key has bits 40..47 == 0 (1/256 of the keys, spread over every rank's
+    prefix range, so every destination and every source takes part; a group is wholly in or
+    out).  Input side: each rank's (key, global index) records of that slice, from its own
+    hashes.  Output side: each rank's exchanged, grouped records of that slice with their
+    representative and Object owner.  Rank 0 groups the input with group_host (the host
+    mirror of the grouping) and applies identifier.object_owners; the output must be the
+    same records, representatives and owners.  Returns the same dict on every rank."""
+    from spacedrive_amd import identifier
+    from spacedrive_amd.dedup import group_host
+    h = d_hash.view(n, 32)[:, :8].to(torch.int64)
+    key = torch.zeros(n, dtype=torch.int64, device=h.device)
+    for j in range(8):  # big-endian u64 of the first 8 hash bytes (the hex cas_id's order)
+        key = key | (h[:, j] << (56 - 8 * j))
+
+    def in_slice(k):
+        return ((k >> 40) & 0xFF) == 0
+
+    sel = in_slice(key) & (d_valid.view(-1) != 0)
+    gidx = torch.arange(start, start + n, dtype=torch.int64, device=h.device)
+    inp = torch.stack([key[sel], gidx[sel]], dim=1)
+    osel = in_slice(recs[:, 0])
+    outp = torch.stack([recs[osel, 0], recs[osel, 1], rep[osel], owners[osel]], dim=1)
+    cdev = dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu"
+    ins = _gather_rows(inp, world, cdev)
+    outs = _gather_rows(outp, world, cdev)
+    ok = torch.zeros(1, dtype=torch.int64, device=cdev)
+    res = {}
+    if int(os.environ.get("RANK", "0")) == 0:
+        a = torch.cat([x.cpu() for x in ins]).numpy()
+        b = torch.cat([x.cpu() for x in outs]).numpy()
+        r, rep_h, ng = group_host(a)
+        own_h = identifier.object_owners(torch.from_numpy(r[:, 1].copy()), torch.from_numpy(rep_h.copy())).numpy()
+        order = np.lexsort((b[:, 1], b[:, 0].view(np.uint64)))
+        b = b[order]
+        same = (len(b) == len(r) and np.array_equal(b[:, :2], r) and np.array_equal(b[:, 2], rep_h)
+                and np.array_equal(b[:, 3], own_h))
+        per_rank_out = [int(x.shape[0]) for x in outs]
+        res = {"records": int(len(r)), "groups": int(ng), "linked": int((own_h != r[:, 1]).sum()),
+               "out_records_per_rank": per_rank_out, "parity": bool(same)}
+        ok[0] = 1 if same else 0
+    if world > 1:
+        dist.broadcast(ok, 0)
+    res["parity"] = bool(int(ok.item()))
+    res["slice"] = "cas_id keys with bits 40..47 == 0 (1/256 of the key space, every prefix range)"
+    res["note"] = ("input records (each rank's own hashes) grouped on rank 0 by group_host + identifier.object_owners "
+                   "vs the exchanged, grouped output of sd_cas_dedup_mgpu from every rank")
+    return res
 
 
 # ------------------------------------------------------------------ with-H2D legs
@@ -208,10 +330,13 @@ def ev_ms(fn, stream, reps=1):
     return e0.elapsed_time(e1) / reps
 
 
-def host_staged(ctx, ext, d_staged, k, dev, stream):
+def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1):
     """with-H2D cas_ids: the first k files' staged messages in pinned host memory through
     the drop-in sd_cas_ids (host plan + H2D + kernels + D2H + hex, windows pipelined on two
-    streams), beside the raw H2D copy of the same bytes and the device-resident kernels."""
+    streams), beside the raw H2D copy of the same bytes and the device-resident kernels.
+    Runs on every rank at once (one PCIe link per GPU): a fixed count of calls -- one warm,
+    then 2 timed -- between barriers; the aggregate is all ranks' files over the slowest
+    rank's time."""
     from spacedrive_amd._native import check, lib
     k = min(k, len(ext))
     nbytes = (int(ext["msg_offset"][k - 1]) + int(ext["msg_len"][k - 1]) + 63) // 64 * 64
@@ -227,23 +352,42 @@ def host_staged(ctx, ext, d_staged, k, dev, stream):
     want = hh.cpu().numpy().reshape(k, 32)[:, :8]
     del dbuf, b, hh
     out = ctypes.create_string_buffer(17 * k)
-    e2e = []
-    for _ in range(3):
-        t0 = time.perf_counter()
+
+    def call():
         check(lib().sd_cas_ids(ctx.handle, host.data_ptr(), nbytes, sub.ctypes.data, k, out, None))
-        e2e.append(time.perf_counter() - t0)
+
+    call()  # warm: the context's windows and tables
+    reps = 2
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        call()
+    e2e_s = (time.perf_counter() - t0) / reps
+    if world > 1:
+        dist.barrier()
     raw = out.raw  # one copy: each .raw access copies the whole buffer
     got = np.frombuffer(bytes.fromhex("".join(raw[17 * i:17 * i + 16].decode() for i in range(k))),
                         np.uint8).reshape(k, 8)
     assert np.array_equal(got, want), "sd_cas_ids differs from the device-resident batch"
-    e2e_s = min(e2e[1:])
-    return {"files": k, "bytes": nbytes, "h2d_ms": h2d_ms, "h2d_GBps": nbytes / (h2d_ms * 1e-3) / 1e9,
-            "kernel_ms": kernel_ms, "kernel_files_per_s": k / (kernel_ms * 1e-3),
-            "end_to_end_ms": e2e_s * 1e3, "end_to_end_files_per_s": k / e2e_s,
-            "end_to_end_GBps": nbytes / e2e_s / 1e9,
-            "note": "sd_cas_ids from pinned host memory (best of 2 warm calls): plan + H2D + kernels + D2H + hex, "
-                    "512 MiB windows on two streams; h2d_ms = one raw copy of the same bytes (HIP events); "
-                    "kernel_ms = the same files device-resident"}
+    res = {"files": k, "bytes": nbytes, "h2d_ms": h2d_ms, "h2d_GBps": nbytes / (h2d_ms * 1e-3) / 1e9,
+           "kernel_ms": kernel_ms, "kernel_files_per_s": k / (kernel_ms * 1e-3),
+           "end_to_end_ms": e2e_s * 1e3, "end_to_end_files_per_s": k / e2e_s,
+           "end_to_end_GBps": nbytes / e2e_s / 1e9,
+           "note": "sd_cas_ids from pinned host memory (mean of 2 calls after a warm one, all ranks at once): "
+                   "plan + H2D + kernels + D2H + hex, 512 MiB windows on two streams; h2d_ms = one raw copy of the "
+                   "same bytes (HIP events); kernel_ms = the same files device-resident"}
+    if world > 1:
+        rows = [None] * world
+        dist.all_gather_object(rows, [e2e_s, k, nbytes])
+        per = [{"rank": r, "end_to_end_files_per_s": row[1] / row[0], "end_to_end_GBps": row[2] / row[0] / 1e9}
+               for r, row in enumerate(rows)]
+        slow = max(row[0] for row in rows)
+        res["per_rank"] = per
+        res["aggregate"] = {"ranks": world, "files_per_s": sum(row[1] for row in rows) / slow,
+                            "GBps": sum(row[2] for row in rows) / slow / 1e9,
+                            "note": "all ranks' files and bytes over the slowest rank's time"}
+    return res
 
 
 def checksum_host(ctx, gib: int, dev, stream):
@@ -356,6 +500,13 @@ def _fs_type(path: str) -> str:
     return fstype
 
 
+def _cpu_s() -> float:
+    """user + system CPU seconds of this process so far (every thread, the library's included)"""
+    import resource
+    r = resource.getrusage(resource.RUSAGE_SELF)
+    return r.ru_utime + r.ru_stime
+
+
 def _scratch_dir(need: int) -> str:
     import tempfile
     base = "/dev/shm"
@@ -410,29 +561,76 @@ def latency(ctx, paths, sizes, calls: int) -> dict:
                 "calls": int(v.size), "calls_per_s": v.size / wall}
 
     res = {}
-    for mode, cpu_max in (("gpu_coalesced", 0), ("policy_default", 16)):
+    keep = ctypes.c_int32(0)
+    check(L.sd_cas_get_tuning(b"batch_cpu_max", ctypes.byref(keep)))
+    # gpu_coalesced: every call coalesced AND every coalesced batch on the GPU (both policies
+    # off); policy_default: the library's defaults (CPU below 16 calls in flight, coalesced
+    # batches through sd_cas_ids_files' batch policy)
+    for mode, cpu_max, batch_max in (("gpu_coalesced", 0, 0), ("policy_default", 16, keep.value)):
         check(L.sd_cas_set_tuning(b"latency_cpu_max", cpu_max))
+        check(L.sd_cas_set_tuning(b"batch_cpu_max", batch_max))
         try:
             run(gpu_call, 1, 20)  # warm
             res[mode] = {"idle": run(gpu_call, 1, calls), "concurrent_64": run(gpu_call, 64, max(4, calls // 16))}
         finally:
             check(L.sd_cas_set_tuning(b"latency_cpu_max", 16))
+            check(L.sd_cas_set_tuning(b"batch_cpu_max", keep.value))
     res["cpu_path"] = {"idle": run(cpu_call, 1, calls), "concurrent_64": run(cpu_call, 64, max(4, calls // 16))}
     res["note"] = ("files of the file-backed leg on tmpfs (page cache warm), one generate_cas_id per call through "
-                   "ctypes from Python threads; gpu_coalesced = sd_cas_id_path with latency_cpu_max 0 "
-                   "(200 us window), policy_default = latency_cpu_max 16, cpu_path = sd_cpu_cas_id_path")
+                   "ctypes from Python threads; gpu_coalesced = sd_cas_id_path with latency_cpu_max 0 and "
+                   "batch_cpu_max 0 (every call coalesced, 200 us window, every batch on the GPU); policy_default = "
+                   "the defaults (latency_cpu_max 16; coalesced batches of <= 4096 on the CPU path); "
+                   "cpu_path = sd_cpu_cas_id_path")
     return res
 
 
-def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool, latency_calls: int):
+def identifier_leg(paths, k: int) -> dict:
+    """The identifier job (file_identifier_job.rs:80-309, mod.rs:100-392) over the first k
+    files: 100-row steps by cursor, Object link/create per step.  (a) look-ahead: each
+    hashing call covers the next 32768 orphans (spacedrive_amd/identifier.py IdentifierJob;
+    generate_cas_ids -> sd_cas_ids_files, the GPU route); (b) per step: each step hashes
+    its own 100 files with the library's CPU path on 16 threads (the reference's per-step
+    structure, integration/rust/core/cas.rs without a GPU).  Both give the same Objects.
+    hash_s = time inside the batched hashing calls; job_s = the whole job, whose stat calls
+    (FileMetadata::new's fs::metadata, mod.rs:65-67) and Object bookkeeping are Python here
+    (the reference's bookkeeping is DB writes, out of scope)."""
+    from spacedrive_amd import cas as sdcas
+    from spacedrive_amd import cpu, identifier
+    paths = paths[:k]
+    res = {"files": len(paths), "steps": (len(paths) + 99) // 100}
+    owners = {}
+    for name, k_ahead, hash_batch in (
+            ("lookahead_gpu", identifier.LOOKAHEAD, sdcas.generate_cas_ids),
+            ("per_step_cpu_path", identifier.CHUNK_SIZE, lambda p, s: cpu.generate_cas_ids(p, s, nthreads=16))):
+        acc = [0.0]
+
+        def timed(p, s, fn=hash_batch):
+            t0 = time.perf_counter()
+            r = fn(p, s)
+            acc[0] += time.perf_counter() - t0
+            return r
+        t0 = time.perf_counter()
+        job = identifier.IdentifierJob(paths, lookahead=k_ahead, metadata=identifier._stat_then_hash(timed)).run()
+        job_s = time.perf_counter() - t0
+        owners[name] = job.owner
+        res[name] = {"job_s": job_s, "hash_s": acc[0], "hash_calls": len(job.hash_calls),
+                     "hash_files_per_s": len(paths) / acc[0], "job_files_per_s": len(paths) / job_s,
+                     "created": sum(c for c, _ in job.step_stats), "linked": sum(x for _, x in job.step_stats)}
+    res["same_objects"] = owners["lookahead_gpu"] == owners["per_step_cpu_path"]
+    res["hash_speedup"] = res["per_step_cpu_path"]["hash_s"] / res["lookahead_gpu"]["hash_s"]
+    assert res["same_objects"], "look-ahead and per-step identifier jobs disagree"
+    return res
+
+
+def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool, latency_calls: int, ident_files: int = 0):
     """The drop-in path from files on disk, as identifier_job_step would drive it
     (file_identifier/mod.rs:107-134): the first k files of this shard are written to a
     scratch directory (sampled files sparse: only the windows cas.rs reads are
     materialised), then timed end to end through sd_cas_ids_files (read stager pool
     overlapped with H2D + kernels + D2H), beside the reference's own read schedule
-    (open, read_exact, seek; cas.rs:27-58) + the SIMD C restatement on 1 and 16 threads
-    and the library's CPU path.  All read from the page cache (files just written); the
-    outputs are asserted equal."""
+    (open, read_exact, seek; cas.rs:27-58) + the SIMD C restatement on 1, 16 and all
+    threads and the library's CPU path on 16 and all threads.  All read from the page cache
+    (files just written); the outputs are asserted equal."""
     import shutil
     import spacedrive_amd as sd
     from spacedrive_amd import synth
@@ -446,17 +644,20 @@ def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool, latency_calls
         t0 = time.perf_counter()
         paths = synth.write_files(d, sub_sizes, host, ext[:k])
         write_s = time.perf_counter() - t0
+        del host
         L = lib()
         arr = (ctypes.c_char_p * k)(*[os.fsencode(p) for p in paths])
         threads = 16
+        nA = all_cores()
         out = ctypes.create_string_buffer(17 * k)
         st = np.zeros(k, np.int32)
         sz = np.ascontiguousarray(sub_sizes, np.uint64)
-        pipe = []
+        pipe, pipe_cpu = [], []
         for _ in range(3):  # first run warms the stager's threads and the context's slots
-            t0 = time.perf_counter()
+            c0, t0 = _cpu_s(), time.perf_counter()
             check(L.sd_cas_ids_files(ctx.handle, arr, sz.ctypes.data, k, out, st.ctypes.data, threads))
             pipe.append(time.perf_counter() - t0)
+            pipe_cpu.append(_cpu_s() - c0)
         assert (st == 0).all(), np.unique(st)
         raw = out.raw
         gpu_ids = [raw[17 * i:17 * i + 16].decode() for i in range(k)]
@@ -464,40 +665,48 @@ def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool, latency_calls
         res = {"files": k, "dir_fs": _fs_type(d), "write_s": write_s,
                "message_bytes": int(ext["msg_len"][:k].astype(np.int64).sum()),
                "gpu": {"files_per_s": k / pipe_s, "ms": pipe_s * 1e3, "stage_threads": threads,
-                       "note": "sd_cas_ids_files: read on the library's stager pool into pinned windows, "
-                               "overlapped with H2D + kernels + D2H + hex; best of 2 warm runs"}}
+                       "host_cpu_us_per_file": min(pipe_cpu[1:]) / k * 1e6,
+                       "note": "sd_cas_ids_files: read by the library's stager threads into a ring of pinned "
+                               "windows, overlapped with H2D + kernels + D2H + hex; best of 2 warm runs"}}
         # the CPU legs time the C calls alone (paths encoded once, outside), best of 2 after a warm run
         cpu_out = ctypes.create_string_buffer(17 * k)
         cpu_st = np.zeros(k, np.int32)
-        lib_runs = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            check(L.sd_cpu_cas_ids_files(arr, sz.ctypes.data, k, cpu_out, cpu_st.ctypes.data, threads))
-            lib_runs.append(time.perf_counter() - t0)
-        assert (cpu_st == 0).all(), np.unique(cpu_st)
-        craw = cpu_out.raw
-        cpu_ids = [craw[17 * i:17 * i + 16].decode() for i in range(k)]
-        res["library_cpu_path"] = {"files_per_s": k / min(lib_runs[1:]), "threads": threads,
-                                   "lanes": sd.cpu.simd_lanes(), "note": "sd_cpu_cas_ids_files, best of 2 warm runs"}
-        assert cpu_ids == gpu_ids, "the library's CPU path differs from its GPU path"
+        for nt, key in ((threads, "library_cpu_path"), (nA, "library_cpu_path_all_cores")):
+            lib_runs, lib_cpu = [], []
+            for _ in range(3):
+                c0, t0 = _cpu_s(), time.perf_counter()
+                check(L.sd_cpu_cas_ids_files(arr, sz.ctypes.data, k, cpu_out, cpu_st.ctypes.data, nt))
+                lib_runs.append(time.perf_counter() - t0)
+                lib_cpu.append(_cpu_s() - c0)
+            assert (cpu_st == 0).all(), np.unique(cpu_st)
+            craw = cpu_out.raw
+            assert [craw[17 * i:17 * i + 16].decode() for i in range(k)] == gpu_ids, \
+                "the library's CPU path differs from its GPU path"
+            res[key] = {"files_per_s": k / min(lib_runs[1:]), "threads": nt, "lanes": sd.cpu.simd_lanes(),
+                        "host_cpu_us_per_file": min(lib_cpu[1:]) / k * 1e6,
+                        "note": "sd_cpu_cas_ids_files, best of 2 warm runs"}
+        res["gpu_over_cpu_path_16_threads"] = res["gpu"]["files_per_s"] / res["library_cpu_path"]["files_per_s"]
         if with_cpu:
             from oracle import native
             ol = native.lib()
             got = np.zeros((k, 8), np.uint8)
             cst = np.zeros(k, np.int32)
             cpu = {}
-            for nt, runs in ((1, 1), (threads, 2)):
+            for nt, runs in ((1, 1), (threads, 2), (nA, 2)):
                 dts = []
+                kk = min(k, 50000) if nt == 1 else k  # one thread: a bounded sample (~0.5 s)
                 for _ in range(runs):
                     t0 = time.perf_counter()
-                    ol.sdo_cas_ids_files(arr, native._p(sz), k, native._p(got), native._p(cst), nt, -1)
+                    ol.sdo_cas_ids_files(arr, native._p(sz), kk, native._p(got), native._p(cst), nt, -1)
                     dts.append(time.perf_counter() - t0)
-                cpu[f"threads_{nt}"] = {"files_per_s": k / min(dts), "seconds": min(dts)}
-            assert (cst == 0).all()
+                cpu[f"threads_{nt}"] = {"files_per_s": kk / min(dts), "seconds": min(dts), "files": kk}
+                assert (cst[:kk] == 0).all()
             want = [got[i].tobytes().hex() for i in range(k)]
             res["cpu_reference_schedule"] = cpu
             res["equal_to_cpu"] = want == gpu_ids
             assert res["equal_to_cpu"], "file-backed GPU cas_ids differ from the CPU restatement"
+        if ident_files > 0:
+            res["identifier_job"] = identifier_leg(paths, ident_files)
         if latency_calls > 0:
             res["latency"] = latency(ctx, paths[:2000], sub_sizes[:2000], latency_calls)
         return res
@@ -507,9 +716,10 @@ def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool, latency_calls
 
 def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
     """file_checksum from files on tmpfs (hash.rs:10-24): 256 MiB files through the drop-in
-    sd_file_checksums (1 MiB reads into pinned windows overlapped with H2D + kernels),
-    beside the reference's read schedule + the SIMD C restatement (oracle, 1 and 16
-    threads) and the library's CPU path; outputs asserted equal."""
+    sd_file_checksums (1 MiB reads into pinned windows overlapped with H2D + kernels; the
+    GPU route, "checksum_cpu_max" = 0) and through its default policy, beside the
+    reference's read schedule + the SIMD C restatement (oracle, 1, 16 and all threads) and
+    the library's CPU path (16 and all threads); outputs asserted equal."""
     import shutil
     import spacedrive_amd as sd
     nf = max(1, mib // 256)
@@ -525,33 +735,43 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
             buf.cpu().numpy().tofile(p)
             paths.append(p)
         del buf
-        runs = []
-        for _ in range(3):  # the first run warms the slots' pinned windows and the page cache
-            t0 = time.perf_counter()
-            gpu = sd.file_checksums(paths)
-            runs.append(time.perf_counter() - t0)
-        gpu_s = min(runs[1:])
         total = nf * flen
-        res = {"files": nf, "bytes": total, "dir_fs": _fs_type(d),
-               "gpu": {"GBps": total / gpu_s / 1e9, "seconds": gpu_s, "first_run_s": runs[0],
-                       "note": "sd_file_checksums: hash.rs's 1 MiB reads as parallel preads into 256 MiB pinned "
-                               "windows, two slots alternating (reads overlap H2D + kernels); best of 2 warm runs"}}
-        cpu_runs = []
-        for _ in range(2):
-            t0 = time.perf_counter()
-            lib_cpu = sd.cpu.file_checksums(paths, nthreads=16)
-            cpu_runs.append(time.perf_counter() - t0)
-        res["library_cpu_path"] = {"GBps": total / min(cpu_runs) / 1e9, "threads": 16, "note": "best of 2"}
-        assert lib_cpu == gpu
+        res = {"files": nf, "bytes": total, "dir_fs": _fs_type(d)}
+        gpu = None
+        default_cpu_max = sd.get_tuning("checksum_cpu_max")
+        for key, cpu_max in (("gpu", 0), ("policy_default", default_cpu_max)):
+            sd.set_tuning("checksum_cpu_max", cpu_max)
+            try:
+                runs = []
+                for _ in range(3):  # the first run warms the slots' pinned windows and the page cache
+                    t0 = time.perf_counter()
+                    got = sd.file_checksums(paths)
+                    runs.append(time.perf_counter() - t0)
+            finally:
+                sd.set_tuning("checksum_cpu_max", default_cpu_max)
+            gpu = gpu or got
+            assert got == gpu
+            res[key] = {"GBps": total / min(runs[1:]) / 1e9, "seconds": min(runs[1:]), "first_run_s": runs[0]}
+        res["gpu"]["note"] = ("sd_file_checksums, GPU route: hash.rs's 1 MiB reads as parallel preads into 256 MiB "
+                              "pinned windows, two slots alternating (reads overlap H2D + kernels); best of 2 warm runs")
+        for nt, key in ((16, "library_cpu_path"), (all_cores(), "library_cpu_path_all_cores")):
+            cpu_runs = []
+            for _ in range(2):
+                t0 = time.perf_counter()
+                lib_cpu = sd.cpu.file_checksums(paths, nthreads=nt)
+                cpu_runs.append(time.perf_counter() - t0)
+            res[key] = {"GBps": total / min(cpu_runs) / 1e9, "threads": nt, "note": "best of 2"}
+            assert lib_cpu == gpu
         if with_cpu:
             from oracle import native
             cpu = {}
-            for nt in (1, 16):
+            for nt in (1, 16, all_cores()):
+                sub = paths[:4] if nt == 1 else paths  # one thread: a bounded sample (1 GiB)
                 t0 = time.perf_counter()
-                got, st = native.file_checksums(paths, nthreads=nt, simd=-1)
+                got, st = native.file_checksums(sub, nthreads=nt, simd=-1)
                 dt = time.perf_counter() - t0
-                cpu[f"threads_{nt}"] = {"GBps": total / dt / 1e9, "seconds": dt}
-            assert (st == 0).all() and [g.tobytes().hex() for g in got] == gpu
+                cpu[f"threads_{nt}"] = {"GBps": len(sub) * flen / dt / 1e9, "seconds": dt, "files": len(sub)}
+                assert (st == 0).all() and [g.tobytes().hex() for g in got] == gpu[:len(sub)]
             res["cpu_reference_schedule"] = cpu
         return res
     finally:
@@ -876,13 +1096,49 @@ def main():
                     "note": "the serial steps' event breakdown (steps_serial)"},
         "dedup": dedup_totals,
     }
+    # ---- the timed steps' output, checked (outside the timed regions) --------------------
+    # (1) hashes: a fixed sample of every rank's shard against the C oracle
+    ps = parity_sample(sizes, cids, twins, d_hash, start)
+    bad = torch.tensor([ps["mismatches"], ps["files"]], dtype=torch.int64,
+                       device=dev if args.dist_backend == "nccl" else "cpu")
+    if world > 1:
+        dist.all_reduce(bad)
+    out["parity_sample"] = dict(ps, files=int(bad[1]), mismatches=int(bad[0]), ranks=world,
+                                rank0_first_bad_global_index=ps["first_bad_global_index"])
+    out["parity_sample"].pop("first_bad_global_index")
+    # (2) the exchange, grouping and Object owners: a key slice from every rank, on rank 0
+    out["dedup"]["parity_slice"] = dedup_parity(d_hash, d_valid, n, start, recs, rep, owners, world, dev)
+    out["dedup"]["parity"] = out["dedup"]["parity_slice"]["parity"]
+    # (3) where one exchange's time goes (one more serial call, events at its phases)
+    if rccl is not None:
+        comm.set_timing(True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        rccl(d_hash.view(n, 32), d_valid, n, start, stream=stream)
+        ph = comm.last_phases()
+        comm.set_timing(False)
+        pt = torch.tensor([ph[k] for k in comm.PHASES], dtype=torch.float64,
+                          device=dev if args.dist_backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(pt, op=dist.ReduceOp.MAX)
+        out["dedup"]["phases_ms"] = dict(ph, note="rank 0's call: partition, all-gather of the count rows + their "
+                                                  "copy to the host, the stream's idle gap while the host reads them "
+                                                  "and queues the exchange (the mid-call sync), grouped send/recv, "
+                                                  "group + owners (HIP events on the call's stream)")
+        out["dedup"]["phases_ms_max_over_ranks"] = {k: float(v) for k, v in zip(comm.PHASES, pt.tolist())}
+    assert out["parity_sample"]["mismatches"] == 0, out["parity_sample"]
+    assert out["dedup"]["parity"], out["dedup"]["parity_slice"]
+
     solo = rank == 0 and world == 1 and not args.no_extras
     with_h2d = {}
-    if solo and args.host_staged_files > 0:
-        with_h2d["cas"] = host_staged(ctx, ext, d_staged, args.host_staged_files, dev, stream)
+    if args.host_staged_files > 0 and not args.no_extras:  # every rank: one PCIe link per GPU
+        k_h2d = args.host_staged_files if world == 1 else min(args.host_staged_files, 150_000)
+        with_h2d["cas"] = host_staged(ctx, ext, d_staged, k_h2d, dev, stream, world)
     if solo and args.file_backed_files > 0:
         out["file_backed"] = file_backed(ctx, sizes, ext, d_staged, args.file_backed_files,
-                                         with_cpu=not args.no_cpu_baseline, latency_calls=args.latency_calls)
+                                         with_cpu=not args.no_cpu_baseline, latency_calls=args.latency_calls,
+                                         ident_files=args.identifier_files)
         if "latency" in out["file_backed"]:
             out["latency"] = out["file_backed"].pop("latency")
     del d_staged, recs, rep, owners
@@ -908,7 +1164,7 @@ def main():
         roof = valu_roof(cb.compressions, ck_ms)
         tr_ck = pmc_traffic("k_ck_leaf", cb.blocks * 256)
         out["checksum"] = {"GBps": float(tot.item()), "unit": "GB/s", "per_gpu_GBps": gbps, "ms_per_run": ck_ms,
-                           "workload": f"configs[3]: {nf} x {flen >> 30} GiB files per GPU, full-file BLAKE3",
+                           "workload": f"configs[3]: {nf} x {flen >> 20} MiB files per GPU, full-file BLAKE3",
                            "roofline": {"bound": "valu", "achieved": roof["achieved"], "peak": VALU_PEAK_TOPS,
                                         "unit": "T int32 VALU lane-ops/s", "frac": roof["frac"],
                                         "frac_full_rate": roof["frac_full_rate"], "peak_basis": PEAK_BASIS,

@@ -205,9 +205,10 @@ int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
 /* Drop-in over host memory (pinned or pageable; hash.rs:10-24 on data already read):
  * full BLAKE3 of n byte ranges of `data` -> 65-byte hex each.  Ranges start 16-byte
  * aligned (ranges of 1 MiB or more are placed on 128-B device lines whatever their host
- * start); no byte outside the ranges is read (a range may end where `data` ends).  Consecutive
- * ranges are copied 256 MiB window at a time, larger ranges stream; two windows alternate
- * so the H2D copies overlap the kernels. */
+ * start); no page that holds no range byte is read (a range may end where `data` ends, and
+ * `data` may have unmapped holes between ranges; bytes between two ranges on a page they
+ * share may be copied).  Consecutive ranges are copied 256 MiB window at a time, larger
+ * ranges stream; two windows alternate so the H2D copies overlap the kernels. */
 int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
                  char* out_hex65);
 /* Drop-in: checksums of n files on disk -> 65-byte lowercase hex each (hash.rs:21-23);
@@ -216,7 +217,11 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
  * ("read_threads"); a pipe or device sequentially.  Small files are packed many per
  * pinned window, large ones (or ones that grow while read) streamed window by window,
  * whatever their final length; two windows alternate so host reads overlap the H2D
- * copies and the kernels. */
+ * copies and the kernels.  Batch policy: a call of at most "checksum_cpu_max" files is
+ * hashed by sd_cpu_file_checksums on "read_threads" threads instead -- by default every
+ * call, because from the page cache the host's threads hash faster than PCIe can carry the
+ * bytes to the GPU; 0 = the GPU route for every call. */
+int sd_file_checksums_stats(sd_cas_ctx* ctx, uint64_t out[2]);  /* calls: [0] CPU path, [1] GPU */
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65,
                       int32_t* status);
 
@@ -228,13 +233,16 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
  * "latency_cpu_max" (default 16; 0 = never) single-file calls are in flight on the
  * context, a call is hashed on the calling thread by the CPU path -- one GPU round trip
  * per file costs more than hashing it; beyond that, concurrent calls are coalesced by a
- * dispatcher thread into one staged GPU batch per window (tuning "coalesce_window_us",
- * default 200, or "coalesce_max" requests, default 4096).  Return SD_OK with *status =
+ * dispatcher thread into one batch per window (tuning "coalesce_window_us", default 200,
+ * or "coalesce_max" requests, default 4096), handed to sd_cas_ids_files /
+ * sd_file_checksums -- whose batch policies route it ("batch_cpu_max",
+ * "checksum_cpu_max": with the defaults a coalesced batch is hashed on the CPU path by
+ * the dispatcher's 16 threads; with them at 0, on the GPU).  Return SD_OK with *status =
  * sd_file_status (the hex is written only for SD_FILE_OK). */
 int sd_cas_id_path(sd_cas_ctx* ctx, const char* path, uint64_t size, char* out_hex17, int32_t* status);
 int sd_file_checksum_path(sd_cas_ctx* ctx, const char* path, char* out_hex65, int32_t* status);
-/* [0] single-file requests, [1] GPU batches they were coalesced into, [2] largest batch,
- * [3] requests hashed on the CPU path */
+/* [0] single-file requests, [1] batches they were coalesced into (each routed by the batch
+ * policies), [2] largest batch, [3] requests hashed on their caller's thread (CPU path) */
 int sd_coalescer_stats(sd_cas_ctx* ctx, uint64_t out[4]);
 
 /* ---------------------------------------------------------------- CPU path (no device) */
@@ -393,9 +401,13 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * "sampled_wave_max" (6144) / "whole_wave_max" (512): a cas batch with at most that many
  * sampled / whole-kind files takes the latency kernels (one wave or workgroup per file),
  * a larger one the throughput kernels -- read when the batch is planned; "batch_cpu_max"
- * (4096): sd_cas_ids_files calls of at most that many files take the CPU path.
- * Unknown keys fail with SD_ERR_INVALID. */
+ * (4096): sd_cas_ids_files calls of at most that many files take the CPU path;
+ * "files_ring" (4): pinned window buffers sd_cas_ids_files' readers may fill ahead of the
+ * copies; "checksum_cpu_max" (2147483647): sd_file_checksums calls of at most that many
+ * files take the CPU path (sd_cpu_file_checksums on "read_threads" threads; 0 = the GPU
+ * route always).  Unknown keys fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);
+int sd_cas_get_tuning(const char* key, int* value);
 /* Read-only probe over d_buf[0, bytes) (bytes a multiple of 4096) for calibrating the
  * PMC byte counters on this kernel family's access patterns: pattern 0 = coalesced
  * 16 B/lane streaming, pattern 1 = one lane per 1 KiB chunk reading 4 x 16 B per 64-byte

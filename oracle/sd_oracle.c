@@ -4,7 +4,9 @@
  * TEST INFRASTRUCTURE ONLY.  Built into oracle/build/libsd_oracle.so.  Only tests/,
  * __graft_entry__.smoke() and bench.py's cpu_baseline leg load it, as the checker
  * and as the timed CPU baseline ("kind": "port").  The product library
- * (spacedrive_amd/libsdcas.so) never links or calls it, and has no CPU fallback.
+ * (spacedrive_amd/libsdcas.so) never links or calls it; the library's own CPU path
+ * (spacedrive_amd/csrc/cpu_blake3.cpp, the sd_cpu_* entry points and the batch policies
+ * that route to them) is a separate implementation, checked against this one by tests/.
  *
  * Restates:
  *   generate_cas_id  /root/reference/core/src/object/cas.rs:23-62 (consts :10-15)

@@ -1,6 +1,9 @@
 // stage_bench.c -- host staging microbenchmark: pread threads (mode 0) vs io_uring batches
-// (mode 1) reading the generate_cas_id windows (cas.rs:27-58) of a file list.  Not part
-// of the product; used to choose the stager design.
+// (mode 1) reading the generate_cas_id windows (cas.rs:27-58) of a file list; mode 2 = the
+// preads of mode 0 into a per-thread 128 KiB buffer (cache-hot, as the CPU path reads)
+// instead of each file's slot of one large buffer; mode 3 = mode 2, then the message copied
+// to its slot of the large buffer with non-temporal (streaming) stores; mode 4 = the same
+// with memcpy.  Not part of the product; used to choose the stager design.
 #define _GNU_SOURCE
 #include <fcntl.h>
 #include <linux/io_uring.h>
@@ -14,6 +17,7 @@
 #include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
+#include <immintrin.h>
 
 static int n; static char** paths; static uint64_t* sizes; static uint8_t* buf; static uint64_t* offs;
 static atomic_int cursor; static int mode, B = 64;
@@ -25,14 +29,29 @@ static int wins(uint64_t size, uint64_t off[6], uint64_t len[6]) {
     for (int s = 0; s < 4; s++) { off[k] = 8192 + s * j; len[k++] = 10240; }
     off[k] = size - 8192; len[k++] = 8192; return k;
 }
+static void nt_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {  /* 64-B aligned dst, n % 64 == 0 */
+    for (uint64_t i = 0; i < n; i += 64) {
+        __m128i a = _mm_load_si128((const __m128i*)(src + i)), b = _mm_load_si128((const __m128i*)(src + i + 16));
+        __m128i c = _mm_load_si128((const __m128i*)(src + i + 32)), d = _mm_load_si128((const __m128i*)(src + i + 48));
+        _mm_stream_si128((__m128i*)(dst + i), a); _mm_stream_si128((__m128i*)(dst + i + 16), b);
+        _mm_stream_si128((__m128i*)(dst + i + 32), c); _mm_stream_si128((__m128i*)(dst + i + 48), d);
+    }
+    _mm_sfence();
+}
 static void* w_pread(void* a) {
+    uint8_t* hot = mode >= 2 ? aligned_alloc(4096, 128 << 10) : 0;
+    if (hot) memset(hot, 0, 128 << 10);
     for (;;) {
         int i = atomic_fetch_add(&cursor, 1); if (i >= n) break;
         int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
-        uint64_t o[6], l[6]; int k = wins(sizes[i], o, l); uint8_t* d = buf + offs[i] + 8;
+        uint64_t o[6], l[6]; int k = wins(sizes[i], o, l); uint8_t* d = hot ? hot + 8 : buf + offs[i] + 8;
         for (int q = 0; q < k; q++) { pread(fd, d, l[q], o[q]); d += l[q]; }
         close(fd);
+        uint64_t m = ((sizes[i] <= 102400 ? 8 + sizes[i] : 57352) + 63) / 64 * 64;
+        if (mode == 3) nt_copy(buf + offs[i], hot, m);
+        if (mode == 4) memcpy(buf + offs[i], hot, m);
     }
+    free(hot);
     return 0;
 }
 struct ring { int fd; unsigned *sq_head, *sq_tail, *sq_mask, *sq_array, *cq_head, *cq_tail, *cq_mask; struct io_uring_sqe* sqes; struct io_uring_cqe* cqes; };
@@ -85,7 +104,7 @@ int main(int argc, char** argv) {
     buf = aligned_alloc(4096, (tot + 4095) / 4096 * 4096); memset(buf, 0, tot);
     for (int rep = 0; rep < 3; rep++) {
         atomic_store(&cursor, 0); pthread_t th[64]; double t0 = now();
-        for (int t = 0; t < T; t++) pthread_create(&th[t], 0, mode ? w_uring : w_pread, 0);
+        for (int t = 0; t < T; t++) pthread_create(&th[t], 0, mode == 1 ? w_uring : w_pread, 0);
         for (int t = 0; t < T; t++) pthread_join(th[t], 0);
         double dt = now() - t0; printf("mode %d T %d: %.1f ms, %.0f files/s, %.2f GB/s\n", mode, T, dt * 1e3, n / dt, tot / dt / 1e9);
     }

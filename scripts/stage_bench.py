@@ -1,7 +1,7 @@
 """Writes a synthetic library's first N files (random bytes in the windows generate_cas_id
 reads; sampled files sparse) to a scratch dir and runs scripts/stage_bench.c over them.
 
-    python scripts/stage_bench.py N THREADS
+    python scripts/stage_bench.py N THREADS[,THREADS...] [MODES, e.g. 0,2,0,2]
 """
 import os
 import subprocess
@@ -13,7 +13,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from spacedrive_amd import synth  # noqa: E402
 
-n, T = int(sys.argv[1]), int(sys.argv[2])
+n, Ts = int(sys.argv[1]), [int(t) for t in sys.argv[2].split(",")]
 sizes, _, _ = synth.library(0, n, 1_250_000)
 rng = np.random.default_rng(1)
 d = tempfile.mkdtemp(prefix="sb_", dir="/dev/shm")
@@ -33,8 +33,11 @@ with open(lst, "w") as f:
 exe = os.path.join(tempfile.mkdtemp(prefix="sbx_"), "stage_bench")  # /dev/shm may be noexec
 src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "stage_bench.c")
 subprocess.run(["gcc", "-O2", "-w", "-o", exe, src, "-lpthread"], check=True)
-for mode, b in ((0, 0), (1, 16), (1, 64), (0, 0), (1, 64)):
-    args = [exe, lst, str(T), str(mode)] + ([str(b)] if mode else [])
-    print(" ".join(args[2:]), flush=True)
-    subprocess.run(args, check=True)
+modes = [(int(m), 0) for m in sys.argv[3].split(",")] if len(sys.argv) > 3 else \
+    [(0, 0), (1, 16), (1, 64), (0, 0), (1, 64)]
+for T in Ts:
+    for mode, b in modes:
+        args = [exe, lst, str(T), str(mode)] + ([str(b or 64)] if mode == 1 else [])
+        print(" ".join(args[2:]), flush=True)
+        subprocess.run(args, check=True)
 subprocess.run(["rm", "-rf", d])

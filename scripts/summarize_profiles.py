@@ -45,6 +45,30 @@ def pmc_rows(path):
     return agg
 
 
+def trace_shapes(tag):
+    """(kernel, grid) -> launch durations in µs from the kernel-trace pass, or {}."""
+    shapes = collections.defaultdict(list)
+    tr = glob.glob(os.path.join(OUT, f"prof_{tag}", "*kernel_trace.csv"))
+    if tr:
+        for r in csv.DictReader(open(tr[0])):
+            shapes[(short(r["Kernel_Name"]), int(r["Grid_Size_X"]))].append(
+                (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return shapes
+
+
+def steady(v):
+    st = v[WARMUP:] if len(v) > WARMUP else v
+    return sum(st) / len(st)
+
+
+# The PMC pass's own launch durations include the counter collection's overhead, and
+# GRBM_GUI_ACTIVE counts the GPU's busy cycles around a launch too: for short launches the
+# ratio is no clock (round 2 printed 3.4-28.8 GHz).  The clock column therefore divides by
+# the same launch shape's steady duration in the kernel-trace pass, and only for launches of
+# at least MIN_CLOCK_US, where the overhead is small; others show "-".
+MIN_CLOCK_US = 500.0
+
+
 def main(tag):
     os.makedirs(PROF, exist_ok=True)
     stats = glob.glob(os.path.join(OUT, f"prof_{tag}", "*kernel_stats.csv"))
@@ -60,12 +84,8 @@ def main(tag):
             for r in rows[:20]:
                 f.write(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                         f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.1f} |\n")
-            tr = glob.glob(os.path.join(OUT, f"prof_{tag}", "*kernel_trace.csv"))
-            if tr:  # per launch shape: bench.py's timed launches vs the warm-up ones
-                shapes = collections.defaultdict(list)
-                for r in csv.DictReader(open(tr[0])):
-                    shapes[(short(r["Kernel_Name"]), int(r["Grid_Size_X"]))].append(
-                        (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            shapes = trace_shapes(tag)
+            if shapes:  # per launch shape: bench.py's timed launches vs the warm-up ones
                 f.write("\nPer launch shape (kernel, grid size in work-items) for the hashing kernels, from "
                         "the kernel trace. `steady avg` drops the first `warmup` launches of the shape "
                         "(clock ramp), i.e. it covers the launches bench.py times.\n\n")
@@ -73,8 +93,7 @@ def main(tag):
                 for (k, g), v in sorted(shapes.items(), key=lambda kv: -sum(kv[1])):
                     if not k.startswith(("k_cas", "k_whole", "k_ck", "k_gb", "k_part", "k_owners")):
                         continue
-                    st = v[WARMUP:] if len(v) > WARMUP else v
-                    f.write(f"| `{k}` | {g} | {len(v)} | {sum(v) / len(v):.1f} | {sum(st) / len(st):.1f} | "
+                    f.write(f"| `{k}` | {g} | {len(v)} | {sum(v) / len(v):.1f} | {steady(v):.1f} | "
                             f"{min(v):.1f} |\n")
         print("wrote", dst)
     pmc = {}
@@ -124,22 +143,28 @@ def main(tag):
         f.write(f"# rocprofv3 PMC per launch shape ({tag})\n\nCommand of every pass: `rocprofv3 --pmc <group> -- "
                 f"{PMC_CMD}` (scripts/profile.sh); one counter group per pass.  HBM bytes = FETCH_SIZE x 1024 x "
                 "calibrated factor + WRITE_SIZE x 1024 (factor from `scripts/pmc_calib.py`'s 4 GiB read probes: "
-                f"{ {k: round(v, 4) for k, v in calib.items()} }).  MHz = GRBM_GUI_ACTIVE / 8 XCDs / launch duration "
-                "in the counter pass (GRBM_GUI_ACTIVE sums the 8 XCDs; a lower bound on the shader clock); lane-ops/clk/CU "
-                "= SQ_INSTS_VALU x 64 lanes / (GUI cycles / 8 x 256 CUs): 64 is the 3-operand issue bound (one wave64 "
-                "op per 4 cycles on each of the 4 SIMDs), 128 the guide's full rate.\n\n")
-        f.write("| kernel | grid | HBM GB/launch | VALU wave-insts | GUI cycles | MHz | lane-ops/clk/CU |\n"
-                "|---|---|---|---|---|---|---|\n")
+                f"{ {k: round(v, 4) for k, v in calib.items()} }).  MHz = GRBM_GUI_ACTIVE / 8 XCDs / the same launch "
+                f"shape's steady duration in the kernel-trace pass (`{tag}_summary.md`), shown only for launches of "
+                f"at least {MIN_CLOCK_US:.0f} µs (GRBM_GUI_ACTIVE also counts the busy cycles around a launch, so "
+                "short launches give no clock); lane-ops/clk/CU = SQ_INSTS_VALU x 64 lanes / (GUI cycles / 8 x 256 "
+                "CUs), same rule: 64 is the measured issue ceiling of BLAKE3's G mix (scripts/valu_probe7.hip), "
+                "128 the SIMD-32 full rate.\n\n")
+        f.write("| kernel | grid | HBM GB/launch | VALU wave-insts | GUI cycles | trace µs | MHz | lane-ops/clk/CU |\n"
+                "|---|---|---|---|---|---|---|---|\n")
+        shapes = trace_shapes(tag)
         for k, lst in sorted(kern.items()):
             if not k.startswith(("k_cas", "k_whole", "k_ck", "k_gb", "k_part", "k_owners", "rccl")):
                 continue
             for e in lst:
                 c = e["counters"]
-                gui, dur, valu = c.get("GRBM_GUI_ACTIVE"), c.get("DURATION_NS"), c.get("SQ_INSTS_VALU")
-                mhz = gui / 8 / dur * 1e3 if gui and dur else None
-                ipc = valu * 64 / (gui / 8 * 256) if gui and valu else None
+                gui, valu = c.get("GRBM_GUI_ACTIVE"), c.get("SQ_INSTS_VALU")
+                tr_us = steady(shapes[(k, e["grid"])]) if shapes.get((k, e["grid"])) else None
+                long_enough = tr_us is not None and tr_us >= MIN_CLOCK_US
+                mhz = gui / 8 / tr_us if gui and long_enough else None
+                ipc = valu * 64 / (gui / 8 * 256) if gui and valu and long_enough else None
                 f.write(f"| `{k}` | {e['grid']} | {e['hbm_bytes_per_launch'] / 1e9:.4g} | "
                         f"{'%.4g' % valu if valu is not None else '-'} | {'%.4g' % gui if gui is not None else '-'} | "
+                        f"{'%.1f' % tr_us if tr_us else '-'} | "
                         f"{'%.0f' % mhz if mhz else '-'} | {'%.1f' % ipc if ipc else '-'} |\n")
     print(f"wrote profiles/{tag}_pmc.md")
 

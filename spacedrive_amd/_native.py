@@ -116,6 +116,8 @@ SIGNATURES = [
     ("sd_checksum_batch_time", I32, [P, P, P, P, I32, P, ctypes.POINTER(ctypes.c_float)]),
     ("sd_valu_peak", I32, [P, ctypes.POINTER(ctypes.c_double)]),
     ("sd_cas_set_tuning", I32, [ctypes.c_char_p, I32]),
+    ("sd_cas_get_tuning", I32, [ctypes.c_char_p, ctypes.POINTER(I32)]),
+    ("sd_file_checksums_stats", I32, [P, P]),
     ("sd_read_probe", I32, [P, P, U64, I32, P]),
 ]
 

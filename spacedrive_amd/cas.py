@@ -145,9 +145,24 @@ def coalescer_stats(device: Optional[int] = None) -> dict:
     return {"requests": int(v[0]), "batches": int(v[1]), "max_batch": int(v[2]), "cpu": int(v[3])}
 
 
+def file_checksums_stats(device: Optional[int] = None) -> dict:
+    """Routes taken by file_checksums (sd_file_checksums): calls on the CPU path by the batch
+    policy ("checksum_cpu_max") and calls through the GPU."""
+    v = np.zeros(2, np.uint64)
+    check(lib().sd_file_checksums_stats(default_context(device).handle, _ptr(v)))
+    return {"cpu": int(v[0]), "gpu": int(v[1])}
+
+
 def set_tuning(key: str, value: int) -> None:
     """sd_cas_set_tuning (process-wide knobs, include/sd_cas.h)."""
     check(lib().sd_cas_set_tuning(key.encode(), int(value)))
+
+
+def get_tuning(key: str) -> int:
+    """sd_cas_get_tuning."""
+    v = ctypes.c_int32(0)
+    check(lib().sd_cas_get_tuning(key.encode(), ctypes.byref(v)))
+    return int(v.value)
 
 
 @dataclass

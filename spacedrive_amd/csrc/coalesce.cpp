@@ -11,7 +11,10 @@
 // context waits for the first request, keeps collecting for a short window (tuning
 // "coalesce_window_us", default 200) or until "coalesce_max" requests (default 4096) are
 // queued, then hashes the whole batch with one sd_cas_ids_files / sd_file_checksums
-// call.  Requests that arrive meanwhile form the next batch, so a busy watcher is served
+// call -- whose batch policies pick the route: with the defaults ("batch_cpu_max" 4096,
+// "checksum_cpu_max" all) a coalesced batch is hashed on the CPU path's 16 threads, which
+// bounds the threads a burst of callers occupies; with the policies at 0 it goes to the
+// GPU.  Requests that arrive meanwhile form the next batch, so a busy watcher is served
 // at batch throughput and an idle one at CPU latency.  Each caller blocks only on its own
 // request.
 #include <string.h>

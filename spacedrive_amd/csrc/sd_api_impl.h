@@ -204,6 +204,7 @@ struct sd_cas_ctx {
     std::mutex coal_mu;
     sd_coalescer* coal = nullptr;  // latency path, created on the first single-file call
     std::atomic<uint64_t> files_calls_cpu{0}, files_calls_gpu{0};  // sd_cas_ids_files routes
+    std::atomic<uint64_t> checksum_calls_cpu{0}, checksum_calls_gpu{0};  // sd_file_checksums routes
     std::mutex pool_mu;
     // File stager threads (sd_cas_ids_files).  One pool per context, grown to the largest
     // thread count any call asked for; a caller holds its shared_ptr while it runs, so a

@@ -331,10 +331,23 @@ void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes,
                 if (ev[k]) (void)hipEventDestroy(ev[k]);
         }
     } cleanup{pool.get(), &sh, false, copied};
-    for (int r = 0; r < RING; r++) HIP_CHECK(hipEventCreateWithFlags(&copied[r], hipEventDisableTiming));
+    // this thread's waits block (hipEventBlockingSync) instead of spinning: the readers need
+    // the cores (a container's CPU quota counts a spinning waiter as a busy core)
+    for (int r = 0; r < RING; r++)
+        HIP_CHECK(hipEventCreateWithFlags(&copied[r], hipEventDisableTiming | hipEventBlockingSync));
+    hipEvent_t done_ev[2] = {nullptr, nullptr};  // a device slot's last D2H / scatter
+    struct EvGuard {
+        hipEvent_t* e;
+        ~EvGuard() {
+            for (int k = 0; k < 2; k++)
+                if (e[k]) (void)hipEventDestroy(e[k]);
+        }
+    } done_guard{done_ev};
+    for (int k = 0; k < 2; k++)
+        HIP_CHECK(hipEventCreateWithFlags(&done_ev[k], hipEventDisableTiming | hipEventBlockingSync));
     auto harvest = [&](int k) {
         if (!launched[k].busy) return;
-        HIP_CHECK(hipStreamSynchronize(slots[k].stream));
+        HIP_CHECK(hipEventSynchronize(done_ev[k]));
         const uint8_t* h = slots[k].host_hashes.u8();
         if (out_hex17)
             for (size_t q = 0; q < launched[k].files.size(); q++)
@@ -412,6 +425,7 @@ void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes,
             } else {
                 HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, m * 32, hipMemcpyDeviceToHost, sl.stream));
             }
+            HIP_CHECK(hipEventRecord(done_ev[k], sl.stream));
             launched[k].files = widx;
             launched[k].busy = true;
         }
@@ -512,6 +526,15 @@ int sd_cas_hashes_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65, int32_t* status) {
     SD_GUARD_BEGIN
     if (!ctx || (n && (!paths || !out_hex65 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    // batch policy: from the page cache the host's threads hash faster than PCIe carries
+    // the bytes, so by default every call takes the CPU path;
+    // "checksum_cpu_max" = 0 sends every call to the GPU route below
+    if (n <= (size_t)std::max(0, tuning_get(SD_TUNE_CHECKSUM_CPU_MAX))) {
+        ctx->checksum_calls_cpu.fetch_add(1, std::memory_order_relaxed);
+        return sd_cpu_file_checksums(paths, n, out_hex65, status,
+                                     std::max(1, std::min(64, tuning_get(SD_TUNE_READ_THREADS))));
+    }
+    ctx->checksum_calls_gpu.fetch_add(1, std::memory_order_relaxed);
     ctx->bind();
     // packs of at most 32 MiB: a pack is read whole before its copy starts, so smaller packs
     // let the next pack's reads overlap this one's H2D and kernels (one 80 MB pack of 100
@@ -748,10 +771,14 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
             continue;
         }
         // the next window: consecutive ranges whose device layout fits W.  Ranges keep their
-        // host-relative offsets, so a run of them is one H2D, except that a range of a leaf
-        // block or more that would start mid-line on the device opens a new run at the next
-        // 128-B line (a mid-line start costs k_ck_leaf 5%); only ascending,
-        // non-overlapping ranges open runs
+        // host-relative offsets, so a run of them is one H2D, except that
+        //  * a gap that holds a whole page no range touches opens a new run (the copy of a
+        //    run reads its gaps: only pages that hold range bytes may be read, since the
+        //    caller's buffer can have unmapped holes between ranges);
+        //  * a range of a leaf block or more that would start mid-line on the device opens a
+        //    new run at the next 128-B line (a mid-line start costs k_ck_leaf 5%, DESIGN.md
+        //    §3.2b).
+        // Only ascending, non-overlapping ranges open runs.
         runs.clear();
         offs.clear();
         ls.clear();
@@ -761,7 +788,8 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
             const uint64_t o = offsets[j], L = lens[j];
             const RunT* r = runs.empty() ? nullptr : &runs.back();
             const bool misaligned = r && (r->dev_lo + (o - r->host_lo)) % SD_STAGE_ALIGN != 0;
-            const bool open = !r || (o >= r->host_end && L >= SD_CK_BLOCK && misaligned);
+            const bool page_gap = r && o >= r->host_end && align_up(r->host_end, 4096) + 4096 <= o;
+            const bool open = !r || page_gap || (o >= r->host_end && L >= SD_CK_BLOCK && misaligned);
             if (r && !open && o < r->host_lo) break;  // before its run: the next window takes it
             const uint64_t dev_lo = open ? (r ? align_up(dev_hi, SD_STAGE_ALIGN) : 0) : r->dev_lo;
             const uint64_t host_lo = open ? o : r->host_lo;

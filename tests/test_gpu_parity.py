@@ -31,13 +31,17 @@ def ctx():
 
 @pytest.fixture(scope="module", autouse=True)
 def _gpu_route_for_batches():
-    """sd_cas_ids_files hashes calls of up to "batch_cpu_max" files on the CPU path; the
-    parity tests below exercise the GPU route, so the module turns the policy off (the
-    policy has its own test) and restores the library default after."""
+    """sd_cas_ids_files hashes calls of up to "batch_cpu_max" files on the CPU path, and
+    sd_file_checksums calls of up to "checksum_cpu_max" (by default all); the parity tests
+    below exercise the GPU routes, so the module turns both policies off (the policies have
+    their own tests) and restores the library defaults after."""
     import spacedrive_amd as sd
+    keep = {k: sd.get_tuning(k) for k in ("batch_cpu_max", "checksum_cpu_max")}
     sd.set_tuning("batch_cpu_max", 0)
+    sd.set_tuning("checksum_cpu_max", 0)  # sd_file_checksums: its GPU route (the default is the CPU path)
     yield
-    sd.set_tuning("batch_cpu_max", 4096)
+    for k, v in keep.items():
+        sd.set_tuning(k, v)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -1035,6 +1039,93 @@ def test_checksums_host_ranges_end_at_a_guard_page(ctx, oracle_native):
         assert libc.mprotect(ctypes.c_void_p(base + npages * page), page, 3) == 0  # back to RW
         del data, whole
         m.close()
+
+
+def test_checksums_host_ranges_around_a_guard_page(ctx, oracle_native):
+    """ranges on both sides of an unreadable page inside one window -- small
+    ranges (which share a run with their neighbours) included -- are hashed without reading
+    the hole: a gap that holds a whole page no range touches starts a new H2D run."""
+    import ctypes
+    import mmap
+    from spacedrive_amd._native import check, lib
+    page = mmap.PAGESIZE
+    m = mmap.mmap(-1, 6 * page)
+    whole = np.frombuffer(m, dtype=np.uint8)
+    rng = np.random.default_rng(5)
+    whole[:] = rng.integers(0, 256, whole.size, dtype=np.uint8)
+    base = whole.ctypes.data
+    libc = ctypes.CDLL(None, use_errno=True)
+    hole = 3 * page  # pages [3, 4) unreadable
+    # before the hole: two small ranges sharing page 2; after it: small ranges on page 4, 5
+    offs = [2 * page + 16, 2 * page + 1024, 3 * page - 48, hole + page, hole + page + 80, 5 * page + 16]
+    lens = [100, 2000, 48, 64, 1000, page - 32]
+    assert libc.mprotect(ctypes.c_void_p(base + hole), page, 0) == 0
+    try:
+        arr_o = np.array(offs, np.uint64)
+        arr_l = np.array(lens, np.uint64)
+        out = ctypes.create_string_buffer(65 * len(lens))
+        check(lib().sd_checksums(ctx.handle, base, arr_o.ctypes.data, arr_l.ctypes.data, len(lens), out))
+    finally:
+        assert libc.mprotect(ctypes.c_void_p(base + hole), page, 3) == 0
+    padded = np.concatenate([whole, np.zeros(128, np.uint8)])
+    want = oracle_native.checksums_simd(padded, arr_o, arr_l, nthreads=NT)
+    raw = out.raw
+    for i in range(len(lens)):
+        assert raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), i
+    del whole
+    m.close()
+
+
+def test_coalesced_batches_take_the_batch_policies(ctx, tmp_path):
+    """beyond "latency_cpu_max" calls in flight, single-file calls are coalesced
+    and the dispatcher hands each batch to sd_cas_ids_files / sd_file_checksums, whose batch
+    policies then route it: with the defaults a coalesced batch (at most "coalesce_max" =
+    4096 files) is hashed on the CPU path, with the policies off on the GPU.  Same results."""
+    import threading
+    import spacedrive_amd as sd
+    from oracle import native
+    sizes = [1, 1017, 102400, 102401, 700_000] * 8
+    paths = []
+    for i, s in enumerate(sizes):
+        p = tmp_path / f"c{i}.bin"
+        p.write_bytes(native.synth_bytes(500 + i, 0, 0, s))
+        paths.append(str(p))
+    want_ids = sd.generate_cas_ids(paths, sizes)
+    want_sums = sd.file_checksums(paths)
+
+    def burst():
+        ids, sums = [None] * len(paths), [None] * len(paths)
+        barrier = threading.Barrier(len(paths))
+
+        def worker(i):
+            barrier.wait()
+            ids[i] = sd.generate_cas_id(paths[i], sizes[i])
+            sums[i] = sd.file_checksum(paths[i])
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(len(paths))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return ids, sums
+
+    keep = {k: sd.get_tuning(k) for k in ("batch_cpu_max", "checksum_cpu_max")}
+    sd.set_tuning("latency_cpu_max", 0)  # every single-file call is coalesced
+    try:
+        for policy in ("default", "off"):
+            sd.set_tuning("batch_cpu_max", 4096 if policy == "default" else 0)
+            sd.set_tuning("checksum_cpu_max", 2147483647 if policy == "default" else 0)
+            c0, k0 = sd.cas_ids_files_stats(), sd.file_checksums_stats()
+            ids, sums = burst()
+            c1, k1 = sd.cas_ids_files_stats(), sd.file_checksums_stats()
+            assert ids == want_ids and sums == want_sums, policy
+            route = "cpu" if policy == "default" else "gpu"
+            other = "gpu" if route == "cpu" else "cpu"
+            assert c1[route] > c0[route] and c1[other] == c0[other], (policy, c0, c1)
+            assert k1[route] > k0[route] and k1[other] == k0[other], (policy, k0, k1)
+    finally:
+        sd.set_tuning("latency_cpu_max", 16)
+        for k, v in keep.items():
+            sd.set_tuning(k, v)
 
 
 def test_split_checksum_ranks_on_one_gpu(ctx, oracle_native):

@@ -118,7 +118,13 @@ def test_lookahead_job_on_the_gpu_route(library):
     more than batch_cpu_max files takes the GPU route."""
     import spacedrive_amd as sd
     paths, want_owner, want_stats, _ = library
-    before = sd.cas_ids_files_stats()["gpu"]
-    job = IdentifierJob(paths, lookahead=32768).run()
+    keep = sd.get_tuning("batch_cpu_max")
+    sd.set_tuning("batch_cpu_max", 1000)  # this library (2345 files) is one call above the threshold
+    try:
+        before = sd.cas_ids_files_stats()
+        job = IdentifierJob(paths, lookahead=32768).run()
+        after = sd.cas_ids_files_stats()
+    finally:
+        sd.set_tuning("batch_cpu_max", keep)
     _check(job, want_owner, want_stats)
-    assert sd.cas_ids_files_stats()["gpu"] > before
+    assert job.hash_calls[0] > 1000 and after["gpu"] > before["gpu"]
