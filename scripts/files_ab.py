@@ -51,7 +51,15 @@ def main():
         a, b = ctypes.create_string_buffer(17 * k), ctypes.create_string_buffer(17 * k)
         keep = sd.get_tuning("batch_cpu_max")
         sd.set_tuning("batch_cpu_max", 0)
-        routes = {"gpu": lambda: L.sd_cas_ids_files(ctx.handle, arr, sz.ctypes.data, k, a, st.ctypes.data, th),
+        def gpu(hot):
+            def run():
+                sd.set_tuning("files_stage_hot", hot)
+                try:
+                    return L.sd_cas_ids_files(ctx.handle, arr, sz.ctypes.data, k, a, st.ctypes.data, th)
+                finally:
+                    sd.set_tuning("files_stage_hot", 0)
+            return run
+        routes = {"gpu": gpu(0), "gpu_stage_hot": gpu(1),
                   "cpu_path": lambda: L.sd_cpu_cas_ids_files(arr, sz.ctypes.data, k, b, st.ctypes.data, th)}
         res = {r: {"s": [], "cpu_s": []} for r in routes}
         for r in routes:  # warm both
@@ -63,6 +71,8 @@ def main():
                 res[r]["s"].append(time.perf_counter() - t0)
                 res[r]["cpu_s"].append(cpu_s() - c0)
         sd.set_tuning("batch_cpu_max", keep)
+        assert a.raw == b.raw
+        check(routes["gpu_stage_hot"]())
         assert a.raw == b.raw
         for r, v in res.items():
             s = np.array(v["s"])

@@ -19,6 +19,8 @@
 #include <functional>
 #include <mutex>
 
+#include <emmintrin.h>
+
 #include "sd_api_impl.h"
 
 using namespace sdi;
@@ -196,6 +198,28 @@ struct Streamer {
 };
 
 
+// A reader thread's cache-resident staging buffer (the longest cas message, padded).
+uint8_t* hot_buffer() {
+    thread_local std::vector<uint8_t> buf(SD_WHOLE_ITEMS_MAX + 256 + 64);
+    return reinterpret_cast<uint8_t*>(align_up(reinterpret_cast<uintptr_t>(buf.data()), 64));
+}
+
+// n bytes (a multiple of 64) from a cache-resident buffer to a 64-byte aligned destination
+// with streaming stores: the destination's lines are written without being read first
+void stream_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    for (uint64_t o = 0; o < n; o += 64) {
+        const __m128i a = _mm_load_si128(reinterpret_cast<const __m128i*>(src + o));
+        const __m128i b = _mm_load_si128(reinterpret_cast<const __m128i*>(src + o + 16));
+        const __m128i c = _mm_load_si128(reinterpret_cast<const __m128i*>(src + o + 32));
+        const __m128i d = _mm_load_si128(reinterpret_cast<const __m128i*>(src + o + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + o), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + o + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + o + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + o + 48), d);
+    }
+    _mm_sfence();
+}
+
 // Hashes (GPU, streaming) the whole-file cas message of a file that held more bytes than
 // its staged extent could take: le64(size) || every byte fs::read returns (cas.rs:25,29).
 int32_t cas_overflow(SlotPair& sl, int& cur, Streamer& st, const char* path, uint64_t size, uint8_t out32[32]) {
@@ -361,6 +385,7 @@ void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes,
         else HIP_CHECK(hipMemcpy(d_hash32 + 32 * f, h, 32, hipMemcpyHostToDevice));
     };
     // ---- the readers: file i into its window's ring buffer
+    const bool stage_hot = tuning_get(SD_TUNE_FILES_STAGE_HOT) != 0;
     pool->start(n, [&](size_t i) {
         const uint32_t w = win_of[i];
         const int r = (int)(w % (uint32_t)RING);
@@ -370,7 +395,18 @@ void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes,
         }
         if (sh.abort.load(std::memory_order_relaxed)) return;
         std::vector<uint8_t> cap;
-        status[i] = stage_one(paths[i], ext[i], ring_buf[r], &cap);
+        if (stage_hot) {  // read into this thread's cache-resident buffer, then stream it out
+            sd_extent e = ext[i];
+            e.msg_offset = 0;
+            uint8_t* hot = hot_buffer();
+            status[i] = stage_one(paths[i], e, hot, &cap);
+            if (status[i] == SD_FILE_OK) {
+                stream_copy(ring_buf[r] + ext[i].msg_offset, hot, sd_align_up(e.msg_len, SD_STAGE_PAD));
+                ext[i].msg_len = e.msg_len;
+            }
+        } else {
+            status[i] = stage_one(paths[i], ext[i], ring_buf[r], &cap);
+        }
         if (!cap.empty()) {
             std::lock_guard<std::mutex> g(sh.mu);
             sh.captured.emplace_back(i, std::move(cap));

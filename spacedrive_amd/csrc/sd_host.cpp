@@ -24,11 +24,11 @@ thread_local std::string g_err;
 // the crossovers lie between 4096 and 8192 sampled files, 256 and 1024 whole-kind files),
 // sd_cas_ids_files calls of up to 4096 files on the CPU path (profiles/r2/r2z6_batch_sizes.json:
 // from the page cache the host's 16 threads beat the GPU route up to ~8000 files a call)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}};
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {0}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
                                                "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",
-                                               "files_ring",         "checksum_cpu_max"};
+                                               "files_ring",         "checksum_cpu_max", "files_stage_hot"};
 }  // namespace
 
 void sd_set_err(const char* fmt, ...) {

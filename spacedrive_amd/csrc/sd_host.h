@@ -57,7 +57,8 @@ enum sd_tune_key {
     SD_TUNE_BATCH_CPU_MAX = 8,    // sd_cas_ids_files: calls of at most this many files take the CPU path
     SD_TUNE_FILES_RING = 9,       // sd_cas_ids_files: pinned window buffers the readers may fill ahead
     SD_TUNE_CHECKSUM_CPU_MAX = 10,  // sd_file_checksums: calls of at most this many files take the CPU path
-    SD_TUNE_NKEYS = 11
+    SD_TUNE_FILES_STAGE_HOT = 11,   // sd_cas_ids_files: read into a per-thread buffer, stream-copy to the window
+    SD_TUNE_NKEYS = 12
 };
 int tuning_get(int key);
 

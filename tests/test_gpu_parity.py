@@ -511,9 +511,13 @@ def test_concurrent_callers_share_a_context(ctx, tmp_path):
     assert not errors, errors
 
 
-def test_cas_ids_files_pipelined_windows(ctx, tmp_path, oracle_native):
-    """sd_cas_ids_files over many 1 MiB windows (stage k+1 while k hashes), with I/O
-    errors and short files interleaved, equals the reference read schedule on the CPU."""
+@pytest.mark.parametrize("ring,hot", [(4, 0), (2, 0), (16, 1)])
+def test_cas_ids_files_pipelined_windows(ctx, tmp_path, oracle_native, ring, hot):
+    """sd_cas_ids_files over many 1 MiB windows (the readers run ahead through a ring of
+    `ring` pinned windows while earlier windows are copied and hashed), with I/O errors and
+    short files interleaved, equals the reference read schedule on the CPU -- with the
+    readers writing the windows directly and through their cache-resident buffer
+    ("files_stage_hot")."""
     import spacedrive_amd as sd
     from spacedrive_amd import synth
     from spacedrive_amd._native import lib
@@ -534,11 +538,15 @@ def test_cas_ids_files_pipelined_windows(ctx, tmp_path, oracle_native):
     plan[small[0]] = int(sizes[small[0]]) + 50  # whole kind, the file is shorter than planned
     plan[small[1]] = int(sizes[small[1]]) - 50  # whole kind, the file is longer than planned
     want, wst = oracle_native.cas_ids_files(paths, np.array(plan, np.uint64), nthreads=4)
-    assert lib().sd_cas_set_tuning(b"files_window_mb", 1) == 0
+    keep = {k: sd.get_tuning(k) for k in ("files_window_mb", "files_ring", "files_stage_hot")}
+    sd.set_tuning("files_window_mb", 1)
+    sd.set_tuning("files_ring", ring)
+    sd.set_tuning("files_stage_hot", hot)
     try:
         got = sd.generate_cas_ids(paths, plan)
     finally:
-        lib().sd_cas_set_tuning(b"files_window_mb", 32)
+        for k, v in keep.items():
+            sd.set_tuning(k, v)
     for i in range(n):
         if wst[i] == 0:
             assert got[i] == want[i].tobytes().hex(), i
