@@ -333,7 +333,8 @@ void parallel_for(size_t n, int nthreads, F fn) {
     }
     // worker threads persist across calls in pools keyed by thread count (creating the
     // threads per call cost a 16-file call ~0.4 ms, most of its time); a pool serves one
-    // call at a time, so concurrent callers take separate pools
+    // call at a time, so concurrent callers take separate pools.  The workers run on
+    // private fd tables (stage_pool.h): every task opens and closes its own files
     static std::mutex mu;
     static std::vector<std::unique_ptr<StagePool>> idle[257];
     std::unique_ptr<StagePool> pool;
@@ -344,7 +345,7 @@ void parallel_for(size_t n, int nthreads, F fn) {
             idle[nthreads].pop_back();
         }
     }
-    if (!pool) pool = std::make_unique<StagePool>(nthreads);
+    if (!pool) pool = std::make_unique<StagePool>(nthreads, true);  // tasks open their own files
     struct Back {
         std::unique_ptr<StagePool>& p;
         int k;
@@ -470,7 +471,11 @@ int sd_cpu_file_checksums(const char* const* paths, size_t n, char* out_hex65, i
         const uint64_t off = task.block * SD_CK_BLOCK;
         const uint64_t want = std::min<uint64_t>(SD_CK_BLOCK, b.len - off);
         uint8_t* buf = scratch(SD_CK_BLOCK);
-        if (pread_full(b.fd, buf, want, off) != (int64_t)want) {  // shrank (or an error): read loop below
+        // the task's own descriptor: pool workers have private fd tables (stage_pool.h)
+        const int fd = open(paths[b.file], O_RDONLY | O_CLOEXEC);
+        const int64_t got = fd < 0 ? -1 : pread_full(fd, buf, want, off);
+        if (fd >= 0) close(fd);
+        if (got != (int64_t)want) {  // shrank, replaced, or an error: the read loop below
             b.failed.store(true, std::memory_order_relaxed);
             return;
         }

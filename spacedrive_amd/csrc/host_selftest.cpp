@@ -420,6 +420,37 @@ void test_coalescer() {
 
 }  // namespace
 
+// ------------------------------------------------------------------ private fd tables
+// A pool with private fd tables (stage_pool.h) must not keep the process's descriptors
+// alive: its workers drop their copies at start, so a pipe's write end closed by the main
+// thread reads as EOF; and its tasks, opening their own files, read them correctly.
+void test_private_fd_tables() {
+    int p[2];
+    CHECK(pipe(p) == 0);
+    {
+        StagePool pool(6, true);
+        const std::string f = g_dir + "/fdtab";
+        {
+            FILE* w = fopen(f.c_str(), "wb");
+            for (int i = 0; i < 4096; i++) fputc(i & 0xFF, w);
+            fclose(w);
+        }
+        std::atomic<int> good{0};
+        pool.run(64, [&](size_t i) {
+            const int fd = open(f.c_str(), O_RDONLY | O_CLOEXEC);
+            uint8_t b = 0;
+            if (fd >= 0 && pread(fd, &b, 1, (off_t)i) == 1 && b == (uint8_t)i) good++;
+            if (fd >= 0) close(fd);
+        });
+        CHECK(good.load() == 64);
+        close(p[1]);  // the only write end left open anywhere
+        fcntl(p[0], F_SETFL, O_NONBLOCK);
+        char c;
+        CHECK(read(p[0], &c, 1) == 0);  // EOF: no worker kept a copy of the write end
+    }
+    close(p[0]);
+}
+
 // ------------------------------------------------------------------ multi-GPU plans
 void test_exchange_plan() {
     // 3 ranks: rows [to0, to1, to2, base, n, capacity, valid]
@@ -482,6 +513,7 @@ int main() {
     test_cpu_batches();
     test_coalescer();
     test_exchange_plan();
+    test_private_fd_tables();
     // clean up the scratch directory
     if (DIR* d = opendir(g_dir.c_str())) {
         while (dirent* e = readdir(d))

@@ -206,14 +206,22 @@ struct sd_cas_ctx {
     std::atomic<uint64_t> files_calls_cpu{0}, files_calls_gpu{0};  // sd_cas_ids_files routes
     std::atomic<uint64_t> checksum_calls_cpu{0}, checksum_calls_gpu{0};  // sd_file_checksums routes
     std::mutex pool_mu;
-    // File stager threads (sd_cas_ids_files).  One pool per context, grown to the largest
-    // thread count any call asked for; a caller holds its shared_ptr while it runs, so a
-    // concurrent call that grows the pool never destroys one in use.
-    std::shared_ptr<StagePool> pool;
+    // Reader threads.  stage_pool: tasks that open and close their own files (the cas
+    // stager, checksum packs), on private fd tables (stage_pool.h); io_pool: parallel preads
+    // of a descriptor the caller opened (a streamed checksum), on the shared table.  One of
+    // each per context, grown to the largest thread count any call asked for; a caller holds
+    // its shared_ptr while it runs, so a concurrent call that grows a pool never destroys
+    // one in use.
+    std::shared_ptr<StagePool> pool, iopool;
     std::shared_ptr<StagePool> stage_pool(int nthreads) {
         std::lock_guard<std::mutex> g(pool_mu);
-        if (!pool || pool->threads() < nthreads) pool = std::make_shared<StagePool>(nthreads);
+        if (!pool || pool->threads() < nthreads) pool = std::make_shared<StagePool>(nthreads, true);
         return pool;
+    }
+    std::shared_ptr<StagePool> io_pool(int nthreads) {
+        std::lock_guard<std::mutex> g(pool_mu);
+        if (!iopool || iopool->threads() < nthreads) iopool = std::make_shared<StagePool>(nthreads, false);
+        return iopool;
     }
     sd_coalescer* coalescer() {
         std::lock_guard<std::mutex> g(coal_mu);

@@ -295,7 +295,8 @@ int sd_cas_stage_files(const char* const* paths, sd_extent* extents, size_t n, u
     if (nthreads < 1) nthreads = 1;
     if ((size_t)nthreads > n) nthreads = n ? (int)n : 1;
     std::atomic<size_t> cursor{0};
-    auto work = [&]() {
+    auto work = [&](bool own_table) {
+        if (own_table) private_fd_table();  // a thread of this call: its own fd table (stage_pool.h)
         for (;;) {
             const size_t i = cursor.fetch_add(1, std::memory_order_relaxed);
             if (i >= n) break;
@@ -303,8 +304,8 @@ int sd_cas_stage_files(const char* const* paths, sd_extent* extents, size_t n, u
         }
     };
     std::vector<std::thread> pool;
-    for (int t = 1; t < nthreads; t++) pool.emplace_back(work);
-    work();
+    for (int t = 1; t < nthreads; t++) pool.emplace_back(work, true);
+    work(false);
     for (auto& th : pool) th.join();
     return SD_OK;
     SD_GUARD_END

@@ -576,7 +576,9 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
     // let the next pack's reads overlap this one's H2D and kernels (one 80 MB pack of 100
     // files took 4.7 ms against 2.3 ms for the CPU path, read-bound alike)
     constexpr uint64_t PACK = 32ull << 20;
-    std::shared_ptr<StagePool> pool = ctx->stage_pool(std::max(1, std::min(64, tuning_get(SD_TUNE_READ_THREADS))));
+    const int read_threads = std::max(1, std::min(64, tuning_get(SD_TUNE_READ_THREADS)));
+    std::shared_ptr<StagePool> pool = ctx->stage_pool(read_threads);  // per-file tasks (stat, packs)
+    std::shared_ptr<StagePool> iopool;  // preads of one open file (streamed files), created on first use
     SlotPair slots(ctx);
     Streamer::prepare(slots);
     // stat every file in parallel: its length picks the route (regular files only)
@@ -618,7 +620,8 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
         const bool reg = fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
         MsgSource src(fd, MsgSource::CHECKSUM_READS);
         if (reg) {
-            src.set_parallel(pool.get());
+            if (!iopool) iopool = ctx->io_pool(read_threads);
+            src.set_parallel(iopool.get());
             src.set_eof_hint((uint64_t)st.st_size);  // a window-multiple file ends with its last window
         }
         try {

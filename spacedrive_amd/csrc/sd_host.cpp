@@ -5,6 +5,8 @@
 
 #include <errno.h>
 #include <fcntl.h>
+#include <sched.h>
+#include <sys/syscall.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -325,6 +327,20 @@ void plan_checksum(CkPlan& p, const uint64_t* offsets, const uint64_t* lens, siz
 }
 
 // ------------------------------------------------------------------ file reading
+void private_fd_table() {
+#if defined(__SANITIZE_THREAD__)
+    // ThreadSanitizer tracks descriptors by number across threads: fd 3 of two private
+    // tables would read as one descriptor raced on.  The TSan build keeps the shared table.
+    return;
+#endif
+    if (unshare(CLONE_FILES) != 0) return;  // not permitted here: keep the shared table
+#ifdef SYS_close_range
+    if (syscall(SYS_close_range, 3u, ~0u, 0u) == 0) return;
+#endif
+    const long hi = sysconf(_SC_OPEN_MAX);
+    for (long fd = 3; fd < (hi > 0 ? hi : 1024); fd++) close((int)fd);
+}
+
 namespace {
 
 // read exactly n bytes at off (read_exact after a seek); 0, SD_FILE_SHORT_READ or io_status

@@ -11,11 +11,21 @@
 #include <thread>
 #include <vector>
 
+// A worker thread of a pool made with private_fds = true runs on its own copy of the
+// process's file-descriptor table, emptied of every inherited descriptor but stdio
+// (unshare(CLONE_FILES) + close_range(3, ~0)): every open()/close() of the process
+// otherwise serialises on one table lock, and with 16 threads opening and closing one
+// file per task that lock -- not the reads -- bounded the stager and the CPU path
+// (scripts/stage_bench.c mode 5).  Tasks on such a pool must open and
+// close their own files: a descriptor opened by another thread is not valid there.
+void private_fd_table();
+
 class StagePool {
 public:
-    explicit StagePool(int nthreads) {
+    explicit StagePool(int nthreads, bool private_fds = false) : private_fds_(private_fds) {
         for (int t = 1; t < nthreads; t++) th_.emplace_back([this] { worker(); });
     }
+    bool private_fds() const { return private_fds_; }
     ~StagePool() {
         {
             std::lock_guard<std::mutex> g(mu_);
@@ -75,6 +85,7 @@ private:
         }
     }
     void worker() {
+        if (private_fds_) private_fd_table();
         uint64_t seen = 0;
         std::unique_lock<std::mutex> g(mu_);
         for (;;) {
@@ -97,4 +108,5 @@ private:
     int busy_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
+    const bool private_fds_;
 };
