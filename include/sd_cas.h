@@ -403,8 +403,8 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * a larger one the throughput kernels -- read when the batch is planned; "batch_cpu_max"
  * (4096): sd_cas_ids_files calls of at most that many files take the CPU path;
  * "files_ring" (4): pinned window buffers sd_cas_ids_files' readers may fill ahead of the
- * copies; "files_stage_hot" (0): 1 = its readers read each file into a per-thread buffer
- * and stream-copy it into the window; "checksum_cpu_max" (2147483647): sd_file_checksums calls of at most that many
+ * copies; "files_stage_hot" (1): its readers read each file into a per-thread buffer and
+ * stream-copy it into the window (0 = read straight into the window); "checksum_cpu_max" (2147483647): sd_file_checksums calls of at most that many
  * files take the CPU path (sd_cpu_file_checksums on "read_threads" threads; 0 = the GPU
  * route always).  Unknown keys fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);

@@ -25,8 +25,12 @@ thread_local std::string g_err;
 // and one workgroup per whole-kind file up to 512 files (profiles/r2/r2z_small_batch_kernels.json:
 // the crossovers lie between 4096 and 8192 sampled files, 256 and 1024 whole-kind files),
 // sd_cas_ids_files calls of up to 4096 files on the CPU path (profiles/r2/r2z6_batch_sizes.json:
-// from the page cache the host's 16 threads beat the GPU route up to ~8000 files a call)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {0}};
+// a call's fixed GPU-route cost -- windows, launches, D2H -- loses to the host's threads below
+// ~4000-8000 files a call), 4 pinned windows the stager may fill ahead, every
+// sd_file_checksums call on the CPU path (from the page cache the host hashes
+// faster than PCIe carries the bytes), the stager's readers through their cache-resident
+// buffers (profiles/r3/r3n_files_ab_private_fds.json: 1.04 vs 0.84 M files/s)
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
                                                "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",
