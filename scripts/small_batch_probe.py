@@ -27,6 +27,7 @@ def _with_policy(fn, cpu_max=4096):
         return fn()
     finally:
         sd.set_tuning("batch_cpu_max", 0)
+    sd.set_tuning("checksum_cpu_max", 0)  # "file_checksums" times the GPU route (the default policy is the CPU path)
 
 
 def main():

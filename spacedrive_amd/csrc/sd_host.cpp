@@ -24,9 +24,10 @@ thread_local std::string g_err;
 // threads for sd_file_checksums, the one-wave-per-file sampled kernel up to 6144 files
 // and one workgroup per whole-kind file up to 512 files (profiles/r2/r2z_small_batch_kernels.json:
 // the crossovers lie between 4096 and 8192 sampled files, 256 and 1024 whole-kind files),
-// sd_cas_ids_files calls of up to 4096 files on the CPU path (profiles/r2/r2z6_batch_sizes.json:
-// a call's fixed GPU-route cost -- windows, launches, D2H -- loses to the host's threads below
-// ~4000-8000 files a call), 4 pinned windows the stager may fill ahead, every
+// sd_cas_ids_files calls of up to 4096 files on the CPU path (profiles/r3/r3p_batch_sizes.json,
+// p50 per call from the page cache on 16 threads: GPU route / CPU path 286 / 109 us at 100
+// files, 3.39 / 3.07 ms at 4000, 6.24 / 6.36 ms at 8000, 10.8 / 13.7 ms at 16000 -- a call's
+// fixed GPU-route cost loses below ~8000 files), 4 pinned windows the stager may fill ahead, every
 // sd_file_checksums call on the CPU path (from the page cache the host hashes
 // faster than PCIe carries the bytes), the stager's readers through their cache-resident
 // buffers (profiles/r3/r3n_files_ab_private_fds.json: 1.04 vs 0.84 M files/s)
