@@ -67,6 +67,9 @@ def steady(v):
 # the same launch shape's steady duration in the kernel-trace pass, and only for launches of
 # at least MIN_CLOCK_US, where the overhead is small; others show "-".
 MIN_CLOCK_US = 500.0
+# ... and only for the compute-bound hashing kernels: a launch that waits (on peers, the
+# host, or atomics) spends its trace duration idle, and no ratio of the two passes is a clock
+CLOCK_KERNELS = ("k_cas_sampled_lanes", "k_cas_sampled_wave", "k_whole_items", "k_whole_wave", "k_ck_leaf")
 
 
 def main(tag):
@@ -145,8 +148,9 @@ def main(tag):
                 "calibrated factor + WRITE_SIZE x 1024 (factor from `scripts/pmc_calib.py`'s 4 GiB read probes: "
                 f"{ {k: round(v, 4) for k, v in calib.items()} }).  MHz = GRBM_GUI_ACTIVE / 8 XCDs / the same launch "
                 f"shape's steady duration in the kernel-trace pass (`{tag}_summary.md`), shown only for launches of "
-                f"at least {MIN_CLOCK_US:.0f} µs (GRBM_GUI_ACTIVE also counts the busy cycles around a launch, so "
-                "short launches give no clock); lane-ops/clk/CU = SQ_INSTS_VALU x 64 lanes / (GUI cycles / 8 x 256 "
+                f"at least {MIN_CLOCK_US:.0f} µs of the compute-bound hashing kernels (GRBM_GUI_ACTIVE also counts the "
+                "busy cycles around a launch, so short launches give no clock, and a launch that waits -- RCCL, the "
+                "grouping's atomics -- is idle for part of its trace duration); lane-ops/clk/CU = SQ_INSTS_VALU x 64 lanes / (GUI cycles / 8 x 256 "
                 "CUs), same rule: 64 is the measured issue ceiling of BLAKE3's G mix (scripts/valu_probe7.hip), "
                 "128 the SIMD-32 full rate.\n\n")
         f.write("| kernel | grid | HBM GB/launch | VALU wave-insts | GUI cycles | trace µs | MHz | lane-ops/clk/CU |\n"
@@ -159,7 +163,7 @@ def main(tag):
                 c = e["counters"]
                 gui, valu = c.get("GRBM_GUI_ACTIVE"), c.get("SQ_INSTS_VALU")
                 tr_us = steady(shapes[(k, e["grid"])]) if shapes.get((k, e["grid"])) else None
-                long_enough = tr_us is not None and tr_us >= MIN_CLOCK_US
+                long_enough = tr_us is not None and tr_us >= MIN_CLOCK_US and k in CLOCK_KERNELS
                 mhz = gui / 8 / tr_us if gui and long_enough else None
                 ipc = valu * 64 / (gui / 8 * 256) if gui and valu and long_enough else None
                 f.write(f"| `{k}` | {e['grid']} | {e['hbm_bytes_per_launch'] / 1e9:.4g} | "
