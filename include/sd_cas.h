@@ -303,6 +303,17 @@ typedef struct sd_comm sd_comm;
 int sd_comm_id(uint8_t* out_id /* SD_COMM_ID_BYTES */);
 int sd_comm_create(sd_cas_ctx* ctx, const uint8_t* id, int nranks, int rank, sd_comm** out);
 void sd_comm_destroy(sd_comm* comm);
+/* In-process communicator: the ranks are threads of ONE process (each with its own context,
+ * on one device or several) that share an sd_comm_group.  Every collective below has the
+ * same semantics over it; the exchange is device-to-device copies between the ranks'
+ * buffers, ordered by a host barrier (a rank whose thread never arrives makes its peers
+ * return SD_ERR_COMM after 120 s).  For a host that drives several GPUs from one process,
+ * and for rehearsing N ranks on one GPU, which RCCL refuses.  Destroy every member comm
+ * before the group. */
+typedef struct sd_comm_group sd_comm_group;
+int sd_comm_group_create(int nranks, sd_comm_group** out);
+void sd_comm_group_destroy(sd_comm_group* group);
+int sd_comm_create_local(sd_cas_ctx* ctx, sd_comm_group* group, int rank, sd_comm** out);
 /* The whole post-hash step of one rank, collective over the communicator: partition its n
  * records by cas_id prefix (sd_dedup_partition), all-gather the count matrix and the
  * shards' index ranges (ncclAllGather), exchange the 16-byte records with grouped

@@ -28,6 +28,10 @@ pub struct sd_cas_ctx {
 pub struct sd_comm {
     _p: [u8; 0],
 }
+#[repr(C)]
+pub struct sd_comm_group {
+    _p: [u8; 0],
+}
 
 #[repr(C)]
 pub struct sd_split_checksum {
@@ -85,6 +89,11 @@ extern "C" {
     pub fn sd_comm_create(ctx: *mut sd_cas_ctx, id: *const u8, nranks: c_int, rank: c_int,
                           out: *mut *mut sd_comm) -> c_int;
     pub fn sd_comm_destroy(comm: *mut sd_comm);
+    // the same collectives with the ranks as threads of one process (several GPUs, one process)
+    pub fn sd_comm_group_create(nranks: c_int, out: *mut *mut sd_comm_group) -> c_int;
+    pub fn sd_comm_group_destroy(group: *mut sd_comm_group);
+    pub fn sd_comm_create_local(ctx: *mut sd_cas_ctx, group: *mut sd_comm_group, rank: c_int,
+                                out: *mut *mut sd_comm) -> c_int;
     pub fn sd_cas_dedup_mgpu(ctx: *mut sd_cas_ctx, comm: *mut sd_comm, d_hash32: *const u8, d_valid: *const u8,
                              n: u64, global_index_base: u64, chunk_size: u64, d_records_out: *mut u64,
                              d_rep_out: *mut u64, d_owner_out: *mut u64, capacity: u64, m_out: *mut u64,

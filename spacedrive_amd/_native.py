@@ -93,6 +93,9 @@ SIGNATURES = [
     ("sd_comm_id", I32, [P]),
     ("sd_comm_create", I32, [P, P, I32, I32, ctypes.POINTER(P)]),
     ("sd_comm_destroy", None, [P]),
+    ("sd_comm_group_create", I32, [I32, ctypes.POINTER(P)]),
+    ("sd_comm_group_destroy", None, [P]),
+    ("sd_comm_create_local", I32, [P, P, I32, ctypes.POINTER(P)]),
     ("sd_comm_set_timing", I32, [P, I32]),
     ("sd_comm_last_phases", I32, [P, P]),
     ("sd_cas_dedup_mgpu", I32, [P, P, P, P, U64, U64, U64, P, P, P, U64, PU64, PU64, P]),
@@ -143,3 +146,37 @@ def check(rc: int) -> None:
     if rc != SD_OK:
         msg = lib().sd_cas_last_error()
         raise SdCasError(rc, msg.decode() if msg else "")
+
+
+def path_array(paths) -> tuple:
+    """(keepalive, char** address) for n paths: one NUL-joined buffer and a u64 pointer array
+    computed from its NUL positions with numpy.  A ctypes array of n separately encoded
+    strings costs ~0.7 us per path in Python (24 ms for the identifier's 32768-file
+    look-ahead call, more than the library's own work); this costs ~0.05 us.  Paths are
+    encoded as os.fsencode does (utf-8, surrogateescape); a path holding a NUL raises
+    ValueError, as open() does."""
+    import numpy as np
+    n = len(paths)
+    try:
+        buf = ("\0".join(paths) + "\0").encode("utf-8", "surrogateescape")
+    except TypeError:  # PathLike or bytes entries
+        buf = b"\0".join(os.fsencode(p) for p in paths) + b"\0"
+    ends = np.flatnonzero(np.frombuffer(buf, np.uint8) == 0)
+    if len(ends) != max(n, 1):
+        raise ValueError("embedded null byte in a path")
+    base = ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p).value
+    ptrs = np.empty(max(n, 1), np.uint64)
+    ptrs[0] = base
+    ptrs[1:] = ends[:-1].astype(np.uint64) + np.uint64(base + 1)
+    return (buf, ptrs), ptrs.ctypes.data
+
+
+def hex_results(out, width: int, status, paths, err) -> list:
+    """The n NUL-terminated hex strings of `width` chars in `out` (a ctypes string buffer),
+    with err(status, path) in place of each entry whose status is not SD_FILE_OK."""
+    import numpy as np
+    n = len(paths)
+    res = np.frombuffer(out, dtype=f"S{width + 1}", count=n).astype(f"U{width}").tolist()
+    for i in np.flatnonzero(np.asarray(status[:n]) != SD_FILE_OK).tolist():
+        res[i] = err(int(status[i]), os.fsdecode(paths[i]))
+    return res

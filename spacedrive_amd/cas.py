@@ -37,7 +37,7 @@ from typing import List, Optional, Sequence, Union
 
 import numpy as np
 
-from ._native import (SD_FILE_IO_ERROR, SD_FILE_OK, SD_FILE_SHORT_READ, check, lib)
+from ._native import (SD_FILE_IO_ERROR, SD_FILE_OK, SD_FILE_SHORT_READ, check, hex_results, lib, path_array)
 from .device import _ptr, default_context
 
 MINIMUM_FILE_SIZE = 1024 * 100  # cas.rs:15
@@ -69,19 +69,12 @@ def generate_cas_ids(paths: Sequence[Union[str, os.PathLike]], sizes: Sequence[i
     ctx = default_context(device)
     sizes_a = np.ascontiguousarray(sizes, dtype=np.uint64)
     status = np.zeros(n, np.int32)
-    arr = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
+    keep, arr = path_array(paths)
     out = ctypes.create_string_buffer(17 * n)
     # library-side pread of header/samples/tail (or the whole file) on its stager pool,
     # overlapped window by window with the H2D copies and kernels
     check(lib().sd_cas_ids_files(ctx.handle, arr, _ptr(sizes_a), n, out, _ptr(status), STAGE_THREADS))
-    raw = out.raw
-    res: List[Union[str, OSError]] = []
-    for i in range(n):
-        if status[i] == SD_FILE_OK:
-            res.append(raw[17 * i:17 * i + 16].decode())
-        else:
-            res.append(_status_error(int(status[i]), os.fsdecode(paths[i])))
-    return res
+    return hex_results(out, 16, status, paths, _status_error)
 
 
 def generate_cas_id(path: Union[str, os.PathLike], size: int, device: Optional[int] = None) -> str:
@@ -105,14 +98,11 @@ def file_checksums(paths: Sequence[Union[str, os.PathLike]],
     if n == 0:
         return []
     ctx = default_context(device)
-    enc = [os.fsencode(p) for p in paths]
-    arr = (ctypes.c_char_p * n)(*enc)
+    keep, arr = path_array(paths)
     out = ctypes.create_string_buffer(65 * n)
     status = np.zeros(n, np.int32)
     check(lib().sd_file_checksums(ctx.handle, arr, n, out, _ptr(status)))
-    raw = out.raw
-    return [raw[65 * i:65 * i + 64].decode() if status[i] == SD_FILE_OK
-            else _status_error(int(status[i]), os.fsdecode(paths[i])) for i in range(n)]
+    return hex_results(out, 64, status, paths, _status_error)
 
 
 def file_checksum(path: Union[str, os.PathLike], device: Optional[int] = None) -> str:

@@ -14,7 +14,7 @@ from typing import List, Optional, Sequence, Union
 
 import numpy as np
 
-from ._native import SD_FILE_OK, check, lib
+from ._native import SD_FILE_OK, check, hex_results, lib, path_array
 from .cas import _status_error
 
 THREADS = 16  # host threads for batches (the CPU share of one GPU on an MI355X node)
@@ -34,12 +34,10 @@ def generate_cas_ids(paths: Sequence[Union[str, os.PathLike]], sizes: Sequence[i
         return []
     sizes_a = np.ascontiguousarray(sizes, dtype=np.uint64)
     status = np.zeros(n, np.int32)
-    arr = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
+    keep, arr = path_array(paths)
     out = ctypes.create_string_buffer(17 * n)
     check(lib().sd_cpu_cas_ids_files(arr, sizes_a.ctypes.data, n, out, status.ctypes.data, nthreads))
-    raw = out.raw
-    return [raw[17 * i:17 * i + 16].decode() if status[i] == SD_FILE_OK
-            else _status_error(int(status[i]), os.fsdecode(paths[i])) for i in range(n)]
+    return hex_results(out, 16, status, paths, _status_error)
 
 
 def generate_cas_id(path: Union[str, os.PathLike], size: int) -> str:
@@ -57,13 +55,11 @@ def file_checksums(paths: Sequence[Union[str, os.PathLike]],
     n = len(paths)
     if n == 0:
         return []
-    arr = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
+    keep, arr = path_array(paths)
     out = ctypes.create_string_buffer(65 * n)
     status = np.zeros(n, np.int32)
     check(lib().sd_cpu_file_checksums(arr, n, out, status.ctypes.data, nthreads))
-    raw = out.raw
-    return [raw[65 * i:65 * i + 64].decode() if status[i] == SD_FILE_OK
-            else _status_error(int(status[i]), os.fsdecode(paths[i])) for i in range(n)]
+    return hex_results(out, 64, status, paths, _status_error)
 
 
 def file_checksum(path: Union[str, os.PathLike]) -> str:

@@ -21,18 +21,58 @@
 //   4. sd_dedup_group + sd_dedup_owners on the received records.
 // A Rust host drives this through sd_comm_id (ncclGetUniqueId on one rank, the 128 bytes
 // passed to the others out of band) and sd_comm_create (ncclCommInitRank).
+//
+// The same calls also run over an in-process group (sd_comm_group_create +
+// sd_comm_create_local): ranks are threads of one process, on one device or several, and
+// steps 2 and 3 become device-to-device copies between the ranks' buffers, ordered by a
+// host barrier.  It serves one process driving several GPUs, and it rehearses N ranks on
+// one GPU, which RCCL refuses ("Duplicate GPU detected") -- the partition, the gathered
+// plan, the per-peer offsets and the grouping are the same code either way.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "sd_internal.h"
 
+// In-process group: a generation barrier plus one published device pointer pair per rank.
+// A rank writes its slots before a barrier and reads its peers' after it; the barrier's
+// mutex orders the two.  A rank that never arrives (its thread failed) makes the others
+// fail with SD_ERR_COMM after `timeout_s` rather than hang.
+struct sd_comm_group {
+    int nranks = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    std::vector<const void*> slot_a, slot_b;
+    std::vector<int> joined;
+    double timeout_s = 120.0;
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t gen = generation;
+        if (++arrived == nranks) {
+            arrived = 0;
+            generation++;
+            cv.notify_all();
+            return;
+        }
+        if (!cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return generation != gen; })) {
+            arrived--;
+            throw sd_failure(SD_ERR_COMM, "in-process group: a rank did not reach the barrier in time");
+        }
+    }
+};
+
 struct sd_comm {
     ncclComm_t comm = nullptr;
+    sd_comm_group* group = nullptr;  // in-process transport instead of RCCL
     int nranks = 0, rank = 0, device = 0;
     // device scratch, grown on demand: the partitioned send records, the all-gather rows
     // (send row + nranks rows)
@@ -53,6 +93,10 @@ struct sd_comm {
         if (d_rows) (void)hipFree(d_rows);
         if (h_rows) (void)hipHostFree(h_rows);
         if (comm) (void)ncclCommDestroy(comm);
+        if (group) {
+            std::lock_guard<std::mutex> lk(group->mu);
+            group->joined[rank] = 0;
+        }
     }
 };
 
@@ -88,9 +132,65 @@ void mark(sd_comm* c, int k, hipStream_t s) {
     HIP_OK(hipEventRecord(c->ev[k], s));
 }
 
+// In-process all-gather of `bytes` per rank: rank p's block at `src` lands at dst + p * bytes
+// (host or device memory) for every p.  In place when src == dst + rank * bytes.
+void local_allgather(sd_comm* c, const void* src, void* dst, size_t bytes, hipStream_t s) {
+    sd_comm_group* g = c->group;
+    HIP_OK(hipStreamSynchronize(s));  // this rank's block is complete
+    g->slot_a[c->rank] = src;
+    g->barrier();
+    for (int p = 0; p < c->nranks; p++) {
+        uint8_t* to = (uint8_t*)dst + (size_t)p * bytes;
+        if (bytes && to != g->slot_a[p]) HIP_OK(hipMemcpyAsync(to, g->slot_a[p], bytes, hipMemcpyDefault, s));
+    }
+    HIP_OK(hipStreamSynchronize(s));
+    g->barrier();  // every rank holds every block: the sources may change again
+}
+
 }  // namespace
 
 extern "C" {
+
+int sd_comm_group_create(int nranks, sd_comm_group** out) {
+    SD_GUARD_BEGIN
+    if (!out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (nranks < 1 || nranks > 64) throw sd_failure(SD_ERR_INVALID, "nranks out of range (1..64)");
+    auto g = std::make_unique<sd_comm_group>();
+    g->nranks = nranks;
+    g->slot_a.assign(nranks, nullptr);
+    g->slot_b.assign(nranks, nullptr);
+    g->joined.assign(nranks, 0);
+    *out = g.release();
+    return SD_OK;
+    SD_GUARD_END
+}
+
+void sd_comm_group_destroy(sd_comm_group* group) { delete group; }
+
+int sd_comm_create_local(sd_cas_ctx* ctx, sd_comm_group* group, int rank, sd_comm** out) {
+    SD_GUARD_BEGIN
+    if (!ctx || !group || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    if (rank < 0 || rank >= group->nranks) throw sd_failure(SD_ERR_INVALID, "rank out of range");
+    *out = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(group->mu);
+        if (group->joined[rank]) throw sd_failure(SD_ERR_INVALID, "rank already joined this group");
+        group->joined[rank] = 1;
+    }
+    auto c = std::make_unique<sd_comm>();
+    c->group = group;
+    c->nranks = group->nranks;
+    c->rank = rank;
+    c->device = sd_ctx_device(ctx);
+    HIP_OK(hipSetDevice(c->device));
+    const size_t row = (size_t)c->nranks + ROW_EXTRA;
+    HIP_OK(hipMalloc(&c->d_rows, sizeof(uint64_t) * row * (c->nranks + 1)));
+    HIP_OK(hipMalloc(&c->d_part_scratch, sdk::dedup_partition_scratch(c->nranks)));
+    HIP_OK(hipHostMalloc((void**)&c->h_rows, sizeof(uint64_t) * (row * (c->nranks + 1) + 1), hipHostMallocDefault));
+    *out = c.release();
+    return SD_OK;
+    SD_GUARD_END
+}
 
 int sd_comm_id(uint8_t* out_id) {
     SD_GUARD_BEGIN
@@ -172,10 +272,16 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
     HIP_OK(hipMemcpyAsync(d_row + R, h_row + R, sizeof(uint64_t) * 3, hipMemcpyHostToDevice, s));
     HIP_OK(hipMemcpyAsync(d_row + R + 3, pscratch + psb / sizeof(uint64_t) - 1, sizeof(uint64_t),
                           hipMemcpyDeviceToDevice, s));
-    NCCL_OK(ncclAllGather(d_row, d_all, row, ncclUint64, comm->comm, s));
     uint64_t* all = comm->h_rows + row;
-    HIP_OK(hipMemcpyAsync(all, d_all, sizeof(uint64_t) * row * R, hipMemcpyDeviceToHost, s));
-    mark(comm, 2, s);
+    if (comm->group) {  // in-process: every rank's row straight into this rank's host table
+        comm->group->slot_b[me] = comm->d_send;  // read by the peers after the barriers below
+        local_allgather(comm, d_row, all, sizeof(uint64_t) * row, s);
+        mark(comm, 2, s);
+    } else {
+        NCCL_OK(ncclAllGather(d_row, d_all, row, ncclUint64, comm->comm, s));
+        HIP_OK(hipMemcpyAsync(all, d_all, sizeof(uint64_t) * row * R, hipMemcpyDeviceToHost, s));
+        mark(comm, 2, s);
+    }
     HIP_OK(hipStreamSynchronize(s));  // the one sync before the exchange: every rank's row
     const ExchangePlan plan = exchange_plan(all, R, me);
     *m_out = plan.recv_total;
@@ -189,14 +295,30 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
     // 3. the all-to-all of the 16-byte records: one send and one receive per peer
     mark(comm, 3, s);
     const uint64_t* send = (const uint64_t*)comm->d_send;
-    NCCL_OK(ncclGroupStart());
-    for (int p = 0; p < R; p++) {
-        if (plan.send_cnt[p])
-            NCCL_OK(ncclSend(send + 2 * plan.send_off[p], 2 * plan.send_cnt[p], ncclUint64, p, comm->comm, s));
-        if (plan.recv_cnt[p])
-            NCCL_OK(ncclRecv(d_records_out + 2 * plan.recv_off[p], 2 * plan.recv_cnt[p], ncclUint64, p, comm->comm, s));
+    if (comm->group) {
+        // in-process: pull what each peer sends here from its partitioned records, which
+        // start at the sum of its counts to the ranks before this one
+        sd_comm_group* g = comm->group;
+        for (int p = 0; p < R; p++) {
+            if (!plan.recv_cnt[p]) continue;
+            uint64_t off = 0;
+            for (int q = 0; q < me; q++) off += all[(size_t)p * row + q];
+            HIP_OK(hipMemcpyAsync(d_records_out + 2 * plan.recv_off[p], (const uint64_t*)g->slot_b[p] + 2 * off,
+                                  16 * plan.recv_cnt[p], hipMemcpyDefault, s));
+        }
+        HIP_OK(hipStreamSynchronize(s));
+        g->barrier();  // every rank has its records: the send buffers may be reused
+    } else {
+        NCCL_OK(ncclGroupStart());
+        for (int p = 0; p < R; p++) {
+            if (plan.send_cnt[p])
+                NCCL_OK(ncclSend(send + 2 * plan.send_off[p], 2 * plan.send_cnt[p], ncclUint64, p, comm->comm, s));
+            if (plan.recv_cnt[p])
+                NCCL_OK(ncclRecv(d_records_out + 2 * plan.recv_off[p], 2 * plan.recv_cnt[p], ncclUint64, p,
+                                 comm->comm, s));
+        }
+        NCCL_OK(ncclGroupEnd());
     }
-    NCCL_OK(ncclGroupEnd());
     mark(comm, 4, s);
     // 4. group by cas_id and assign Objects (chunk-of-100 rule) on the received records
     uint64_t ng = 0;
@@ -244,7 +366,8 @@ int sd_split_checksum_mgpu(sd_cas_ctx* ctx, sd_comm* comm, sd_split_checksum* sp
     check_rc(sd_split_checksum_leaves(ctx, split, d_slice, d_cvs, stream));
     if (comm->nranks > 1) {
         const size_t slot_bytes = (size_t)p.q * 32;
-        NCCL_OK(ncclAllGather(d_cvs + (size_t)p.rank * slot_bytes, d_cvs, slot_bytes, ncclUint8, comm->comm, s));
+        if (comm->group) local_allgather(comm, d_cvs + (size_t)p.rank * slot_bytes, d_cvs, slot_bytes, s);
+        else NCCL_OK(ncclAllGather(d_cvs + (size_t)p.rank * slot_bytes, d_cvs, slot_bytes, ncclUint8, comm->comm, s));
     }
     check_rc(sd_split_checksum_root(ctx, split, d_cvs, d_hash32, stream));
     return SD_OK;

@@ -78,10 +78,10 @@ class Context:
         """sd_cas_hashes_files: generate_cas_id's messages of these files hashed into
         d_hash32 (device, n x 32 B; the cas_id is each row's first 8 bytes) and, if given,
         d_valid (device, n B: hashed and not empty).  Returns the int32 status per file."""
-        import os
+        from ._native import path_array
         n = len(paths)
         status = np.zeros(max(n, 1), np.int32)
-        arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+        keep, arr = path_array(paths)
         sz = np.ascontiguousarray(sizes, dtype=np.uint64)
         assert d_hash32.numel() >= 32 * n and (d_valid is None or d_valid.numel() >= n)
         check(lib().sd_cas_hashes_files(self.handle, arr, _ptr(sz), n, _ptr(d_hash32),
@@ -138,8 +138,24 @@ class Context:
         return int(m.value), int(ng.value)
 
 
+class CommGroup:
+    """sd_comm_group: the in-process rendezvous of ``nranks`` ranks that are threads of one
+    process (one Comm per thread, each on its own Context).  Close it after its Comms."""
+
+    def __init__(self, nranks: int):
+        h = ctypes.c_void_p()
+        check(lib().sd_comm_group_create(nranks, ctypes.byref(h)))
+        self.handle, self.nranks = h, nranks
+
+    def close(self) -> None:
+        if self.handle:
+            lib().sd_comm_group_destroy(self.handle)
+            self.handle = None
+
+
 class Comm:
-    """libsdcas's RCCL communicator (sd_comm): one per rank, on its context's device."""
+    """libsdcas's communicator (sd_comm): one per rank, on its context's device -- RCCL, or
+    the in-process transport of a CommGroup."""
 
     ID_BYTES = 128
 
@@ -149,11 +165,18 @@ class Comm:
         check(lib().sd_comm_id(buf))
         return buf.raw
 
-    def __init__(self, ctx: Context, uid: bytes, nranks: int, rank: int):
-        assert len(uid) == Comm.ID_BYTES
+    def __init__(self, ctx: Context, uid: Optional[bytes], nranks: int, rank: int,
+                 group: Optional["CommGroup"] = None):
+        """RCCL (``uid`` from ``unique_id()`` on one rank) or, with ``group``, the in-process
+        transport (sd_comm_create_local: the ranks are threads of this process)."""
         h = ctypes.c_void_p()
-        check(lib().sd_comm_create(ctx.handle, uid, nranks, rank, ctypes.byref(h)))
-        self.handle, self.nranks, self.rank = h, nranks, rank
+        if group is not None:
+            assert group.nranks == nranks
+            check(lib().sd_comm_create_local(ctx.handle, group.handle, rank, ctypes.byref(h)))
+        else:
+            assert uid is not None and len(uid) == Comm.ID_BYTES
+            check(lib().sd_comm_create(ctx.handle, uid, nranks, rank, ctypes.byref(h)))
+        self.handle, self.nranks, self.rank, self.group = h, nranks, rank, group
 
     PHASES = ("partition", "allgather_rows", "host_turnaround", "sendrecv", "group_owners")  # SD_DEDUP_PHASES
 

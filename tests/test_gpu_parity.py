@@ -1189,6 +1189,136 @@ def test_split_checksum_mgpu_through_rccl_single_rank(ctx, oracle_native, rccl_c
     assert checksum_split(d[:total + 64], total, ctx=ctx) == want
 
 
+def _run_ranks(R, fn):
+    """fn(rank) on R threads (ctypes releases the GIL inside the library); results by rank,
+    the first exception re-raised."""
+    import threading
+    out, errs = [None] * R, []
+
+    def body(r):
+        try:
+            out[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(R)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=180)
+    assert not any(t.is_alive() for t in ts), "a rank thread did not finish"
+    if errs:
+        raise errs[0]
+    return out
+
+
+@pytest.mark.parametrize("R", [2, 3, 5])
+def test_dedup_mgpu_in_process_ranks(ctx, R):
+    """sd_cas_dedup_mgpu with R > 1 ranks (configs[4]'s exchange): RCCL
+    refuses two ranks on one GPU, so the ranks are threads of this process on the in-process
+    transport (sd_comm_create_local) -- the same partition, gathered count matrix, capacity
+    check, per-peer offsets, grouping and Object rule as over RCCL.  Uneven shards; each
+    rank's output == the host grouping of the records whose cas_id prefix it owns, with the
+    chunk-of-100 owners; an undersized rank makes every rank return SD_ERR_CAPACITY, and a
+    second round of calls on the same communicators (buffers reused) agrees."""
+    from spacedrive_amd import dedup
+    from spacedrive_amd._native import SD_ERR_CAPACITY, SdCasError
+    from spacedrive_amd.dedup import dest_of
+    from spacedrive_amd.device import Comm, CommGroup, Context
+    from spacedrive_amd.identifier import object_owners
+    n = 90000
+    sizes, cids, twins = synth.library(0, n, n, dup_frac=0.3)
+    h = gpu_cas(ctx, sizes, cids, twins)
+    valid = sizes != 0
+    keys = keys_from_hashes(h)
+    cuts = [0] + [int(c) for c in np.cumsum(np.random.default_rng(R).dirichlet(np.ones(R)) * n)[:-1]] + [n]
+    group = CommGroup(R)
+    ctxs = [Context(0) for _ in range(R)]
+    comms = [Comm(ctxs[r], None, R, r, group=group) for r in range(R)]
+    d_hash = torch.from_numpy(h.reshape(-1).copy()).cuda()  # flat: a shard is a byte offset
+    d_valid = torch.from_numpy(valid.astype(np.uint8)).cuda()
+    torch.cuda.synchronize()
+    all_recs = np.stack([keys[valid].view(np.int64), np.arange(n)[valid]], axis=1)
+    dst = dest_of(all_recs[:, 0].view(np.uint64), R)
+
+    def rank_call(r, capacity):
+        lo, hi = cuts[r], cuts[r + 1]
+        st = torch.cuda.Stream()
+        if capacity is not None:
+            buf = torch.empty((max(capacity, 1), 2), dtype=torch.int64, device="cuda")
+            try:
+                ctxs[r].dedup_mgpu(comms[r], d_hash[lo * 32:], d_valid[lo:], hi - lo, lo, buf, buf[:, 0].clone(),
+                                   buf[:, 1].clone(), capacity, stream=st)
+            except SdCasError as e:
+                return e.rc, e.needed
+            return 0, None
+        runner = dedup.RcclDedup(ctxs[r], comms[r], d_hash.device, capacity=hi - lo + 1024)
+        res = []
+        for _ in range(2):
+            recs, rep, ng, own = runner(d_hash[lo * 32:], d_valid[lo:], hi - lo, lo, stream=st)
+            st.synchronize()
+            res.append((recs.cpu().numpy(), rep.cpu().numpy(), ng, own.cpu().numpy()))
+        return res
+
+    try:
+        # rank 1 undersized: every rank stops before the exchange, each told its own need
+        caps = [n] * R
+        caps[1] = 3
+        got = _run_ranks(R, lambda r: rank_call(r, caps[r]))
+        for r in range(R):
+            assert got[r] == (SD_ERR_CAPACITY, int((dst == r).sum())), (r, got[r])
+        got = _run_ranks(R, lambda r: rank_call(r, None))
+        assert sum(len(g[0][0]) for g in got) == int(valid.sum())
+        for r in range(R):
+            gr, grep, gng = group_host(all_recs[dst == r])
+            want_owner = object_owners(torch.from_numpy(gr[:, 1].copy()), torch.from_numpy(grep), 100).numpy()
+            for recs, rep, ng, own in got[r]:
+                assert ng == gng, (r, ng, gng)
+                assert np.array_equal(recs, gr) and np.array_equal(rep, grep)
+                assert np.array_equal(own, want_owner)
+    finally:
+        for c in comms:
+            c.close()
+        group.close()
+        for c in ctxs:
+            c.close()
+
+
+def test_split_checksum_mgpu_in_process_ranks(ctx, oracle_native):
+    """sd_split_checksum_mgpu over R = 3 and 4 in-process ranks: each rank hashes its own
+    blocks into its own CV buffer, the in-place all-gather fills the others' slots, and
+    every rank's root equals the oracle's BLAKE3 of the whole file."""
+    from spacedrive_amd.device import Comm, CommGroup, Context, SplitChecksum
+    total = (45 << 20) + 77
+    d = torch.zeros(total + 128, dtype=torch.uint8, device="cuda")
+    ctx.synth_fill(902, 0, total, d)
+    torch.cuda.synchronize()
+    want = oracle_native.checksum_synth_mt(total, 902, 0, nthreads=NT).hex()
+    for R in (3, 4):
+        group = CommGroup(R)
+        ctxs = [Context(0) for _ in range(R)]
+        comms = [Comm(ctxs[r], None, R, r, group=group) for r in range(R)]
+
+        def rank(r):
+            sc = SplitChecksum(ctxs[r], total, R, r)
+            cvs = torch.zeros(sc.cv_bytes, dtype=torch.uint8, device="cuda")
+            out = torch.zeros(32, dtype=torch.uint8, device="cuda")
+            st = torch.cuda.Stream()
+            sc.mgpu(comms[r], d[sc.offset:], cvs, out, stream=st)
+            st.synchronize()
+            sc.close()
+            return bytes(out.cpu().numpy()).hex()
+
+        try:
+            assert _run_ranks(R, rank) == [want] * R
+        finally:
+            for c in comms:
+                c.close()
+            group.close()
+            for c in ctxs:
+                c.close()
+
+
 @pytest.mark.parametrize("route", ["batch", "single-gpu"])
 def test_pipe_whole_kind_reads_every_byte(ctx, tmp_path, oracle_native, route):
     """generate_cas_id on a pipe (a metadata length of 0, as non_indexed passes for one):
