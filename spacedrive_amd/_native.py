@@ -176,7 +176,12 @@ def hex_results(out, width: int, status, paths, err) -> list:
     with err(status, path) in place of each entry whose status is not SD_FILE_OK."""
     import numpy as np
     n = len(paths)
+    bad = np.flatnonzero(np.asarray(status[:n]) != SD_FILE_OK).tolist()
+    if not bad:  # every entry is `width` hex chars + NUL: one C-level split
+        res = ctypes.string_at(out, (width + 1) * n - 1).decode("latin-1").split("\0")
+        if len(res) == n and all(len(r) == width for r in (res[0], res[-1])):
+            return res
     res = np.frombuffer(out, dtype=f"S{width + 1}", count=n).astype(f"U{width}").tolist()
-    for i in np.flatnonzero(np.asarray(status[:n]) != SD_FILE_OK).tolist():
+    for i in bad:
         res[i] = err(int(status[i]), os.fsdecode(paths[i]))
     return res
