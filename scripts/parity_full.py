@@ -12,6 +12,12 @@ This runs the whole 10 M-file library the 8-GPU bench hashes -- the same per-ran
   concatenated in source-rank order as the all-to-all delivers them, and each is grouped
   on the device (sd_dedup_group).  Records, representatives and group counts must equal
   the host grouping of the ORACLE's cas_ids;
+* the same exchange through the library's own multi-rank code: the 8 shards' hashes go to
+  8 ranks that are threads of this process on the in-process communicator
+  (sd_comm_create_local; RCCL refuses 8 ranks on one GPU), each calls sd_cas_dedup_mgpu
+  (partition, gathered count matrix, per-peer record copies, grouping, Object rule) and its
+  records, representatives and owners must equal the host grouping + object_owners of the
+  oracle's cas_ids of the prefix range it owns;
 * configs[3]: the 16 x 4 GiB validator files bench.py times (content ids 10000..10015)
   plus a mixed 2-8 GiB set, full 32-byte BLAKE3 vs the chunk-parallel C oracle.
 
@@ -59,6 +65,7 @@ def cas_library(ctx, n_total: int, shards: int, nthreads: int) -> dict:
     recs = torch.empty((n, 2), dtype=torch.int64, device="cuda")
     all_sizes = np.empty(n_total, np.uint64)
     t_gpu = 0.0
+    shard_hashes, shard_valid = [], []  # per rank, for the in-process sd_cas_dedup_mgpu
     for s in range(shards):
         start = s * n
         sizes, cids, twins = synth.library(start, n, n_total)
@@ -77,6 +84,8 @@ def cas_library(ctx, n_total: int, shards: int, nthreads: int) -> dict:
         torch.cuda.synchronize()
         t_gpu += time.perf_counter() - t0
         ids[start:start + n] = d_hash.view(n, 32)[:, :8].cpu().numpy()
+        shard_hashes.append(d_hash.clone())
+        shard_valid.append(d_valid)
         c = counts.cpu().numpy()
         r = recs[:nv].cpu().numpy()
         off = np.concatenate([[0], np.cumsum(c)])
@@ -104,11 +113,13 @@ def cas_library(ctx, n_total: int, shards: int, nthreads: int) -> dict:
     dest = dest_of(keys, shards)
     groups = rep_mismatch = rec_mismatch = 0
     dup_files = 0
+    host_groups = []
     for d in range(shards):
         got = np.concatenate(buckets[d]) if buckets[d] else np.zeros((0, 2), np.int64)
         sel = valid & (dest == d)
         host = np.stack([keys[sel].view(np.int64), gidx[sel]], axis=1)
         hr, hrep, hng = group_host(host)
+        host_groups.append((hr, hrep, hng))
         dr = torch.from_numpy(got).cuda()
         drep = torch.empty(max(len(got), 1), dtype=torch.int64, device="cuda")
         ng = ctx.dedup_group(dr, len(got), drep, index_sorted=True)
@@ -119,12 +130,76 @@ def cas_library(ctx, n_total: int, shards: int, nthreads: int) -> dict:
         groups += ng
         assert ng == hng or rec_mismatch, (d, ng, hng)
         dup_files += int((hrep != hr[:, 1]).sum())
+    del buckets
+    exchange = exchange_inprocess(shard_hashes, shard_valid, n, shards, host_groups)
+    del shard_hashes, shard_valid
+    torch.cuda.empty_cache()
     return {"files": n_total, "shards": shards, "files_per_shard": n, "cas_id_mismatches": int(len(bad)),
             "first_mismatches": [int(i) for i in bad[:10]],
             "empty_files": int((~valid).sum()), "sampled_files": int((all_sizes > 102400).sum()),
             "dedup": {"records": int(valid.sum()), "groups": int(groups), "duplicate_files": dup_files,
                       "bucket_record_mismatches": rec_mismatch, "bucket_rep_mismatches": rep_mismatch},
+            "exchange_inprocess": exchange,
             "gpu_s": t_gpu, "oracle_s": t_cpu, "oracle_threads": nthreads}
+
+
+def exchange_inprocess(hashes, valids, n: int, shards: int, host_groups) -> dict:
+    """sd_cas_dedup_mgpu over `shards` ranks that are threads of this process (one context and
+    stream each, the in-process communicator), rank r holding shard r's hashes; every rank's
+    output vs the host grouping (+ the chunk-of-100 Object rule) of its prefix range."""
+    import threading
+    from spacedrive_amd import dedup
+    from spacedrive_amd.device import Comm, CommGroup, Context
+    from spacedrive_amd.identifier import object_owners
+    group = CommGroup(shards)
+    ctxs = [Context(0) for _ in range(shards)]
+    comms = [Comm(ctxs[r], None, shards, r, group=group) for r in range(shards)]
+    for c in comms:
+        c.set_timing(True)
+    out, errs = [None] * shards, []
+
+    def rank(r):
+        try:
+            st = torch.cuda.Stream()
+            runner = dedup.RcclDedup(ctxs[r], comms[r], hashes[r].device, capacity=n * 5 // 4)
+            res = []
+            for _ in range(2):  # the second call reuses the buffers (and times the warm exchange)
+                t0 = time.perf_counter()
+                recs, rep, ng, own = runner(hashes[r], valids[r], n, r * n, stream=st)
+                st.synchronize()
+                res.append(time.perf_counter() - t0)
+            out[r] = (recs.cpu().numpy(), rep.cpu().numpy(), ng, own.cpu().numpy(), res, comms[r].last_phases())
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    try:
+        ts = [threading.Thread(target=rank, args=(r,)) for r in range(shards)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise errs[0]
+    finally:
+        for c in comms:
+            c.close()
+        group.close()
+        for c in ctxs:
+            c.close()
+    mism = {"records": 0, "reps": 0, "groups": 0, "owners": 0}
+    per_rank = []
+    for r in range(shards):
+        recs, rep, ng, own, secs, phases = out[r]
+        hr, hrep, hng = host_groups[r]
+        want_own = object_owners(torch.from_numpy(hr[:, 1].copy()), torch.from_numpy(hrep), 100).numpy()
+        mism["records"] += int(not np.array_equal(recs, hr))
+        mism["reps"] += int(not np.array_equal(rep, hrep))
+        mism["groups"] += int(ng != hng)
+        mism["owners"] += int(not np.array_equal(own, want_own))
+        per_rank.append({"records": int(len(recs)), "groups": int(ng), "call_ms": [x * 1e3 for x in secs],
+                         "phases_ms": phases})
+    return {"ranks": shards, "transport": "in-process (sd_comm_create_local), all ranks on one GPU",
+            "rank_mismatches": mism, "parity": not any(mism.values()), "per_rank": per_rank}
 
 
 def checksums(ctx, files, nthreads: int) -> dict:
@@ -181,7 +256,7 @@ def main():
         with open(a.out, "w") as f:
             f.write(s + "\n")
     ok = r["cas"]["cas_id_mismatches"] == 0 and r["cas"]["dedup"]["bucket_record_mismatches"] == 0 \
-        and r["cas"]["dedup"]["bucket_rep_mismatches"] == 0 \
+        and r["cas"]["dedup"]["bucket_rep_mismatches"] == 0 and r["cas"]["exchange_inprocess"]["parity"] \
         and all(r.get(k, {"mismatches": 0})["mismatches"] == 0 for k in ("checksum_configs3", "checksum_mixed"))
     sys.exit(0 if ok else 1)
 

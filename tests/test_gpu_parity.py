@@ -1212,7 +1212,7 @@ def _run_ranks(R, fn):
     return out
 
 
-@pytest.mark.parametrize("R", [2, 3, 5])
+@pytest.mark.parametrize("R", [2, 3, 5, 8])
 def test_dedup_mgpu_in_process_ranks(ctx, R):
     """sd_cas_dedup_mgpu with R > 1 ranks (configs[4]'s exchange): RCCL
     refuses two ranks on one GPU, so the ranks are threads of this process on the in-process
