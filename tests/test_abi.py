@@ -234,3 +234,37 @@ def test_rust_step_excerpts_use_the_shim():
     assert LOOKAHEAD == 32768
     assert "file_checksums(full_paths.clone()).await" in valid
     assert "ValidatorError::FileIO(FileIOError::from((full_path, e))))?" in valid  # `?` per file (:147-149)
+
+
+def test_path_array_and_hex_results(tmp_path):
+    """The batched wrappers' marshalling: path_array's char** holds every path as os.fsencode
+    gives it (str, bytes, PathLike, non-UTF-8 bytes), rejects an embedded NUL like open();
+    hex_results returns the hex strings and the caller's error for each failed status --
+    and the CPU path called through them hashes real files like the single-file call."""
+    import pathlib
+    from spacedrive_amd import cpu
+    from spacedrive_amd._native import hex_results, path_array
+    paths = ["/a/b", b"/c\xff/d", pathlib.Path("/e f/é"), "/" + "x" * 300]
+    keep, arr = path_array(paths)
+    ptrs = np.ctypeslib.as_array((ctypes.c_uint64 * len(paths)).from_address(arr))
+    assert [ctypes.string_at(int(p)) for p in ptrs] == [os.fsencode(p) for p in paths]
+    with pytest.raises(ValueError):
+        path_array(["ok", "bad\0path"])
+    out = ctypes.create_string_buffer(b"".join(b"%016x\0" % i for i in range(5)), 17 * 5)
+    st = np.array([0, 0, 2 | (2 << 16), 0, 0], np.int32)
+    got = hex_results(out, 16, st, ["p0", "p1", "p2", "p3", "p4"], lambda s, p: (s, p))
+    assert got == ["%016x" % 0, "%016x" % 1, (st[2], "p2"), "%016x" % 3, "%016x" % 4]
+    assert hex_results(out, 16, np.zeros(5, np.int32), ["p"] * 5, None) == ["%016x" % i for i in range(5)]
+    files = []
+    for i, n in enumerate([1, 5000, 102401, 0]):
+        f = tmp_path / f"f{i}"
+        f.write_bytes(bytes((j * 7 + i) % 251 for j in range(n)))
+        files.append(str(f))
+    files.append(str(tmp_path / "missing"))
+    sizes = [os.path.getsize(f) if os.path.exists(f) else 10 for f in files]
+    batch = cpu.generate_cas_ids(files, sizes)
+    for f, s, r in zip(files, sizes, batch):
+        if os.path.exists(f):
+            assert r == cpu.generate_cas_id(f, s)
+        else:
+            assert isinstance(r, OSError) and r.filename == f
