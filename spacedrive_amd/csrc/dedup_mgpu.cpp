@@ -32,43 +32,12 @@
 #include <rccl/rccl.h>
 #include <string.h>
 
-#include <chrono>
-#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "sd_internal.h"
-
-// In-process group: a generation barrier plus one published device pointer pair per rank.
-// A rank writes its slots before a barrier and reads its peers' after it; the barrier's
-// mutex orders the two.  A rank that never arrives (its thread failed) makes the others
-// fail with SD_ERR_COMM after `timeout_s` rather than hang.
-struct sd_comm_group {
-    int nranks = 0;
-    std::mutex mu;
-    std::condition_variable cv;
-    int arrived = 0;
-    uint64_t generation = 0;
-    std::vector<const void*> slot_a, slot_b;
-    std::vector<int> joined;
-    double timeout_s = 120.0;
-    void barrier() {
-        std::unique_lock<std::mutex> lk(mu);
-        const uint64_t gen = generation;
-        if (++arrived == nranks) {
-            arrived = 0;
-            generation++;
-            cv.notify_all();
-            return;
-        }
-        if (!cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return generation != gen; })) {
-            arrived--;
-            throw sd_failure(SD_ERR_COMM, "in-process group: a rank did not reach the barrier in time");
-        }
-    }
-};
 
 struct sd_comm {
     ncclComm_t comm = nullptr;
@@ -155,12 +124,7 @@ int sd_comm_group_create(int nranks, sd_comm_group** out) {
     SD_GUARD_BEGIN
     if (!out) throw sd_failure(SD_ERR_INVALID, "null argument");
     if (nranks < 1 || nranks > 64) throw sd_failure(SD_ERR_INVALID, "nranks out of range (1..64)");
-    auto g = std::make_unique<sd_comm_group>();
-    g->nranks = nranks;
-    g->slot_a.assign(nranks, nullptr);
-    g->slot_b.assign(nranks, nullptr);
-    g->joined.assign(nranks, 0);
-    *out = g.release();
+    *out = new sd_comm_group(nranks);
     return SD_OK;
     SD_GUARD_END
 }

@@ -451,6 +451,49 @@ void test_private_fd_tables() {
     close(p[0]);
 }
 
+// ------------------------------------------------------------------ in-process communicator
+// sd_comm_group's barrier and slots, as sd_cas_dedup_mgpu uses them: publish, barrier,
+// read every peer's slot, barrier -- each rank must see exactly this round's values; and a
+// rank that never arrives makes the others fail with SD_ERR_COMM, leaving the group usable.
+void test_comm_group() {
+    const int R = 5, ROUNDS = 300;
+    sd_comm_group g(R);
+    std::atomic<int> bad{0};
+    std::vector<std::thread> th;
+    for (int r = 0; r < R; r++)
+        th.emplace_back([&, r] {
+            for (int k = 0; k < ROUNDS; k++) {
+                g.slot_a[r] = (const void*)(uintptr_t)(k * R + r + 1);
+                g.barrier();
+                for (int p = 0; p < R; p++)
+                    if (g.slot_a[p] != (const void*)(uintptr_t)(k * R + p + 1)) bad++;
+                g.barrier();
+            }
+        });
+    for (auto& t : th) t.join();
+    CHECK(bad == 0);
+    sd_comm_group h(3);
+    h.timeout_s = 0.2;
+    std::atomic<int> comm_errs{0};
+    th.clear();
+    for (int r = 0; r < 2; r++)  // rank 2 never arrives
+        th.emplace_back([&] {
+            try {
+                h.barrier();
+            } catch (const sd_failure& e) {
+                if (e.rc == SD_ERR_COMM) comm_errs++;
+            }
+        });
+    for (auto& t : th) t.join();
+    CHECK(comm_errs == 2);
+    CHECK(h.arrived == 0);
+    th.clear();
+    h.timeout_s = 30;
+    for (int r = 0; r < 3; r++) th.emplace_back([&] { h.barrier(); });  // all three: it completes
+    for (auto& t : th) t.join();
+    CHECK(h.generation == 1);
+}
+
 // ------------------------------------------------------------------ multi-GPU plans
 void test_exchange_plan() {
     // 3 ranks: rows [to0, to1, to2, base, n, capacity, valid]
@@ -513,6 +556,7 @@ int main() {
     test_cpu_batches();
     test_coalescer();
     test_exchange_plan();
+    test_comm_group();
     test_private_fd_tables();
     // clean up the scratch directory
     if (DIR* d = opendir(g_dir.c_str())) {

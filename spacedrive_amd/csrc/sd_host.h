@@ -7,7 +7,10 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -160,6 +163,43 @@ struct ExchangePlan {
 };
 constexpr int SD_EXCHANGE_ROW_EXTRA = 4;
 ExchangePlan exchange_plan(const uint64_t* rows, int R, int me);
+
+// The in-process communicator's rendezvous (sd_comm_group_create, dedup_mgpu.cpp): its
+// ranks are threads of one process.  A generation barrier plus one published pointer pair
+// per rank: a rank writes its slots before a barrier and reads its peers' after it, the
+// barrier's mutex ordering the two.  A rank that never arrives (its thread failed) makes
+// the others throw SD_ERR_COMM after `timeout_s` rather than hang.
+struct sd_comm_group {
+    int nranks = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    std::vector<const void*> slot_a, slot_b;
+    std::vector<int> joined;
+    double timeout_s = 120.0;
+    explicit sd_comm_group(int n) : nranks(n), slot_a(n, nullptr), slot_b(n, nullptr), joined(n, 0) {}
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t gen = generation;
+        if (++arrived == nranks) {
+            arrived = 0;
+            generation++;
+            cv.notify_all();
+            return;
+        }
+        // a system_clock deadline: libstdc++ waits on it with pthread_cond_timedwait, which
+        // TSan intercepts (a steady_clock wait_for goes to pthread_cond_clockwait, which GCC
+        // 11's TSan does not, and reads as a double lock); a clock step only moves a timeout
+        const auto deadline = std::chrono::system_clock::now() +
+                              std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                                  std::chrono::duration<double>(timeout_s));
+        if (!cv.wait_until(lk, deadline, [&] { return generation != gen; })) {
+            arrived--;
+            throw sd_failure(SD_ERR_COMM, "in-process group: a rank did not reach the barrier in time");
+        }
+    }
+};
 
 // ------------------------------------------------------------------ file reading
 // Reads one file's cas message into staged + e.msg_offset exactly as generate_cas_id reads
