@@ -60,11 +60,18 @@ def sweep(ctx, stream, dev, kind, ns):
 
 
 def main():
+    """--large: the library-scale batches instead (the one-wave-per-file design of the
+    north_star sketch against the shipped throughput kernels at 262 144 files, 500 000
+    sampled files and configs[1]'s 1 M small files)."""
     dev = torch.device("cuda", 0)
     ctx = sd.Context(0)
     stream = torch.cuda.current_stream()
-    out = {"sampled": sweep(ctx, stream, dev, "sampled", (1, 8, 64, 256, 1024, 2048, 4096, 8192, 16384, 65536)),
-           "whole": sweep(ctx, stream, dev, "whole", (1, 16, 100, 256, 1024, 2048, 4096, 8192, 16384, 65536))}
+    if "--large" in sys.argv:
+        out = {"sampled": sweep(ctx, stream, dev, "sampled", (262144, 500000)),
+               "whole": sweep(ctx, stream, dev, "whole", (262144, 1000000))}
+    else:
+        out = {"sampled": sweep(ctx, stream, dev, "sampled", (1, 8, 64, 256, 1024, 2048, 4096, 8192, 16384, 65536)),
+               "whole": sweep(ctx, stream, dev, "whole", (1, 16, 100, 256, 1024, 2048, 4096, 8192, 16384, 65536))}
     print(json.dumps(out))
 
 
