@@ -263,6 +263,16 @@ impl Comm {
             _ => Err(io::Error::new(io::ErrorKind::Other, last_error())),
         }
     }
+    /// One rank of an in-process group: the ranks are threads of this process, each with its
+    /// own context (`ctx`, e.g. one per device from sd_cas_ctx_create); every collective has
+    /// the RCCL communicator's semantics.  Drop every member before the group.
+    pub fn join_local(group: &CommGroup, ctx: *mut sd_cas_ctx, rank: i32) -> Result<Comm, io::Error> {
+        let mut p = std::ptr::null_mut();
+        match unsafe { sd_comm_create_local(ctx, group.0, rank, &mut p) } {
+            SD_OK => Ok(Comm(p)),
+            _ => Err(io::Error::new(io::ErrorKind::Other, last_error())),
+        }
+    }
     pub fn raw(&self) -> *mut sd_comm {
         self.0
     }
@@ -271,5 +281,26 @@ impl Comm {
 impl Drop for Comm {
     fn drop(&mut self) {
         unsafe { sd_comm_destroy(self.0) }
+    }
+}
+
+/// The rendezvous of an in-process group of `nranks` ranks (sd_comm_group_create).
+pub struct CommGroup(*mut sd_comm_group);
+unsafe impl Send for CommGroup {}
+unsafe impl Sync for CommGroup {}
+
+impl CommGroup {
+    pub fn new(nranks: i32) -> Result<CommGroup, io::Error> {
+        let mut p = std::ptr::null_mut();
+        match unsafe { sd_comm_group_create(nranks, &mut p) } {
+            SD_OK => Ok(CommGroup(p)),
+            _ => Err(io::Error::new(io::ErrorKind::Other, last_error())),
+        }
+    }
+}
+
+impl Drop for CommGroup {
+    fn drop(&mut self) {
+        unsafe { sd_comm_group_destroy(self.0) }
     }
 }
