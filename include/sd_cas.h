@@ -217,11 +217,16 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
  * ("read_threads"); a pipe or device sequentially.  Small files are packed many per
  * pinned window, large ones (or ones that grow while read) streamed window by window,
  * whatever their final length; two windows alternate so host reads overlap the H2D
- * copies and the kernels.  Batch policy: a call of at most "checksum_cpu_max" files is
- * hashed by sd_cpu_file_checksums on "read_threads" threads instead -- by default every
- * call, because from the page cache the host's threads hash faster than PCIe can carry the
- * bytes to the GPU; 0 = the GPU route for every call. */
+ * copies and the kernels.  Batch policy: with "checksum_hybrid_threads" g > 0 (default 0:
+ * off), a call whose regular files of >= 8 MiB add up to >= 512 MiB is split between that
+ * GPU route (on g of the "read_threads") and sd_cpu_file_checksums (the rest of the
+ * threads), running at once: the large files go to whichever route is free next, the small
+ * ones to the CPU path.  Any other call of at most "checksum_cpu_max" files is
+ * hashed by sd_cpu_file_checksums on "read_threads" threads -- by default every such call,
+ * because from the page cache the host's threads hash faster than PCIe can carry the bytes
+ * to the GPU; "checksum_cpu_max" 0 = the GPU route alone for every call. */
 int sd_file_checksums_stats(sd_cas_ctx* ctx, uint64_t out[2]);  /* calls: [0] CPU path, [1] GPU */
+int sd_file_checksums_routes(sd_cas_ctx* ctx, uint64_t out[3]); /* [0] CPU path, [1] GPU, [2] split */
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65,
                       int32_t* status);
 
@@ -417,7 +422,9 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * copies; "files_stage_hot" (1): its readers read each file into a per-thread buffer and
  * stream-copy it into the window (0 = read straight into the window); "checksum_cpu_max" (2147483647): sd_file_checksums calls of at most that many
  * files take the CPU path (sd_cpu_file_checksums on "read_threads" threads; 0 = the GPU
- * route always).  Unknown keys fail with SD_ERR_INVALID. */
+ * route always); "checksum_hybrid_threads" (0): reader threads of the GPU route when
+ * sd_file_checksums splits a large call with the CPU path (0 = never split).  Unknown keys
+ * fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);
 int sd_cas_get_tuning(const char* key, int* value);
 /* Read-only probe over d_buf[0, bytes) (bytes a multiple of 4096) for calibrating the

@@ -136,11 +136,12 @@ def coalescer_stats(device: Optional[int] = None) -> dict:
 
 
 def file_checksums_stats(device: Optional[int] = None) -> dict:
-    """Routes taken by file_checksums (sd_file_checksums): calls on the CPU path by the batch
-    policy ("checksum_cpu_max") and calls through the GPU."""
-    v = np.zeros(2, np.uint64)
-    check(lib().sd_file_checksums_stats(default_context(device).handle, _ptr(v)))
-    return {"cpu": int(v[0]), "gpu": int(v[1])}
+    """Routes taken by file_checksums (sd_file_checksums_routes): calls on the CPU path by the
+    batch policy ("checksum_cpu_max"), calls through the GPU alone, and calls split between
+    the GPU route and the CPU path ("checksum_hybrid_threads")."""
+    v = np.zeros(3, np.uint64)
+    check(lib().sd_file_checksums_routes(default_context(device).handle, _ptr(v)))
+    return {"cpu": int(v[0]), "gpu": int(v[1]), "hybrid": int(v[2])}
 
 
 def set_tuning(key: str, value: int) -> None:

@@ -204,7 +204,8 @@ struct sd_cas_ctx {
     std::mutex coal_mu;
     sd_coalescer* coal = nullptr;  // latency path, created on the first single-file call
     std::atomic<uint64_t> files_calls_cpu{0}, files_calls_gpu{0};  // sd_cas_ids_files routes
-    std::atomic<uint64_t> checksum_calls_cpu{0}, checksum_calls_gpu{0};  // sd_file_checksums routes
+    std::atomic<uint64_t> checksum_calls_cpu{0}, checksum_calls_gpu{0},  // sd_file_checksums routes
+        checksum_calls_hybrid{0};
     std::mutex pool_mu;
     // Reader threads.  stage_pool: tasks that open and close their own files (the cas
     // stager, checksum packs), on private fd tables (stage_pool.h); io_pool: parallel preads

@@ -474,6 +474,16 @@ int sd_file_checksums_stats(sd_cas_ctx* ctx, uint64_t out[2]) {
     SD_GUARD_END
 }
 
+int sd_file_checksums_routes(sd_cas_ctx* ctx, uint64_t out[3]) {
+    SD_GUARD_BEGIN
+    if (!ctx || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    out[0] = ctx->checksum_calls_cpu.load(std::memory_order_relaxed);
+    out[1] = ctx->checksum_calls_gpu.load(std::memory_order_relaxed);
+    out[2] = ctx->checksum_calls_hybrid.load(std::memory_order_relaxed);
+    return SD_OK;
+    SD_GUARD_END
+}
+
 // ---------------------------------------------------------------------- checksums
 int sd_checksum_batch_create(sd_cas_ctx* ctx, const uint64_t* offsets, const uint64_t* lens, size_t n,
                              sd_checksum_batch** out) {

@@ -18,6 +18,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <thread>
 
 #include <emmintrin.h>
 
@@ -550,47 +551,44 @@ int sd_cas_hashes_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_
     SD_GUARD_END
 }
 
-// file_checksum (hash.rs:10-24) for n paths.  Each file is read as the reference reads it:
-// hash.rs's 1 MiB read calls until one returns fewer.  For a regular file those reads are
-// exactly its bytes up to EOF, so regular files are read with parallel preads on the
-// context's stager pool ("read_threads"); anything else (a pipe, a device) with the
-// literal sequential loop.  Small regular files are packed (128-B aligned) into the current
-// slot's pinned window by their stat length -- one batch per window, read in parallel,
-// each file probed past its length in case it grew --; while the GPU hashes one slot's
-// window the host reads the next into the other.  Larger files, files that grew, and
-// non-regular files stream window by window (Streamer), whatever their final length.
-int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65, int32_t* status) {
-    SD_GUARD_BEGIN
-    if (!ctx || (n && (!paths || !out_hex65 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
-    // batch policy: from the page cache the host's threads hash faster than PCIe carries
-    // the bytes, so by default every call takes the CPU path;
-    // "checksum_cpu_max" = 0 sends every call to the GPU route below
-    if (n <= (size_t)std::max(0, tuning_get(SD_TUNE_CHECKSUM_CPU_MAX))) {
-        ctx->checksum_calls_cpu.fetch_add(1, std::memory_order_relaxed);
-        return sd_cpu_file_checksums(paths, n, out_hex65, status,
-                                     std::max(1, std::min(64, tuning_get(SD_TUNE_READ_THREADS))));
-    }
-    ctx->checksum_calls_gpu.fetch_add(1, std::memory_order_relaxed);
-    ctx->bind();
-    // packs of at most 32 MiB: a pack is read whole before its copy starts, so smaller packs
-    // let the next pack's reads overlap this one's H2D and kernels (one 80 MB pack of 100
-    // files took 4.7 ms against 2.3 ms for the CPU path, read-bound alike)
-    constexpr uint64_t PACK = 32ull << 20;
-    const int read_threads = std::max(1, std::min(64, tuning_get(SD_TUNE_READ_THREADS)));
-    std::shared_ptr<StagePool> pool = ctx->stage_pool(read_threads);  // per-file tasks (stat, packs)
-    std::shared_ptr<StagePool> iopool;  // preads of one open file (streamed files), created on first use
-    SlotPair slots(ctx);
-    Streamer::prepare(slots);
-    // stat every file in parallel: its length picks the route (regular files only)
-    std::vector<uint64_t> hint(n, 0);
-    std::vector<uint8_t> regular(n, 0);
-    pool->run(n, [&](size_t i) {
+namespace {
+
+// stat every file in parallel: its length picks the route (regular files only)
+void stat_files(StagePool& pool, const char* const* paths, size_t n, std::vector<uint64_t>& hint,
+                std::vector<uint8_t>& regular) {
+    hint.assign(n, 0);
+    regular.assign(n, 0);
+    pool.run(n, [&](size_t i) {
         struct stat st;
         if (stat(paths[i], &st) == 0 && S_ISREG(st.st_mode)) {
             hint[i] = (uint64_t)st.st_size;
             regular[i] = 1;
         }
     });
+}
+
+// The GPU route of sd_file_checksums over the files next() yields (SIZE_MAX ends them), on
+// `read_threads` reader threads.  Each file is read as the reference reads it: hash.rs's
+// 1 MiB read calls until one returns fewer.  For a regular file those reads are exactly its
+// bytes up to EOF, so regular files are read with parallel preads; anything else (a pipe,
+// a device) with the literal sequential loop.  Small regular files are packed (128-B
+// aligned) into the current slot's pinned window by their stat length -- one batch per
+// window, read in parallel, each file probed past its length in case it grew --; while the
+// GPU hashes one slot's window the host reads the next into the other.  Larger files,
+// files that grew, and non-regular files stream window by window (Streamer), whatever their
+// final length.  hint / regular: stat_files' output for all n files.
+void gpu_file_checksums(sd_cas_ctx* ctx, const char* const* paths, char* out_hex65, int32_t* status,
+                        int read_threads, const std::vector<uint64_t>& hint, const std::vector<uint8_t>& regular,
+                        const std::function<size_t()>& next) {
+    ctx->bind();
+    // packs of at most 32 MiB: a pack is read whole before its copy starts, so smaller packs
+    // let the next pack's reads overlap this one's H2D and kernels (one 80 MB pack of 100
+    // files took 4.7 ms against 2.3 ms for the CPU path, read-bound alike)
+    constexpr uint64_t PACK = 32ull << 20;
+    std::shared_ptr<StagePool> pool = ctx->stage_pool(read_threads);  // per-file tasks (packs)
+    std::shared_ptr<StagePool> iopool;  // preads of one open file (streamed files), created on first use
+    SlotPair slots(ctx);
+    Streamer::prepare(slots);
     struct Pending {
         std::vector<size_t> files;  // files whose hashes land in this slot's host_hashes
         bool busy = false;
@@ -690,7 +688,7 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
         pend[k].files = std::move(ok);
         pend[k].busy = true;
     };
-    for (size_t i = 0; i < n; i++) {
+    for (size_t i; (i = next()) != SIZE_MAX;) {
         status[i] = SD_FILE_OK;
         if (!regular[i] || hint[i] + 128 > PACK / 2) {  // a pipe / device / unreadable path, or large
             submit_pack();
@@ -713,6 +711,106 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
     harvest(0);
     harvest(1);
     streamer.finish(slots);
+}
+
+}  // namespace
+
+// file_checksum (hash.rs:10-24) for n paths: the batch policy picks the CPU path, the GPU
+// route (gpu_file_checksums) or both at once.
+//   * "checksum_cpu_max" = 0: the GPU route for every call.
+//   * Hybrid ("checksum_hybrid_threads" = g > 0; off by default): a call whose regular files
+//     of >= 8 MiB add up to >= 512 MiB is split.  From the page cache the GPU route is
+//     PCIe-bound with few reader threads while the CPU path is bound by its threads
+//     (scripts/hybrid_checksum_probe.py), so the GPU route gets g of the "read_threads" and
+//     the CPU path the rest, on a second host thread.  The large files go to whichever
+//     route is free next (one shared cursor, largest first), so neither waits on a static
+//     split; the small and non-regular files go to the CPU path.  Measured from the page
+//     cache (profiles/r3/r3z_hybrid_checksum_probe.json) it is not a reliable win: the GPU
+//     route's reader threads spend about as much CPU copying page-cache bytes into pinned
+//     memory as the CPU path spends reading and hashing them, so the split moves little
+//     work off the host (78-90 GB/s against 81-87 for the CPU path alone).  Kept opt-in for
+//     hosts with fewer cores per GPU.
+//   * Otherwise calls of at most "checksum_cpu_max" files (default: all) take the CPU path:
+//     from the page cache the host's threads hash faster than PCIe carries the bytes.
+int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65, int32_t* status) {
+    SD_GUARD_BEGIN
+    if (!ctx || (n && (!paths || !out_hex65 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
+    const int threads = std::max(1, std::min(64, tuning_get(SD_TUNE_READ_THREADS)));
+    const int cpu_max = std::max(0, tuning_get(SD_TUNE_CHECKSUM_CPU_MAX));
+    const int hyb = std::max(0, tuning_get(SD_TUNE_CHECKSUM_HYBRID_THREADS));
+    std::vector<uint64_t> hint;
+    std::vector<uint8_t> regular;
+    if (cpu_max != 0 && hyb > 0 && hyb < threads && n >= 2) {
+        constexpr uint64_t BIG_FILE = 8ull << 20, BIG_TOTAL = 512ull << 20;
+        stat_files(*ctx->stage_pool(threads), paths, n, hint, regular);
+        std::vector<size_t> big, rest;
+        uint64_t big_bytes = 0;
+        for (size_t i = 0; i < n; i++) {
+            if (regular[i] && hint[i] >= BIG_FILE) {
+                big.push_back(i);
+                big_bytes += hint[i];
+            } else {
+                rest.push_back(i);
+            }
+        }
+        if (big.size() >= 2 && big_bytes >= BIG_TOTAL) {
+            ctx->checksum_calls_hybrid.fetch_add(1, std::memory_order_relaxed);
+            std::stable_sort(big.begin(), big.end(), [&](size_t a, size_t b) { return hint[a] > hint[b]; });
+            std::atomic<size_t> cursor{0};
+            auto next_big = [&]() -> size_t {
+                const size_t k = cursor.fetch_add(1, std::memory_order_relaxed);
+                return k < big.size() ? big[k] : SIZE_MAX;
+            };
+            const int cpu_threads = threads - hyb;
+            int cpu_rc = SD_OK;
+            std::string cpu_err;
+            std::thread cpu([&] {
+                if (!rest.empty()) {  // the small and non-regular files: one CPU-path call
+                    std::vector<const char*> p(rest.size());
+                    std::vector<char> hex(rest.size() * 65);
+                    std::vector<int32_t> st(rest.size());
+                    for (size_t q = 0; q < rest.size(); q++) p[q] = paths[rest[q]];
+                    cpu_rc = sd_cpu_file_checksums(p.data(), rest.size(), hex.data(), st.data(), cpu_threads);
+                    if (cpu_rc != SD_OK) {
+                        cpu_err = sd_cas_last_error();
+                        cursor.store(big.size());  // stop the GPU route at its next file
+                        return;
+                    }
+                    for (size_t q = 0; q < rest.size(); q++) {
+                        status[rest[q]] = st[q];
+                        memcpy(out_hex65 + 65 * rest[q], hex.data() + 65 * q, 65);
+                    }
+                }
+                for (size_t i; (i = next_big()) != SIZE_MAX;) {  // then large files, as they come
+                    cpu_rc = sd_cpu_file_checksums(paths + i, 1, out_hex65 + 65 * i, status + i, cpu_threads);
+                    if (cpu_rc != SD_OK) {
+                        cpu_err = sd_cas_last_error();
+                        cursor.store(big.size());
+                        return;
+                    }
+                }
+            });
+            try {
+                gpu_file_checksums(ctx, paths, out_hex65, status, hyb, hint, regular, next_big);
+            } catch (...) {
+                cursor.store(big.size());  // the CPU thread takes no further file
+                cpu.join();
+                throw;
+            }
+            cpu.join();
+            if (cpu_rc != SD_OK) throw sd_failure(cpu_rc, cpu_err);
+            return SD_OK;
+        }
+    }
+    if (n <= (size_t)cpu_max) {
+        ctx->checksum_calls_cpu.fetch_add(1, std::memory_order_relaxed);
+        return sd_cpu_file_checksums(paths, n, out_hex65, status, threads);
+    }
+    ctx->checksum_calls_gpu.fetch_add(1, std::memory_order_relaxed);
+    if (hint.size() != n) stat_files(*ctx->stage_pool(threads), paths, n, hint, regular);
+    size_t i = 0;
+    gpu_file_checksums(ctx, paths, out_hex65, status, threads, hint, regular,
+                       [&]() -> size_t { return i < n ? i++ : SIZE_MAX; });
     return SD_OK;
     SD_GUARD_END
 }

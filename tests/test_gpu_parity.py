@@ -478,6 +478,68 @@ def test_file_checksums_packing_and_streaming(ctx, tmp_path):
         assert got[i] == want[i], (i, sizes[i])
 
 
+def test_file_checksums_hybrid_split(ctx, tmp_path):
+    """sd_file_checksums' split policy (opt-in "checksum_hybrid_threads"): a call whose regular
+    files of >= 8 MiB total >= 512 MiB runs the GPU route and the CPU path at once, the large
+    files going to whichever is free, the small ones and a FIFO to the CPU path.  Every
+    result equals the oracle's read schedule (hash.rs:10-24), an unreadable path keeps its
+    error, and the call is counted as split; below the threshold the CPU path alone runs."""
+    import threading
+    import spacedrive_amd as sd
+    from oracle import native
+    MiB = 1 << 20
+    sizes = [40 * MiB + 3, 8 * MiB, 3000, 0, 96 * MiB + 1, 64 * MiB, 12345, 130 * MiB + 77, 16 * MiB - 1,
+             72 * MiB, 5 * MiB, 100 * MiB + 5, 33 * MiB]
+    paths = []
+    for i, sz in enumerate(sizes):
+        p = tmp_path / f"h{i}"
+        with open(p, "wb") as f:
+            pos = 0
+            while pos < sz:
+                k = min(32 << 20, sz - pos)
+                f.write(cs.synth_bytes(5000 + i, 0, pos, k))
+                pos += k
+        paths.append(str(p))
+    fifo = str(tmp_path / "fifo")
+    os.mkfifo(fifo)
+    fifo_data = cs.synth_bytes(6000, 0, 0, 4000)  # one write: hash.rs's first read returns it
+
+    def feed():
+        with open(fifo, "wb", buffering=0) as f:
+            f.write(fifo_data)
+    paths.insert(5, fifo)
+    paths.insert(9, str(tmp_path / "missing"))
+    want_h, want_st = native.file_checksums([p for p in paths if p != fifo], nthreads=NT)
+    want = dict(zip([p for p in paths if p != fifo], zip(want_h, want_st)))
+    keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads")}
+    sd.set_tuning("checksum_cpu_max", 2147483647)  # the library default (the module sets 0)
+    sd.set_tuning("checksum_hybrid_threads", 6)  # opt-in
+    try:
+        before = sd.file_checksums_stats()
+        t = threading.Thread(target=feed)
+        t.start()
+        got = sd.file_checksums(paths)
+        t.join()
+        after = sd.file_checksums_stats()
+        assert after["hybrid"] == before["hybrid"] + 1 and after["cpu"] == before["cpu"]
+        assert got[5] == native.blake3(fifo_data).hex()
+        for p, g in zip(paths, got):
+            if p == fifo:
+                continue
+            h, st = want[p]
+            if st != 0:
+                assert isinstance(g, OSError), p
+            else:
+                assert g == h.tobytes().hex(), p
+        # under 512 MiB of large files: the CPU path alone
+        small_call = [p for p, sz in zip(paths[:4], sizes[:4])]
+        sd.file_checksums(small_call)
+        assert sd.file_checksums_stats()["cpu"] == after["cpu"] + 1
+    finally:
+        for k, v in keep.items():
+            sd.set_tuning(k, v)
+
+
 def test_concurrent_callers_share_a_context(ctx, tmp_path):
     # the C ABI is thread-safe and re-entrant: 6 host threads, one context
     import threading
