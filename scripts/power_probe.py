@@ -3,8 +3,11 @@ is the hashing kernels' clock under load (2.1-2.2 GHz against 2.38 GHz for the G
 registers) set by the power limit?  hwmon sysfs of the visible card, sampled every 20 ms
 on a host thread while the GPU runs:
 
+  idle        nothing launched (the board's floor)
   valu_peak   k_valu_peak: the kernels' G block from registers (sd_valu_peak)
   hbm_read    sd_read_probe pattern 0: a coalesced 16 GiB read, no hashing
+  hbm_read_lane_1k / _2k   the same bytes read as the hashing kernels do: one lane per 1 KiB
+              chunk (2 KiB chunk pair), 16 B loads walking it -- energy per byte by pattern
   sampled     CasBatch.run over 250 000 sampled files (k_cas_sampled_lanes + _merge)
   checksum    ChecksumBatch.run over 4 x 1 GiB (k_ck_leaf + k_ck_reduce)
 
@@ -26,11 +29,20 @@ from spacedrive_amd._native import check, lib  # noqa: E402
 
 
 def hwmon_dirs():
+    """The visible device's hwmon first (matched by PCI address: the host's other cards are
+    listed in sysfs too), then the rest."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    buf = ctypes.create_string_buffer(64)
+    mine = ""
+    if hip.hipDeviceGetPCIBusId(buf, 64, 0) == 0:
+        mine = buf.value.decode().lower()
     out = []
     for h in sorted(glob.glob("/sys/class/drm/card*/device/hwmon/hwmon*")):
         names = os.listdir(h)
         if any(n.startswith("power1") for n in names) or "freq1_input" in names:
-            out.append(h)
+            pci = os.path.basename(os.path.realpath(os.path.join(h, "..", ".."))).lower()
+            out.insert(0, h) if mine and pci == mine else out.append(h)
     return out
 
 
@@ -69,7 +81,7 @@ def main():
     secs = float(sys.argv[1]) if len(sys.argv) > 1 else 4.0
     ctx = sd.default_context(0)
     dirs = hwmon_dirs()
-    res = {"hwmon": dirs, "seconds": secs, "modes": {}}
+    res = {"hwmon": dirs, "hwmon_of_this_device": dirs[0] if dirs else None, "seconds": secs, "modes": {}}
     # inputs
     n = 250_000
     sizes = np.full(n, 1 << 30, np.uint64) + np.arange(n, dtype=np.uint64)
@@ -95,8 +107,11 @@ def main():
     L = lib()
     s = torch.cuda.current_stream().cuda_stream
     modes = {
+        "idle": lambda: time.sleep(0.005),
         "valu_peak": lambda: ctx.valu_peak(),
         "hbm_read": lambda: check(L.sd_read_probe(ctx.handle, d_rd.data_ptr(), d_rd.numel(), 0, s)),
+        "hbm_read_lane_1k": lambda: check(L.sd_read_probe(ctx.handle, d_rd.data_ptr(), d_rd.numel(), 1, s)),
+        "hbm_read_lane_2k": lambda: check(L.sd_read_probe(ctx.handle, d_rd.data_ptr(), d_rd.numel(), 2, s)),
         "sampled": lambda: cas.run(d_st, d_hash),
         "checksum": lambda: ck.run(d_ck, d_ckh),
     }
