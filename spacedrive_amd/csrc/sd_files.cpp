@@ -765,6 +765,7 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
             int cpu_rc = SD_OK;
             std::string cpu_err;
             std::thread cpu([&] {
+              try {
                 if (!rest.empty()) {  // the small and non-regular files: one CPU-path call
                     std::vector<const char*> p(rest.size());
                     std::vector<char> hex(rest.size() * 65);
@@ -789,6 +790,11 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
                         return;
                     }
                 }
+              } catch (...) {  // an allocation here: nothing may escape a thread
+                cpu_rc = SD_ERR_NOMEM;
+                cpu_err = "host allocation failed in the CPU half of a split sd_file_checksums call";
+                cursor.store(big.size());
+              }
             });
             try {
                 gpu_file_checksums(ctx, paths, out_hex65, status, hyb, hint, regular, next_big);
