@@ -48,7 +48,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 # rate datapath, not a harness limit.  BLAKE3's G mix written in asm, registers only, issues
 # at 39.5 T = 64.7 lane-ops/clk/CU (the in-library k_valu_peak is the same block: 39.3-39.5 T,
 # profiles/r3/r3d_valu_peak.txt).  So the roof is 64 lane-ops/clk/CU x 256 CU x 2.4 GHz:
-VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
+N_CUS = 256
+VALU_PEAK_TOPS = N_CUS * 64 * 2.4e9 / 1e12
 # The guide's full VALU rate (MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 op in 2
 # cycles): 256 x 128 x 2.4 GHz = 78.6 T lane-ops/s -- reported as frac_full_rate.
 VALU_FULL_RATE_TOPS = 256 * 128 * 2.4e9 / 1e12
@@ -142,6 +143,64 @@ def pmc_traffic_sum(kernels, grids):
 
 def whole_grid(batch) -> int:
     return ((batch.full_items + 255) // 256 + (batch.tail_items + 255) // 256) * 256
+
+
+class ClockSampler:
+    """This device's shader clock and board power from its hwmon (sysfs; the host's other
+    cards are listed too, so the device is matched by PCI address), sampled every 10 ms on a
+    host thread while the timed steps run: the clock the kernels actually ran at, so the
+    roofline can say how much of the gap to the nominal 2.4 GHz ceiling is the clock
+    (the board's power limit) and how much is issue.  None when unreadable."""
+
+    def __init__(self, device: int):
+        import glob
+        self.dir, self.rows, self.stop, self.t = None, [], None, None
+        try:
+            import ctypes
+            buf = ctypes.create_string_buffer(64)
+            if ctypes.CDLL("libamdhip64.so").hipDeviceGetPCIBusId(buf, 64, int(device)) != 0:
+                return
+            want = buf.value.decode().lower()
+            for h in glob.glob("/sys/class/drm/card*/device/hwmon/hwmon*"):
+                pci = os.path.basename(os.path.realpath(os.path.join(h, "..", ".."))).lower()
+                if pci == want and os.path.exists(os.path.join(h, "freq1_input")):
+                    self.dir = h
+        except Exception:  # noqa: BLE001 -- a diagnostic: absent is fine
+            self.dir = None
+
+    def _read(self, key):
+        try:
+            with open(os.path.join(self.dir, key)) as f:
+                return int(f.read().strip())
+        except (OSError, ValueError):
+            return None
+
+    def _run(self):
+        while not self.stop.is_set():
+            self.rows.append((self._read("freq1_input"), self._read("power1_input")))
+            self.stop.wait(0.01)
+
+    def start(self):
+        import threading
+        if self.dir:
+            self.stop = threading.Event()
+            self.t = threading.Thread(target=self._run, daemon=True)
+            self.t.start()
+        return self
+
+    def result(self):
+        if not self.dir or self.t is None:
+            return None
+        self.stop.set()
+        self.t.join()
+        f = [r[0] for r in self.rows if r[0]]
+        p = [r[1] for r in self.rows if r[1]]
+        if not f:
+            return None
+        return {"sclk_mhz_median": float(np.median(f)) / 1e6, "sclk_mhz_min": min(f) / 1e6, "samples": len(f),
+                "board_power_w_median": float(np.median(p)) / 1e6 if p else None,
+                "power_cap_w": (self._read("power1_cap") or 0) / 1e6 or None, "hwmon": self.dir,
+                "note": "this device's hwmon, sampled every 10 ms over the timed steps"}
 
 
 def valu_roof(compressions: int, ms: float) -> dict:
@@ -984,6 +1043,7 @@ def main():
               "note": "each step's hashing, then its dedup, on one stream (the kernel breakdown below)"}
     value = serial["value"]
     pipelined = None
+    clock_res = None
     if rccl is not None and not args.no_overlap:
         # The same K steps as an indexer runs consecutive batches: batch k's exchange and
         # grouping (sd_cas_dedup_mgpu, its host syncs, the RCCL collectives) on one stream
@@ -1028,12 +1088,14 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        clock = ClockSampler(dev.index if dev.index is not None else 0).start()
         t0 = time.perf_counter()
         pres = pipelined_steps(args.steps, timed=True)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         p_elapsed = time.perf_counter() - t0
+        clock_res = clock.result()
         if world > 1:
             t = torch.tensor([p_elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1085,6 +1147,10 @@ def main():
                      "algorithmic": {"compressions_per_launch": dom_comp, "lane_ops_per_compression": 672,
                                      "bytes_per_launch": dom_bytes,
                                      "per_unit": "sampled file: 953 compressions, 57352 B read + 32 B written"},
+                     "clock": clock_res,
+                     "frac_of_issue_ceiling_at_clock": (
+                         dom["achieved"] * 1e12 / (64 * N_CUS * clock_res["sclk_mhz_median"] * 1e6)
+                         if clock_res else None),
                      "measured_valu_peak": valu_peak / 1e12,
                      "frac_of_measured_peak": dom["achieved"] * 1e12 / valu_peak if valu_peak else None,
                      "hbm": {"achieved": dom_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
