@@ -521,7 +521,9 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
     h1 = torch.zeros(nfiles * 32, dtype=torch.uint8, device=dev)
     b.run(d_staged, h0, stream)
     cold_ms = warm(lambda: b.run(d_staged, h1, stream), stream, warm_ms)
+    clock = ClockSampler(dev.index if dev.index is not None else 0).start()
     ms = ev_ms(lambda: b.run(d_staged, h1, stream), stream, reps=reps)
+    clock_res = clock.result()
     deterministic = bool(torch.equal(h0, h1))
     roof = valu_roof(b.compressions, ms)
     if which == "sampled":
@@ -538,6 +540,9 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
            "msg_GBps": b.msg_bytes / (ms * 1e-3) / 1e9, "compressions": b.compressions,
            "valu_frac": roof["frac"], "valu_frac_full_rate": roof["frac_full_rate"],
            "valu_frac_of_measured_peak": roof["achieved"] * 1e12 / valu_peak if valu_peak else None,
+           "clock": clock_res,
+           "valu_frac_at_clock": (roof["achieved"] * 1e12 / (64 * N_CUS * clock_res["sclk_mhz_median"] * 1e6)
+                                  if clock_res else None),
            "kernels": kernels, "launch_grid": grid,
            "traffic": tr["bytes"] if tr else None, "deterministic": deterministic}
     del d_staged, h0, h1, b
@@ -1228,7 +1233,9 @@ def main():
         d_sum = torch.empty(nf * 32, dtype=torch.uint8, device=dev)
         cb.run(d_data, d_sum, stream)
         warm(lambda: cb.run(d_data, d_sum, stream), stream, args.warm_ms)
+        ck_clock = ClockSampler(dev.index if dev.index is not None else 0).start()
         ck_ms = ev_ms(lambda: cb.run(d_data, d_sum, stream), stream, reps=args.checksum_steps)
+        ck_clock = ck_clock.result()
         gbps = cb.total_bytes / (ck_ms * 1e-3) / 1e9
         tot = torch.tensor([gbps], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         if world > 1:
@@ -1240,6 +1247,10 @@ def main():
                            "roofline": {"bound": "valu", "achieved": roof["achieved"], "peak": VALU_PEAK_TOPS,
                                         "unit": "T int32 VALU lane-ops/s", "frac": roof["frac"],
                                         "frac_full_rate": roof["frac_full_rate"], "peak_basis": PEAK_BASIS,
+                                        "clock": ck_clock,
+                                        "frac_of_issue_ceiling_at_clock": (
+                                            roof["achieved"] * 1e12 / (64 * N_CUS * ck_clock["sclk_mhz_median"] * 1e6)
+                                            if ck_clock else None),
                                         "hbm": {"achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                                 "frac": gbps / HBM_PEAK_GBPS}},
                            "launch_grid": cb.blocks * 256, "traffic": tr_ck["bytes"] if tr_ck else None}
