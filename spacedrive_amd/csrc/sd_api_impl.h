@@ -169,18 +169,6 @@ struct sd_cas_batch {
     // byte ranges, its hashes scattered to out[long_idx[i]]
     sd_checksum_batch lng;
     sdi::DevBuf long_out;
-    // "batch_fork": the whole-kind kernels on a second stream beside the sampled ones,
-    // forked from and joined back to the caller's stream by events (created on first use)
-    struct ForkJoin {
-        hipStream_t side = nullptr;
-        hipEvent_t fork = nullptr, join = nullptr;
-        ~ForkJoin() {
-            if (fork) (void)hipEventDestroy(fork);
-            if (join) (void)hipEventDestroy(join);
-            if (side) (void)hipStreamDestroy(side);
-        }
-    };
-    mutable ForkJoin fj;
     // host tables (packed into tab by the plan)
     std::vector<uint32_t> h_sidx, h_long_idx;
     std::vector<sd_u32x4> h_wrows;  // whole_wave: (u64 message offset, length, output row)

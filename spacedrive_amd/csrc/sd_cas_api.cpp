@@ -141,23 +141,11 @@ void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_ha
     uint32_t* out = reinterpret_cast<uint32_t*>(d_hash32);
     // small batches take the latency kernels (one wave / workgroup per file), large ones the
     // throughput kernels; the plan chose ("sampled_wave_max", "whole_wave_max")
-    const hipStream_t s0 = s;
-    const bool fork = tuning_get(SD_TUNE_BATCH_FORK) > 0 && (parts & SD_PART_SAMPLED) && (parts & SD_PART_WHOLE) &&
-                      b->n_sampled && !b->sampled_wave && b->n_whole && !b->whole_wave;
-    if (fork) {  // the whole-kind kernels on the side stream, after everything before on s
-        auto& fj = b->fj;
-        if (!fj.side) HIP_CHECK(hipStreamCreateWithFlags(&fj.side, hipStreamNonBlocking));
-        if (!fj.fork) HIP_CHECK(hipEventCreateWithFlags(&fj.fork, hipEventDisableTiming));
-        if (!fj.join) HIP_CHECK(hipEventCreateWithFlags(&fj.join, hipEventDisableTiming));
-        HIP_CHECK(hipEventRecord(fj.fork, s0));
-        HIP_CHECK(hipStreamWaitEvent(fj.side, fj.fork, 0));
-    }
     if ((parts & SD_PART_SAMPLED) && b->sampled_wave)
         HIP_CHECK(sdk::launch_cas_sampled_wave(d_staged, b->d_soff(), b->d_sidx(), b->n_sampled, out, s));
     else if (parts & SD_PART_SAMPLED)
         HIP_CHECK(sdk::launch_cas_sampled(d_staged, b->d_soff(), b->d_sidx(), b->n_sampled, b->srows.as<uint32_t>(),
                                           out, s));
-    if (fork) s = b->fj.side;
     if (parts & SD_PART_WHOLE) {
         const WholePlan& w = b->whole;
         if (b->whole_wave)
@@ -172,10 +160,6 @@ void run_cas_batch(const sd_cas_batch* b, const uint8_t* d_staged, uint8_t* d_ha
             HIP_CHECK(sdk::launch_scatter_hash(b->long_out.as<uint32_t>(), b->d_lidx(), b->n_long, out,
                                                s));
         }
-    }
-    if (fork) {  // join: the caller's stream waits for the side stream's kernels
-        HIP_CHECK(hipEventRecord(b->fj.join, b->fj.side));
-        HIP_CHECK(hipStreamWaitEvent(s0, b->fj.join, 0));
     }
 }
 

@@ -34,12 +34,12 @@ thread_local std::string g_err;
 // of sd_file_checksums calls between the GPU route and the CPU path (opt-in: from the page
 // cache it measured 78-90 GB/s against 81-87 for the CPU path alone, within the box's
 // noise; profiles/r3/r3z_hybrid_checksum_probe.json)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {0}, {0}};
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {0}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
                                                "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",
                                                "files_ring",         "checksum_cpu_max", "files_stage_hot",
-                                               "checksum_hybrid_threads", "batch_fork"};
+                                               "checksum_hybrid_threads"};
 }  // namespace
 
 void sd_set_err(const char* fmt, ...) {
