@@ -50,6 +50,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 # profiles/r3/r3d_valu_peak.txt).  So the roof is 64 lane-ops/clk/CU x 256 CU x 2.4 GHz:
 N_CUS = 256
 VALU_PEAK_TOPS = N_CUS * 64 * 2.4e9 / 1e12
+# The G mix's measured issue rate per clock (valu_probe7, 8 waves/SIMD: 39.51 T at 2386 MHz =
+# 64.7 lane-ops/clk/CU): the denominator of the roofline's frac at the measured clock.
+G_MIX_LANE_OPS_PER_CLK = 64.7
 # The guide's full VALU rate (MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 op in 2
 # cycles): 256 x 128 x 2.4 GHz = 78.6 T lane-ops/s -- reported as frac_full_rate.
 VALU_FULL_RATE_TOPS = 256 * 128 * 2.4e9 / 1e12
@@ -541,7 +544,8 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
            "valu_frac": roof["frac"], "valu_frac_full_rate": roof["frac_full_rate"],
            "valu_frac_of_measured_peak": roof["achieved"] * 1e12 / valu_peak if valu_peak else None,
            "clock": clock_res,
-           "valu_frac_at_clock": (roof["achieved"] * 1e12 / (64 * N_CUS * clock_res["sclk_mhz_median"] * 1e6)
+           "valu_frac_at_clock": (roof["achieved"] * 1e12
+                                  / (G_MIX_LANE_OPS_PER_CLK * N_CUS * clock_res["sclk_mhz_median"] * 1e6)
                                   if clock_res else None),
            "kernels": kernels, "launch_grid": grid,
            "traffic": tr["bytes"] if tr else None, "deterministic": deterministic}
@@ -1154,7 +1158,7 @@ def main():
                                      "per_unit": "sampled file: 953 compressions, 57352 B read + 32 B written"},
                      "clock": clock_res,
                      "frac_of_issue_ceiling_at_clock": (
-                         dom["achieved"] * 1e12 / (64 * N_CUS * clock_res["sclk_mhz_median"] * 1e6)
+                         dom["achieved"] * 1e12 / (G_MIX_LANE_OPS_PER_CLK * N_CUS * clock_res["sclk_mhz_median"] * 1e6)
                          if clock_res else None),
                      "measured_valu_peak": valu_peak / 1e12,
                      "frac_of_measured_peak": dom["achieved"] * 1e12 / valu_peak if valu_peak else None,
@@ -1249,7 +1253,8 @@ def main():
                                         "frac_full_rate": roof["frac_full_rate"], "peak_basis": PEAK_BASIS,
                                         "clock": ck_clock,
                                         "frac_of_issue_ceiling_at_clock": (
-                                            roof["achieved"] * 1e12 / (64 * N_CUS * ck_clock["sclk_mhz_median"] * 1e6)
+                                            roof["achieved"] * 1e12
+                                            / (G_MIX_LANE_OPS_PER_CLK * N_CUS * ck_clock["sclk_mhz_median"] * 1e6)
                                             if ck_clock else None),
                                         "hbm": {"achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                                 "frac": gbps / HBM_PEAK_GBPS}},
