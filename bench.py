@@ -418,17 +418,34 @@ def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1):
     def call():
         check(lib().sd_cas_ids(ctx.handle, host.data_ptr(), nbytes, sub.ctypes.data, k, out, None))
 
-    call()  # warm: the context's windows and tables
-    reps = 2
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        call()
-    e2e_s = (time.perf_counter() - t0) / reps
-    if world > 1:
-        dist.barrier()
+    import spacedrive_amd as sd
+    keep = sd.get_tuning("host_cohash_threads")
+    e2e = {}
+    for mode, h in (("gpu_only", 0), ("default", keep)):  # the GPU alone, then the library default
+        sd.set_tuning("host_cohash_threads", h)
+        try:
+            call()  # warm: the context's windows and tables
+            reps = 2
+            if world > 1:
+                dist.barrier()
+            s0 = np.zeros(2, np.uint64)
+            s1 = np.zeros(2, np.uint64)
+            check(lib().sd_cas_ids_stats(ctx.handle, s0.ctypes.data))
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                call()
+            e2e[mode] = ((time.perf_counter() - t0) / reps, h)
+            check(lib().sd_cas_ids_stats(ctx.handle, s1.ctypes.data))
+            e2e[mode] += (float((s1 - s0)[1]) / (reps * k),)
+            if world > 1:
+                dist.barrier()
+        finally:
+            sd.set_tuning("host_cohash_threads", keep)
+        if mode == "gpu_only":
+            raw_gpu = out.raw
+    e2e_s = e2e["default"][0]
     raw = out.raw  # one copy: each .raw access copies the whole buffer
+    assert raw == raw_gpu, "sd_cas_ids with host co-hashing differs from the GPU alone"
     got = np.frombuffer(bytes.fromhex("".join(raw[17 * i:17 * i + 16].decode() for i in range(k))),
                         np.uint8).reshape(k, 8)
     assert np.array_equal(got, want), "sd_cas_ids differs from the device-resident batch"
@@ -436,9 +453,15 @@ def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1):
            "kernel_ms": kernel_ms, "kernel_files_per_s": k / (kernel_ms * 1e-3),
            "end_to_end_ms": e2e_s * 1e3, "end_to_end_files_per_s": k / e2e_s,
            "end_to_end_GBps": nbytes / e2e_s / 1e9,
+           "host_cohash_threads": e2e["default"][1], "host_share": e2e["default"][2],
+           "gpu_only": {"end_to_end_ms": e2e["gpu_only"][0] * 1e3,
+                        "end_to_end_files_per_s": k / e2e["gpu_only"][0],
+                        "end_to_end_GBps": nbytes / e2e["gpu_only"][0] / 1e9},
            "note": "sd_cas_ids from pinned host memory (mean of 2 calls after a warm one, all ranks at once): "
-                   "plan + H2D + kernels + D2H + hex, 512 MiB windows on two streams; h2d_ms = one raw copy of the "
-                   "same bytes (HIP events); kernel_ms = the same files device-resident"}
+                   "plan + H2D + kernels + D2H + hex, 512 MiB windows on two streams, with the library default "
+                   "of host_cohash_threads host threads hashing files from the end of the list meanwhile "
+                   "(host_share = their fraction of the files); gpu_only = the same call with 0; h2d_ms = one "
+                   "raw copy of the same bytes (HIP events); kernel_ms = the same files device-resident"}
     if world > 1:
         rows = [None] * world
         dist.all_gather_object(rows, [e2e_s, k, nbytes])

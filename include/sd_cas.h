@@ -139,7 +139,12 @@ int sd_cas_stage_files(const char* const* paths, sd_extent* extents, size_t n, u
  * 16 lowercase hex chars + NUL (cas.rs:61), 17 bytes per file.  status may be NULL;
  * entries whose status[i] != SD_FILE_OK on input are skipped and left untouched.  Whole-
  * kind messages of any length are accepted (longer than 8 + 102400 B: hashed by the
- * chunk-parallel checksum kernels). */
+ * chunk-parallel checksum kernels).  A call of >= 16384 files is PCIe-bound, and feeding
+ * the GPU costs the host only DMA, so "host_cohash_threads" (default 15; 0 = GPU only)
+ * host threads hash files from the end of the list on the library's CPU path meanwhile,
+ * the GPU taking windows from the front until the two meet; sd_cas_ids_stats counts the
+ * files each side hashed. */
+int sd_cas_ids_stats(sd_cas_ctx* ctx, uint64_t out[2]); /* files hashed: [0] GPU, [1] host threads */
 int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes,
                const sd_extent* extents, size_t n, char* out_hex17, int32_t* status);
 
@@ -423,7 +428,9 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * stream-copy it into the window (0 = read straight into the window); "checksum_cpu_max" (2147483647): sd_file_checksums calls of at most that many
  * files take the CPU path (sd_cpu_file_checksums on "read_threads" threads; 0 = the GPU
  * route always); "checksum_hybrid_threads" (0): reader threads of the GPU route when
- * sd_file_checksums splits a large call with the CPU path (0 = never split).  Unknown keys
+ * sd_file_checksums splits a large call with the CPU path (0 = never split);
+ * "host_cohash_threads" (15): host threads hashing beside the GPU in sd_cas_ids calls of
+ * >= 16384 files (0 = the GPU alone).  Unknown keys
  * fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);
 int sd_cas_get_tuning(const char* key, int* value);

@@ -388,21 +388,79 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
         }
         wins[k].busy = false;
     };
+    // Co-hashing ("host_cohash_threads" h > 0, calls of >= 16384 files): the messages are
+    // already in host memory, so feeding the GPU costs the host almost nothing (DMA), and the
+    // call is bound by PCIe; h host threads hash files from the END of the list on the CPU
+    // path meanwhile, claiming chunks of files, while the windows for the GPU are claimed
+    // from the front -- under one lock, so the two meet wherever their rates put them.
+    const int cohash = std::max(0, std::min(64, tuning_get(SD_TUNE_HOST_COHASH_THREADS)));
+    constexpr size_t COHASH_MIN = 16384, COHASH_CHUNK = 256;
+    std::mutex claim_mu;
+    size_t back = live.size();  // live[back, end) is claimed by the host threads
+    std::atomic<uint64_t> host_files{0};
+    std::atomic<bool> host_failed{false};
+    std::vector<std::thread> hosts;
+    struct Join {
+        std::vector<std::thread>& t;
+        std::mutex& mu;
+        size_t& back;
+        ~Join() {  // on an exception below: stop claiming, then wait
+            {
+                std::lock_guard<std::mutex> g(mu);
+                back = 0;
+            }
+            for (auto& x : t)
+                if (x.joinable()) x.join();
+        }
+    } join_hosts{hosts, claim_mu, back};
+    size_t front = 0;  // live[0, front) is claimed by the GPU windows
+    if (cohash > 0 && live.size() >= COHASH_MIN) {
+        for (int t = 0; t < cohash; t++)
+            hosts.emplace_back([&] {
+                for (;;) {
+                    size_t a, b;
+                    {
+                        std::lock_guard<std::mutex> g(claim_mu);
+                        if (back <= front) return;
+                        b = back;
+                        a = b - std::min(COHASH_CHUNK, b - front);
+                        back = a;
+                    }
+                    for (size_t q = a; q < b; q++) {
+                        const sd_extent& e = extents[live[q]];
+                        if (e.msg_offset + e.msg_len > staged_bytes) {
+                            host_failed = true;
+                            continue;
+                        }
+                        uint8_t h[32];
+                        cpu_blake3(staged + e.msg_offset, e.msg_len, h);
+                        to_hex(h, 8, out_hex17 + live[q] * 17);  // cas.rs:61 to_hex()[..16]
+                        if (status) status[live[q]] = SD_FILE_OK;
+                    }
+                    host_files.fetch_add(b - a, std::memory_order_relaxed);
+                }
+            });
+    }
     std::vector<sd_extent> ext;
     size_t gi = 0;
-    for (int w = 0; gi < live.size(); w ^= 1) {
+    for (int w = 0;; w ^= 1) {
         harvest(w);  // frees slot w (its previous window is done)
         uint64_t lo = UINT64_MAX, hi = 0;
         size_t gj = gi;
-        while (gj < live.size()) {
-            const sd_extent& e = extents[live[gj]];
-            const uint64_t nlo = std::min(lo, e.msg_offset);
-            const uint64_t nhi = std::max(hi, align_up(e.msg_offset + e.msg_len, SD_STAGE_PAD));
-            if (gj > gi && nhi - nlo > WINDOW) break;
-            lo = nlo;
-            hi = nhi;
-            gj++;
+        {
+            std::lock_guard<std::mutex> g(claim_mu);
+            while (gj < back) {
+                const sd_extent& e = extents[live[gj]];
+                const uint64_t nlo = std::min(lo, e.msg_offset);
+                const uint64_t nhi = std::max(hi, align_up(e.msg_offset + e.msg_len, SD_STAGE_PAD));
+                if (gj > gi && nhi - nlo > WINDOW) break;
+                lo = nlo;
+                hi = nhi;
+                gj++;
+            }
+            front = gj;
         }
+        if (gj == gi) break;  // the host threads hold the rest
         if (hi > staged_bytes) throw sd_failure(SD_ERR_INVALID, "extent beyond staged_bytes");
         ext.clear();
         for (size_t q = gi; q < gj; q++) {
@@ -423,6 +481,19 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
     }
     harvest(0);
     harvest(1);
+    for (auto& t : hosts) t.join();
+    ctx->cas_ids_gpu_files.fetch_add(gi, std::memory_order_relaxed);
+    ctx->cas_ids_host_files.fetch_add(host_files.load(), std::memory_order_relaxed);
+    if (host_failed) throw sd_failure(SD_ERR_INVALID, "extent beyond staged_bytes");
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_cas_ids_stats(sd_cas_ctx* ctx, uint64_t out[2]) {
+    SD_GUARD_BEGIN
+    if (!ctx || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    out[0] = ctx->cas_ids_gpu_files.load(std::memory_order_relaxed);
+    out[1] = ctx->cas_ids_host_files.load(std::memory_order_relaxed);
     return SD_OK;
     SD_GUARD_END
 }

@@ -33,13 +33,15 @@ thread_local std::string g_err;
 // buffers (profiles/r3/r3n_files_ab_private_fds.json: 1.04 vs 0.84 M files/s), and no split
 // of sd_file_checksums calls between the GPU route and the CPU path (opt-in: from the page
 // cache it measured 78-90 GB/s against 81-87 for the CPU path alone, within the box's
-// noise; profiles/r3/r3z_hybrid_checksum_probe.json)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {0}};
+// noise; profiles/r3/r3z_hybrid_checksum_probe.json); 15 host threads hashing beside the GPU in
+// large sd_cas_ids calls (profiles/r3/r3ad_cohash_probe.json: 300 000 files from pinned memory,
+// GPU alone 1.89-1.94 M files/s, CPU path alone 2.24-2.36 M, both at once 3.87-4.08 M)
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {0}, {15}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
                                                "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",
                                                "files_ring",         "checksum_cpu_max", "files_stage_hot",
-                                               "checksum_hybrid_threads"};
+                                               "checksum_hybrid_threads", "host_cohash_threads"};
 }  // namespace
 
 void sd_set_err(const char* fmt, ...) {

@@ -62,7 +62,8 @@ enum sd_tune_key {
     SD_TUNE_CHECKSUM_CPU_MAX = 10,  // sd_file_checksums: calls of at most this many files take the CPU path
     SD_TUNE_FILES_STAGE_HOT = 11,   // sd_cas_ids_files: read into a per-thread buffer, stream-copy to the window
     SD_TUNE_CHECKSUM_HYBRID_THREADS = 12,  // sd_file_checksums: reader threads of the GPU route in a hybrid call
-    SD_TUNE_NKEYS = 13
+    SD_TUNE_HOST_COHASH_THREADS = 13,      // sd_cas_ids: host threads hashing beside the GPU (large calls)
+    SD_TUNE_NKEYS = 14
 };
 int tuning_get(int key);
 

@@ -145,10 +145,14 @@ def test_cas_pattern_goldens_host_staged(ctx, golden):
         assert raw[17 * i:17 * i + 16].decode() == cp[s], s
 
 
-def test_sd_cas_ids_pipelined_windows(ctx):
+@pytest.mark.parametrize("cohash", [0, 15])
+def test_sd_cas_ids_pipelined_windows(ctx, cohash):
     # the drop-in host entry point over several 512 MiB windows (two alternating streams),
-    # with entries pre-marked failed that must be skipped and left untouched
+    # with entries pre-marked failed that must be skipped and left untouched -- the GPU
+    # alone, and with 15 host threads hashing from the end of the list beside it
+    # ("host_cohash_threads"): both sides must have hashed files, every result equal
     import ctypes
+    import spacedrive_amd as sd
     from spacedrive_amd._native import check, lib
     n = 40000
     sizes, cids, twins = synth.library(0, n, n, small_frac=0.3)
@@ -158,8 +162,20 @@ def test_sd_cas_ids_pipelined_windows(ctx):
     status = np.zeros(n, np.int32)
     status[::1001] = 2  # staging failed upstream
     out = ctypes.create_string_buffer(b"#" * (17 * n), 17 * n)
-    check(lib().sd_cas_ids(ctx.handle, host.data_ptr(), len(staged), ext.ctypes.data, n, out,
-                           status.ctypes.data))
+    keep = sd.get_tuning("host_cohash_threads")
+    before = np.zeros(2, np.uint64)
+    after = np.zeros(2, np.uint64)
+    check(lib().sd_cas_ids_stats(ctx.handle, before.ctypes.data))
+    sd.set_tuning("host_cohash_threads", cohash)
+    try:
+        check(lib().sd_cas_ids(ctx.handle, host.data_ptr(), len(staged), ext.ctypes.data, n, out,
+                               status.ctypes.data))
+    finally:
+        sd.set_tuning("host_cohash_threads", keep)
+    check(lib().sd_cas_ids_stats(ctx.handle, after.ctypes.data))
+    gpu_files, host_files = (int(x) for x in after - before)
+    assert gpu_files + host_files == n - len(range(0, n, 1001))
+    assert (host_files > 0 and gpu_files > 0) if cohash else host_files == 0
     raw = out.raw
     for i in range(n):
         if i % 1001 == 0:
