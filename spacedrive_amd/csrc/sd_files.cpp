@@ -28,6 +28,12 @@ using namespace sdi;
 
 namespace {
 
+// host-side co-hashing (sd_checksums): ranges from this size on are hashed block-parallel
+constexpr uint64_t SD_CPU_SPLIT_MIN = 8ull << 20;
+void check_rc(int rc) {
+    if (rc != SD_OK) throw sd_failure(rc, sd_cas_last_error());
+}
+
 // ------------------------------------------------------- streaming (unknown length)
 // Hashes messages read front to back from a MsgSource through 256 MiB windows on the two
 // alternating slots.  A message's length is only known when its source ends, which is all
@@ -884,7 +890,82 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         uint64_t host_lo, host_end, dev_lo;
     };
     std::vector<RunT> runs;
+    // Co-hashing (as sd_cas_ids, "host_cohash_threads" h > 0, calls of >= 1 GiB): one host
+    // thread claims ranges from the END -- one large range, or consecutive small ones up to
+    // 64 MiB -- and hashes them with h pool threads on the CPU path (a range of 8 MiB or
+    // more block-parallel: its 1 MiB blocks' chaining values on all threads, then the root),
+    // while the loop below claims its windows and streamed ranges from the front.
+    const int cohash = std::max(0, std::min(64, tuning_get(SD_TUNE_HOST_COHASH_THREADS)));
+    uint64_t all_bytes = 0;
+    for (size_t q = 0; q < n; q++) all_bytes += lens[q];
+    std::mutex claim_mu;
+    size_t back = n, front = 0;  // [back, n) claimed by the host, [0, front) by the GPU loop
+    int host_rc = SD_OK;
+    std::string host_err;
+    std::thread host;
+    struct JoinHost {
+        std::thread& t;
+        std::mutex& mu;
+        size_t& back;
+        ~JoinHost() {
+            {
+                std::lock_guard<std::mutex> g(mu);
+                back = 0;
+            }
+            if (t.joinable()) t.join();
+        }
+    } join_host{host, claim_mu, back};
+    if (cohash > 0 && n && all_bytes >= (1ull << 30)) {
+        host = std::thread([&] {
+            try {
+                std::vector<uint8_t> h32, cvs;
+                for (;;) {
+                    size_t b0, b1;
+                    {
+                        std::lock_guard<std::mutex> g(claim_mu);
+                        if (back <= front) return;
+                        b1 = back;
+                        b0 = b1 - 1;
+                        uint64_t sum = lens[b0];
+                        while (b0 > front && lens[b0] < SD_CPU_SPLIT_MIN && lens[b0 - 1] < SD_CPU_SPLIT_MIN &&
+                               sum + lens[b0 - 1] <= (64ull << 20)) {
+                            b0--;
+                            sum += lens[b0];
+                        }
+                        back = b0;
+                    }
+                    h32.resize((b1 - b0) * 32);
+                    if (b1 - b0 == 1 && lens[b0] >= SD_CPU_SPLIT_MIN) {  // one large range, block-parallel
+                        uint64_t o = 0, l = 0, cvb = 0;
+                        check_rc(sd_split_range(lens[b0], 1, 0, &o, &l, &cvb));
+                        cvs.resize(cvb);
+                        check_rc(sd_cpu_split_leaves(data + offsets[b0], lens[b0], 1, 0, cvs.data(), cohash));
+                        check_rc(sd_cpu_split_root(cvs.data(), lens[b0], h32.data()));
+                    } else {
+                        check_rc(sd_cpu_checksums(data, offsets + b0, lens + b0, b1 - b0, h32.data(), cohash));
+                    }
+                    for (size_t q = b0; q < b1; q++) to_hex(h32.data() + 32 * (q - b0), 32, out_hex65 + 65 * q);
+                }
+            } catch (const sd_failure& e) {
+                host_rc = e.rc;
+                host_err = e.what();
+            } catch (...) {
+                host_rc = SD_ERR_NOMEM;
+                host_err = "host allocation failed in a co-hashed sd_checksums call";
+            }
+            std::lock_guard<std::mutex> g(claim_mu);
+            back = front;  // the GPU loop takes nothing further from here on: stop it
+        });
+    }
+    // the GPU loop's claims: range i is the GPU's if no host thread took it
+    auto claim = [&](size_t i) -> bool {
+        std::lock_guard<std::mutex> g(claim_mu);
+        if (i >= back) return false;
+        front = std::max(front, i + 1);
+        return true;
+    };
     for (size_t i = 0; i < n;) {
+        if (!claim(i)) break;
         if (lens[i] + 128 > W) {  // one large range, streamed
             harvest(0);
             harvest(1);
@@ -927,7 +1008,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         ls.clear();
         uint64_t dev_hi = 0;  // the device layout's padded end
         size_t j = i;
-        while (j < n && lens[j] + 128 <= W) {
+        while (j < n && lens[j] + 128 <= W && (j == i || claim(j))) {
             const uint64_t o = offsets[j], L = lens[j];
             const RunT* r = runs.empty() ? nullptr : &runs.back();
             const bool misaligned = r && (r->dev_lo + (o - r->host_lo)) % SD_STAGE_ALIGN != 0;
@@ -938,7 +1019,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
             const uint64_t host_lo = open ? o : r->host_lo;
             const uint64_t d = dev_lo + (o - host_lo);
             const uint64_t nhi = std::max(dev_hi, align_up(d + L, 64));
-            if (j > i && nhi > W) break;
+            if (j > i && nhi > W) break;  // (a range claimed here and not taken: see below)
             if (open) runs.push_back(RunT{o, o + L, dev_lo});
             else runs.back().host_end = std::max(runs.back().host_end, o + L);
             offs.push_back(d);
@@ -964,6 +1045,8 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     }
     harvest(0);
     harvest(1);
+    if (host.joinable()) host.join();
+    if (host_rc != SD_OK) throw sd_failure(host_rc, host_err);
     return SD_OK;
     SD_GUARD_END
 }

@@ -1054,6 +1054,43 @@ def test_checksums_from_host_memory(ctx, oracle_native):
         assert raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), lens[i]
 
 
+@pytest.mark.parametrize("cohash", [0, 15])
+def test_checksums_from_host_memory_cohashed(ctx, oracle_native, cohash):
+    """sd_checksums over > 1 GiB of host ranges (large ranges streamed, runs of small ones
+    packed) with host threads co-hashing from the end ("host_cohash_threads" 15: large
+    ranges block-parallel on the CPU path, small ones in batches) and without: every hash
+    equals the oracle's, whichever side took its range."""
+    import ctypes
+    import spacedrive_amd as sd
+    from spacedrive_amd._native import check, lib
+    MiB = 1 << 20
+    rng = np.random.default_rng(41)
+    lens = [(300 << 20) + 5, 0, 77, (150 << 20) + 1] + [int(x) for x in rng.integers(1, 3 * MiB, 180)] + \
+        [(260 << 20) + 3, 9 * MiB, 1025, (200 << 20) + 64, 5]
+    offs, off = [], 0
+    for L in lens:
+        offs.append(off)
+        off = (off + L + 128 + 127) // 128 * 128
+    assert off > (1 << 30)
+    d = torch.randint(0, 256, (off + 64,), dtype=torch.uint8, device="cuda")
+    host = torch.empty(off + 64, dtype=torch.uint8, pin_memory=True)
+    host.copy_(d)
+    del d
+    arr_o = np.array(offs, np.uint64)
+    arr_l = np.array(lens, np.uint64)
+    out = ctypes.create_string_buffer(65 * len(lens))
+    keep = sd.get_tuning("host_cohash_threads")
+    sd.set_tuning("host_cohash_threads", cohash)
+    try:
+        check(lib().sd_checksums(ctx.handle, host.data_ptr(), arr_o.ctypes.data, arr_l.ctypes.data, len(lens), out))
+    finally:
+        sd.set_tuning("host_cohash_threads", keep)
+    want = oracle_native.checksums_simd(host.numpy(), arr_o, arr_l, nthreads=NT)
+    raw = out.raw
+    for i in range(len(lens)):
+        assert raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), (i, lens[i])
+
+
 def test_checksums_host_ranges_any_layout(ctx, oracle_native):
     """sd_checksums over host ranges laid out every way a caller may: 16-byte starts (leaf-
     sized ranges then start a new copy run on a 128-B device line), gaps,
