@@ -213,7 +213,10 @@ int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
  * start); no page that holds no range byte is read (a range may end where `data` ends, and
  * `data` may have unmapped holes between ranges; bytes between two ranges on a page they
  * share may be copied).  Consecutive ranges are copied 256 MiB window at a time, larger
- * ranges stream; two windows alternate so the H2D copies overlap the kernels. */
+ * ranges stream; two windows alternate so the H2D copies overlap the kernels.  In calls of
+ * >= 1 GiB, "host_cohash_threads" host threads (default 15; 0 = GPU only) hash ranges from
+ * the end on the CPU path meanwhile (ranges of >= 8 MiB block-parallel), the GPU taking
+ * them from the front until the two meet. */
 int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
                  char* out_hex65);
 /* Drop-in: checksums of n files on disk -> 65-byte lowercase hex each (hash.rs:21-23);
@@ -430,7 +433,7 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * route always); "checksum_hybrid_threads" (0): reader threads of the GPU route when
  * sd_file_checksums splits a large call with the CPU path (0 = never split);
  * "host_cohash_threads" (15): host threads hashing beside the GPU in sd_cas_ids calls of
- * >= 16384 files (0 = the GPU alone).  Unknown keys
+ * >= 16384 files and sd_checksums calls of >= 1 GiB (0 = the GPU alone).  Unknown keys
  * fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);
 int sd_cas_get_tuning(const char* key, int* value);
