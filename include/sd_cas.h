@@ -139,7 +139,7 @@ int sd_cas_stage_files(const char* const* paths, sd_extent* extents, size_t n, u
  * 16 lowercase hex chars + NUL (cas.rs:61), 17 bytes per file.  status may be NULL;
  * entries whose status[i] != SD_FILE_OK on input are skipped and left untouched.  Whole-
  * kind messages of any length are accepted (longer than 8 + 102400 B: hashed by the
- * chunk-parallel checksum kernels).  A call of >= 16384 files is PCIe-bound, and feeding
+ * chunk-parallel checksum kernels).  A call of >= 8192 files is PCIe-bound, and feeding
  * the GPU costs the host only DMA, so "host_cohash_threads" (default 15; 0 = GPU only)
  * host threads hash files from the end of the list on the library's CPU path meanwhile,
  * the GPU taking windows from the front until the two meet; sd_cas_ids_stats counts the
@@ -433,7 +433,7 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * route always); "checksum_hybrid_threads" (0): reader threads of the GPU route when
  * sd_file_checksums splits a large call with the CPU path (0 = never split);
  * "host_cohash_threads" (15): host threads hashing beside the GPU in sd_cas_ids calls of
- * >= 16384 files and sd_checksums calls of >= 1 GiB (0 = the GPU alone).  Unknown keys
+ * >= 8192 files and sd_checksums calls of >= 1 GiB (0 = the GPU alone).  Unknown keys
  * fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);
 int sd_cas_get_tuning(const char* key, int* value);

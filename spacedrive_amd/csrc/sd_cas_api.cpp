@@ -388,13 +388,13 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
         }
         wins[k].busy = false;
     };
-    // Co-hashing ("host_cohash_threads" h > 0, calls of >= 16384 files): the messages are
+    // Co-hashing ("host_cohash_threads" h > 0, calls of >= 8192 files): the messages are
     // already in host memory, so feeding the GPU costs the host almost nothing (DMA), and the
     // call is bound by PCIe; h host threads hash files from the END of the list on the CPU
     // path meanwhile, claiming chunks of files, while the windows for the GPU are claimed
     // from the front -- under one lock, so the two meet wherever their rates put them.
     const int cohash = std::max(0, std::min(64, tuning_get(SD_TUNE_HOST_COHASH_THREADS)));
-    constexpr size_t COHASH_MIN = 16384, COHASH_CHUNK = 256;
+    constexpr size_t COHASH_MIN = 8192, COHASH_CHUNK = 256;
     std::mutex claim_mu;
     size_t back = live.size();  // live[back, end) is claimed by the host threads
     std::atomic<uint64_t> host_files{0};
@@ -414,7 +414,11 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
         }
     } join_hosts{hosts, claim_mu, back};
     size_t front = 0;  // live[0, front) is claimed by the GPU windows
+    // while co-hashing, the GPU claims 128 MiB windows (~2 ms of PCIe each), so a mid-size
+    // call is not taken whole by its first window before the host threads have started
+    uint64_t window = WINDOW;
     if (cohash > 0 && live.size() >= COHASH_MIN) {
+        window = 128ull << 20;
         for (int t = 0; t < cohash; t++)
             hosts.emplace_back([&] {
                 for (;;) {
@@ -453,7 +457,7 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
                 const sd_extent& e = extents[live[gj]];
                 const uint64_t nlo = std::min(lo, e.msg_offset);
                 const uint64_t nhi = std::max(hi, align_up(e.msg_offset + e.msg_len, SD_STAGE_PAD));
-                if (gj > gi && nhi - nlo > WINDOW) break;
+                if (gj > gi && nhi - nlo > window) break;
                 lo = nlo;
                 hi = nhi;
                 gj++;
