@@ -369,6 +369,12 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
     live.reserve(n);
     for (size_t i = 0; i < n; i++)
         if (!status || status[i] == SD_FILE_OK) live.push_back(i);
+    // every live extent is checked before anything is hashed, whichever side will hash it
+    for (size_t i : live) {
+        validate_extent(extents[i], i);
+        if (extents[i].msg_offset + extents[i].msg_len > staged_bytes)
+            throw sd_failure(SD_ERR_INVALID, "extent beyond staged_bytes");
+    }
     // windows of files (index order) whose staged span fits WINDOW bytes; two slots
     // alternate so window k+1's H2D copy overlaps window k's kernels
     const uint64_t WINDOW = 512ull << 20;
@@ -398,7 +404,6 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
     std::mutex claim_mu;
     size_t back = live.size();  // live[back, end) is claimed by the host threads
     std::atomic<uint64_t> host_files{0};
-    std::atomic<bool> host_failed{false};
     std::vector<std::thread> hosts;
     struct Join {
         std::vector<std::thread>& t;
@@ -431,11 +436,7 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
                         back = a;
                     }
                     for (size_t q = a; q < b; q++) {
-                        const sd_extent& e = extents[live[q]];
-                        if (e.msg_offset + e.msg_len > staged_bytes) {
-                            host_failed = true;
-                            continue;
-                        }
+                        const sd_extent& e = extents[live[q]];  // validated above
                         uint8_t h[32];
                         cpu_blake3(staged + e.msg_offset, e.msg_len, h);
                         to_hex(h, 8, out_hex17 + live[q] * 17);  // cas.rs:61 to_hex()[..16]
@@ -488,7 +489,6 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
     for (auto& t : hosts) t.join();
     ctx->cas_ids_gpu_files.fetch_add(gi, std::memory_order_relaxed);
     ctx->cas_ids_host_files.fetch_add(host_files.load(), std::memory_order_relaxed);
-    if (host_failed) throw sd_failure(SD_ERR_INVALID, "extent beyond staged_bytes");
     return SD_OK;
     SD_GUARD_END
 }
