@@ -403,6 +403,7 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
     constexpr size_t COHASH_MIN = 8192, COHASH_CHUNK = 256;
     std::mutex claim_mu;
     size_t back = live.size();  // live[back, end) is claimed by the host threads
+    size_t front = 0;           // live[0, front) is claimed by the GPU windows
     std::atomic<uint64_t> host_files{0};
     std::vector<std::thread> hosts;
     struct Join {
@@ -417,8 +418,7 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
             for (auto& x : t)
                 if (x.joinable()) x.join();
         }
-    } join_hosts{hosts, claim_mu, back};
-    size_t front = 0;  // live[0, front) is claimed by the GPU windows
+    } join_hosts{hosts, claim_mu, back};  // declared after everything the threads touch
     // while co-hashing, the GPU claims 128 MiB windows (~2 ms of PCIe each), so a mid-size
     // call is not taken whole by its first window before the host threads have started
     uint64_t window = WINDOW;
