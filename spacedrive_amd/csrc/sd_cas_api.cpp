@@ -399,7 +399,9 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
     // call is bound by PCIe; h host threads hash files from the END of the list on the CPU
     // path meanwhile, claiming chunks of files, while the windows for the GPU are claimed
     // from the front -- under one lock, so the two meet wherever their rates put them.
-    const int cohash = std::max(0, std::min(64, tuning_get(SD_TUNE_HOST_COHASH_THREADS)));
+    // (never more host threads than the machine has cores, less one for this thread)
+    const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS),
+                                             (int)std::thread::hardware_concurrency() - 1}));
     constexpr size_t COHASH_MIN = 8192, COHASH_CHUNK = 256;
     std::mutex claim_mu;
     size_t back = live.size();  // live[back, end) is claimed by the host threads

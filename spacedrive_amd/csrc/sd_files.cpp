@@ -895,7 +895,9 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     // 64 MiB -- and hashes them with h pool threads on the CPU path (a range of 8 MiB or
     // more block-parallel: its 1 MiB blocks' chaining values on all threads, then the root),
     // while the loop below claims its windows and streamed ranges from the front.
-    const int cohash = std::max(0, std::min(64, tuning_get(SD_TUNE_HOST_COHASH_THREADS)));
+    // (never more host threads than the machine has cores, less one for this thread)
+    const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS),
+                                             (int)std::thread::hardware_concurrency() - 1}));
     uint64_t all_bytes = 0;
     for (size_t q = 0; q < n; q++) all_bytes += lens[q];
     std::mutex claim_mu;
