@@ -463,6 +463,17 @@ int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged, std::vector<u
         current_pos += jump;
     }
     if (st != SD_FILE_OK) return st;
+    // :54-58 the footer at SeekFrom::End(-8192).  In the common case the file is exactly
+    // `size` bytes long: one pread of 8192 + 1 bytes at size - 8192 then returns exactly 8192
+    // -- the footer, and proof that the end is at `size` (the extra byte lands in the
+    // message's zero padding and is cleared).  Anything else (a file longer or shorter than
+    // `size`, an interrupted read) seeks to the real end as the reference does.
+    ssize_t r;
+    do {
+        r = pread(f.fd, p, H + 1, (off_t)(size - H));
+    } while (r < 0 && errno == EINTR);
+    if (r == (ssize_t)H) return SD_FILE_OK;
+    p[H] = 0;  // the probe byte, if the file was longer
     const off_t end = lseek(f.fd, -(off_t)H, SEEK_END);  // :54-55 SeekFrom::End(-8192)
     if (end < 0) return io_status(errno);
     return pread_exact(f.fd, p, H, (uint64_t)end);  // :56-58
