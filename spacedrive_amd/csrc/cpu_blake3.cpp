@@ -302,6 +302,24 @@ int32_t cpu_cas_id_file(const char* path, uint64_t size, char out_hex17[17]) {
     } else {  // cas.rs:25-29: le64(size) || fs::read
         Fd f{open(path, O_RDONLY | O_CLOEXEC)};
         if (f.fd < 0) return io_status(errno);
+        {
+            // a seekable file in one call (as stage_one): le64(size), then up to the buffer's
+            // room; a regular file's short count is its end.  A longer file, or a pipe
+            // (ESPIPE, nothing consumed), takes the streaming read below.
+            constexpr uint64_t ROOM = (128 << 10) - 8;
+            uint8_t* msg = scratch(128 << 10);
+            for (int i = 0; i < 8; i++) msg[i] = (uint8_t)(size >> (8 * i));
+            ssize_t r;
+            do {
+                r = pread(f.fd, msg + 8, ROOM, 0);
+            } while (r < 0 && errno == EINTR);
+            if (r >= 0 && (uint64_t)r < ROOM) {
+                cpu_blake3(msg, 8 + (size_t)r, h);
+                hex_lower(h, 8, out_hex17);  // cas.rs:61 to_hex()[..16]
+                return SD_FILE_OK;
+            }
+            if (r < 0 && errno != ESPIPE) return io_status(errno);
+        }
         MsgSource src(f.fd, MsgSource::READ_TO_EOF);
         src.set_prefix_le64(size);
         const int32_t st = hash_source(src, scratch(128 << 10), 128 << 10, h);

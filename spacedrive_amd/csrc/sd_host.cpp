@@ -11,6 +11,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -411,6 +412,26 @@ int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged, std::vector<u
     if (f.fd < 0) return io_status(errno);
     if (e.kind == SD_KIND_WHOLE) {  // cas.rs:29 fs::read: read_to_end
         const uint64_t room = e.msg_len - 8;
+        {
+            // A seekable file in one call: the planned room plus a probe byte.  For a regular
+            // file a count short of what was asked is its end, so this is read_to_end's
+            // outcome without its final zero-length read; a count past the room means the
+            // file holds more than planned.  A pipe or character device fails with ESPIPE
+            // having consumed nothing, and takes the read loop below.
+            uint8_t probe;
+            struct iovec iov[2] = {{dst + 8, (size_t)room}, {&probe, 1}};
+            ssize_t r;
+            do {
+                r = preadv(f.fd, iov, 2, 0);
+            } while (r < 0 && errno == EINTR);
+            if (r >= 0) {
+                if ((uint64_t)r > room) return SD_FILE_CHANGED;  // the caller re-reads it whole
+                e.msg_len = (uint32_t)(8 + r);
+                memset(dst + e.msg_len, 0, padded - e.msg_len);
+                return SD_FILE_OK;
+            }
+            if (errno != ESPIPE) return io_status(errno);
+        }
         uint64_t got = 0;
         for (;;) {
             if (got == room) {  // planned room full: does the file hold more?
