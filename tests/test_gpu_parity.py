@@ -1419,6 +1419,7 @@ def test_split_checksum_mgpu_in_process_ranks(ctx, oracle_native):
             cvs = torch.zeros(sc.cv_bytes, dtype=torch.uint8, device="cuda")
             out = torch.zeros(32, dtype=torch.uint8, device="cuda")
             st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.current_stream())  # the zero fills above, queued on that stream
             sc.mgpu(comms[r], d[sc.offset:], cvs, out, stream=st)
             st.synchronize()
             sc.close()
