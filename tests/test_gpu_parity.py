@@ -989,6 +989,7 @@ def test_dedup_of_one_batch_beside_the_next_batchs_hashing(ctx, rccl_comm):
     valid = [torch.from_numpy((lib[0] != 0).astype(np.uint8)).cuda() for lib in libs]
     hs, ds = torch.cuda.Stream(), torch.cuda.Stream()
     bufs = [torch.zeros(n * 32, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    hs.wait_stream(torch.cuda.current_stream())  # the zero fills, queued on the default stream
     e_hash = [torch.cuda.Event() for _ in range(2)]
     e_ded = [torch.cuda.Event() for _ in range(2)]
     runner = dedup.RcclDedup(ctx, rccl_comm, bufs[0].device, capacity=n + 1024)
