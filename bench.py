@@ -70,6 +70,44 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# True when the process group is up (world > 1, or --force-dist at any world size): every
+# collective below is gated on it, not on the world size, so a one-rank rehearsal runs the
+# same statements an 8-rank node does
+DIST = False
+
+
+def rccl_libs() -> dict:
+    """Which RCCL this process uses (VERDICT r3 "two RCCL libraries"): every librccl file
+    mapped into the process (/proc/self/maps), the one libsdcas's communicators are bound
+    to with the version it reports (sd_comm_rccl_info), and torch's RCCL version."""
+    from spacedrive_amd import _native
+    mapped = set()
+    try:
+        for line in open("/proc/self/maps"):
+            parts = line.split()
+            if len(parts) >= 6 and "librccl" in os.path.basename(parts[-1]):
+                mapped.add(os.path.realpath(parts[-1]))
+    except OSError:
+        pass
+    try:
+        v = torch.cuda.nccl.version()
+        torch_v = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 -- a diagnostic
+        torch_v = None
+    info = _native.rccl_info()
+    return {"mapped": sorted(mapped), "sdcas_comm": info, "torch_nccl_version": torch_v,
+            "one_rccl": len(mapped) == 1 and info["path"] in mapped,
+            "note": "librccl.so.1 is one soname: torch loads its own copy first (ProcessGroupNCCL), and libsdcas's "
+                    "NEEDED librccl.so.1 binds to that same copy -- one RCCL serves both communicators"}
+
+
+def parity(files: int, mismatches: int, what: str, **kw) -> dict:
+    """A leg's oracle check (outside its timed region); a mismatch fails the run."""
+    res = dict(files=int(files), mismatches=int(mismatches), oracle=what, **kw)
+    assert mismatches == 0, res
+    return res
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -83,6 +121,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target seconds per CPU-baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (rehearsal)")
+    p.add_argument("--force-dist", action="store_true",
+                   help="initialise the process group even at world size 1 and take the N > 1 code path "
+                        "(every collective, the per-rank legs, no N = 1 side legs): a one-GPU rehearsal of the "
+                        "8-GPU run, launched with torch.distributed.run --nproc-per-node 1")
     p.add_argument("--dedup", default=None, choices=["rccl", "torch"],
                    help="exchange transport: rccl = sd_cas_dedup_mgpu (C ABI; default with nccl), torch = "
                         "torch.distributed all_to_all (default with gloo)")
@@ -240,8 +282,17 @@ def host_cpu() -> dict:
 
 
 def all_cores() -> int:
-    """nproc: every CPU this process may run on (SURVEY.md 8(d) configs[0](ii))."""
+    """nproc: every CPU in this process's affinity mask."""
     return len(os.sched_getaffinity(0))
+
+
+def effective_cpus() -> int:
+    """The CPUs this process can actually use: its affinity mask, capped by the cgroup's CPU
+    quota (rounded up) where one is set -- SURVEY.md 8(d) configs[0](ii)'s "all cores" on a
+    container whose nproc exceeds its quota (the GPU box: 256 online, a 16-CPU quota)."""
+    q = host_cpu().get("cgroup_cpu_quota")
+    n = all_cores()
+    return max(1, min(n, int(np.ceil(q)))) if q else n
 
 
 def cpu_baseline(sizes, cids, twins, seconds: float):
@@ -254,7 +305,7 @@ def cpu_baseline(sizes, cids, twins, seconds: float):
     per step), and all cores (nproc)."""
     from oracle import native
     from spacedrive_amd.device import stage_plan
-    threads = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share for one GPU
+    threads = max(1, min(16, effective_cpus()))  # the box's CPU share for one GPU
     level = native.simd_level(-1)
 
     def rate(nthreads, n0):
@@ -272,7 +323,7 @@ def cpu_baseline(sizes, cids, twins, seconds: float):
 
     n1, dt1, b1 = rate(1, 2000)
     nT, dtT, bT = rate(threads, 20000)
-    nA = all_cores()
+    nA = effective_cpus()
     nN, dtN, bN = rate(nA, 100000)
     simd = {0: "scalar", 1: "AVX2 8-way", 2: "AVX-512 16-way"}[level]
     return {
@@ -283,40 +334,56 @@ def cpu_baseline(sizes, cids, twins, seconds: float):
         "single_thread": {"value": n1 / dt1, "unit": "files/s", "cores": 1, "sample_files": n1,
                           "GBps": b1 / dt1 / 1e9},
         "all_cores": {"value": nN / dtN, "unit": "files/s", "cores": nA, "sample_files": nN, "GBps": bN / dtN / 1e9,
-                      "cgroup_cpu_quota": host_cpu().get("cgroup_cpu_quota"),
-                      "note": "the same hash-only leg on nproc threads; where the container's cgroup caps CPU time "
-                              "(cgroup_cpu_quota CPUs), nproc threads share that quota and are throttled"},
+                      "nproc": all_cores(), "cgroup_cpu_quota": host_cpu().get("cgroup_cpu_quota"),
+                      "note": "the same hash-only leg on every CPU this process can use: min(nproc, the cgroup's CPU "
+                              "quota) threads (a thread count past the quota only shares the same CPU time)"},
         "simd": simd, "host_cpu": host_cpu(),
     }
 
 
 # ------------------------------------------------------------------ parity of the timed steps
+def oracle_threads() -> int:
+    """host threads for the oracle checks: the CPUs this process may use, at most 16"""
+    return max(1, min(16, effective_cpus()))
+
+
+def sample_idx(n: int, k: int = 4096, head: int = 32) -> np.ndarray:
+    """k indices at an even stride over [0, n) plus the first `head` (the edge sizes)"""
+    return np.unique(np.concatenate([np.arange(min(head, n)), np.linspace(0, n - 1, min(k, n)).astype(np.int64)]))
+
+
+def oracle_hashes(sizes, cids, twins, idx) -> np.ndarray:
+    """[len(idx), 32]: the full BLAKE3 of the cas messages of synthetic files idx, built by
+    the C oracle from the same generator and hashed by its scalar BLAKE3 (oracle/sd_oracle.c)"""
+    from oracle import native
+    from spacedrive_amd.device import stage_plan
+    s, c, t = sizes[idx], cids[idx], twins[idx]
+    ext, total = stage_plan(s)
+    buf = native.stage_synth(s, c, t, ext["msg_offset"], total)
+    return native.checksums(buf, ext["msg_offset"], ext["msg_len"], nthreads=oracle_threads())
+
+
 def parity_sample(sizes, cids, twins, d_hash, start: int, k: int = 4096) -> dict:
     """The timed steps' own output checked against the oracle (outside the timed region):
     a fixed sample of this rank's shard -- k files at an even stride, plus the shard's first
     32 (the edge sizes of SURVEY.md 8(d) on rank 0) -- has its cas messages built by the C
     oracle from the same generator and hashed by the oracle's BLAKE3 (oracle/sd_oracle.c);
     every sampled file's full 32-byte hash in d_hash must be equal."""
-    from oracle import native
-    from spacedrive_amd.device import stage_plan
     n = len(sizes)
-    idx = np.unique(np.concatenate([np.arange(min(32, n)), np.linspace(0, n - 1, min(k, n)).astype(np.int64)]))
-    s, c, t = sizes[idx], cids[idx], twins[idx]
-    ext, total = stage_plan(s)
-    buf = native.stage_synth(s, c, t, ext["msg_offset"], total)
-    want = native.checksums(buf, ext["msg_offset"], ext["msg_len"], nthreads=16)
+    idx = sample_idx(n, k)
+    want = oracle_hashes(sizes, cids, twins, idx)
     got = d_hash.view(-1, 32)[torch.from_numpy(idx).to(d_hash.device)].cpu().numpy()
     bad = np.nonzero((got != want).any(axis=1))[0]
     return {"files": int(len(idx)), "mismatches": int(len(bad)),
             "first_bad_global_index": int(start + idx[bad[0]]) if len(bad) else None,
-            "sampled_kind": int((s > 102400).sum()),
+            "sampled_kind": int((sizes[idx] > 102400).sum()),
             "note": "full 32-byte hashes of the timed steps' output vs the C oracle (oracle/sd_oracle.c) on the "
                     "same generator: the shard's first 32 files + an even-stride sample"}
 
 
 def _gather_rows(t: torch.Tensor, world: int, dev) -> list:
     """all_gather of a [m, w] int64 tensor whose m differs per rank (padded to the max)."""
-    if world == 1:
+    if not DIST:
         return [t]
     m = torch.tensor([t.shape[0]], dtype=torch.int64, device=dev)
     ms = [torch.zeros_like(m) for _ in range(world)]
@@ -329,7 +396,7 @@ def _gather_rows(t: torch.Tensor, world: int, dev) -> list:
     return [o[:int(k.item())] for o, k in zip(outs, ms)]
 
 
-def dedup_parity(d_hash, d_valid, n: int, start: int, recs, rep, owners, world: int, dev) -> dict:
+def dedup_parity(d_hash, d_valid, n: int, start: int, recs, rep, owners, world: int, dev, transport: str) -> dict:
     """The multi-rank exchange checked end to end on a slice of the key space: every record
     whose cas_id key has bits 40..47 == 0 (1/256 of the keys, spread over every rank's
     prefix range, so every destination and every source takes part; a group is wholly in or
@@ -371,12 +438,16 @@ def dedup_parity(d_hash, d_valid, n: int, start: int, recs, rep, owners, world: 
         res = {"records": int(len(r)), "groups": int(ng), "linked": int((own_h != r[:, 1]).sum()),
                "out_records_per_rank": per_rank_out, "parity": bool(same)}
         ok[0] = 1 if same else 0
-    if world > 1:
+    if DIST:
         dist.broadcast(ok, 0)
     res["parity"] = bool(int(ok.item()))
     res["slice"] = "cas_id keys with bits 40..47 == 0 (1/256 of the key space, every prefix range)"
+    out_side = {"rccl": "sd_cas_dedup_mgpu over libsdcas's RCCL communicator",
+                "torch": "dedup.dedup_shard over torch.distributed (" + (dist.get_backend() if DIST else "no") +
+                         " process group)"}[transport]
+    res["transport"] = transport
     res["note"] = ("input records (each rank's own hashes) grouped on rank 0 by group_host + identifier.object_owners "
-                   "vs the exchanged, grouped output of sd_cas_dedup_mgpu from every rank")
+                   f"vs the exchanged, grouped output of {out_side} from every rank")
     return res
 
 
@@ -392,7 +463,7 @@ def ev_ms(fn, stream, reps=1):
     return e0.elapsed_time(e1) / reps
 
 
-def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1):
+def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1, lib_=None):
     """with-H2D cas_ids: the first k files' staged messages in pinned host memory through
     the drop-in sd_cas_ids (host plan + H2D + kernels + D2H + hex, windows pipelined on two
     streams), beside the raw H2D copy of the same bytes and the device-resident kernels.
@@ -426,7 +497,7 @@ def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1):
         try:
             call()  # warm: the context's windows and tables
             reps = 2
-            if world > 1:
+            if DIST:
                 dist.barrier()
             s0 = np.zeros(2, np.uint64)
             s1 = np.zeros(2, np.uint64)
@@ -437,7 +508,7 @@ def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1):
             e2e[mode] = ((time.perf_counter() - t0) / reps, h)
             check(lib().sd_cas_ids_stats(ctx.handle, s1.ctypes.data))
             e2e[mode] += (float((s1 - s0)[1]) / (reps * k),)
-            if world > 1:
+            if DIST:
                 dist.barrier()
         finally:
             sd.set_tuning("host_cohash_threads", keep)
@@ -449,6 +520,12 @@ def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1):
     got = np.frombuffer(bytes.fromhex("".join(raw[17 * i:17 * i + 16].decode() for i in range(k))),
                         np.uint8).reshape(k, 8)
     assert np.array_equal(got, want), "sd_cas_ids differs from the device-resident batch"
+    par = None
+    if lib_ is not None:  # the call's own cas_ids against the oracle, on an even-stride sample
+        idx = sample_idx(k)
+        w8 = oracle_hashes(*lib_, idx)[:, :8]
+        par = parity(len(idx), int((got[idx] != w8).any(axis=1).sum()),
+                     "cas_ids of an even-stride sample (+ the first 32) vs the C oracle on the same generator")
     res = {"files": k, "bytes": nbytes, "h2d_ms": h2d_ms, "h2d_GBps": nbytes / (h2d_ms * 1e-3) / 1e9,
            "kernel_ms": kernel_ms, "kernel_files_per_s": k / (kernel_ms * 1e-3),
            "end_to_end_ms": e2e_s * 1e3, "end_to_end_files_per_s": k / e2e_s,
@@ -457,12 +534,13 @@ def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1):
            "gpu_only": {"end_to_end_ms": e2e["gpu_only"][0] * 1e3,
                         "end_to_end_files_per_s": k / e2e["gpu_only"][0],
                         "end_to_end_GBps": nbytes / e2e["gpu_only"][0] / 1e9},
+           "parity": par,
            "note": "sd_cas_ids from pinned host memory (mean of 2 calls after a warm one, all ranks at once): "
                    "plan + H2D + kernels + D2H + hex, 512 MiB windows on two streams, with the library default "
                    "of host_cohash_threads host threads hashing files from the end of the list meanwhile "
                    "(host_share = their fraction of the files); gpu_only = the same call with 0; h2d_ms = one "
                    "raw copy of the same bytes (HIP events); kernel_ms = the same files device-resident"}
-    if world > 1:
+    if DIST:
         rows = [None] * world
         dist.all_gather_object(rows, [e2e_s, k, nbytes])
         per = [{"rank": r, "end_to_end_files_per_s": row[1] / row[0], "end_to_end_GBps": row[2] / row[0] / 1e9}
@@ -519,7 +597,11 @@ def checksum_host(ctx, gib: int, dev, stream):
         assert got == want, f"sd_checksums ({mode}) differs from the device-resident batch"
         e2e[mode] = min(runs)
     e2e_s = e2e["default"]
-    return {"files": nf, "bytes": total, "h2d_ms": h2d_ms, "h2d_GBps": total / (h2d_ms * 1e-3) / 1e9,
+    from oracle import native
+    bad = sum(native.checksum_synth_mt(flen, 20_000 + i, 0, nthreads=oracle_threads()).hex() != got[i]
+              for i in range(nf))
+    par = parity(nf, bad, "every file's 64-hex checksum vs the C oracle's chunk-parallel BLAKE3 of the same content")
+    return {"files": nf, "bytes": total, "h2d_ms": h2d_ms, "h2d_GBps": total / (h2d_ms * 1e-3) / 1e9, "parity": par,
             "kernel_ms": kernel_ms, "kernel_GBps": total / (kernel_ms * 1e-3) / 1e9,
             "end_to_end_ms": e2e_s * 1e3, "end_to_end_GBps": total / e2e_s / 1e9, "host_cohash_threads": keep,
             "gpu_only": {"end_to_end_ms": e2e["gpu_only"] * 1e3, "end_to_end_GBps": total / e2e["gpu_only"] / 1e9},
@@ -544,8 +626,8 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
     """configs[1] (1 M files <= 100 KiB, whole-content cas_id) or configs[2] (1 M files
     > 100 KiB, sampled cas_id) on this GPU: kernel-only files/s over device-resident
     staged messages, timed with HIP events on the launch stream, plus determinism of the
-    full 32-byte hashes across runs (a size-independent property; bit-exactness vs the
-    oracle is pinned by tests/test_gpu_parity.py on the same generator)."""
+    full 32-byte hashes across runs and, outside the timing, a 4 096-file even-stride
+    sample of the timed output against the oracle (`parity`)."""
     import spacedrive_amd as sd
     from spacedrive_amd import synth
     gen = synth.small_library if which == "small" else synth.sampled_library
@@ -571,6 +653,7 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
     else:
         kernels, grid = ["k_whole_items", "k_whole_merge8"], whole_grid(b)
         tr = pmc_traffic(kernels[0], grid)
+    ps = parity_sample(sizes, cids, twins, h1, 0)
     res = {"workload": ("configs[1]: 1M files <= 100 KiB, whole-content cas_id (log-uniform sizes 1..102400)"
                         if which == "small" else
                         "configs[2]: 1M files > 100 KiB, sampled cas_id (log-uniform sizes 102401..4 GiB)"),
@@ -584,7 +667,9 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
                                   / (G_MIX_LANE_OPS_PER_CLK * N_CUS * clock_res["sclk_mhz_median"] * 1e6)
                                   if clock_res else None),
            "kernels": kernels, "launch_grid": grid,
-           "traffic": tr["bytes"] if tr else None, "deterministic": deterministic}
+           "traffic": tr["bytes"] if tr else None, "deterministic": deterministic,
+           "parity": parity(ps["files"], ps["mismatches"], "full 32-byte hashes of an even-stride sample (+ the first "
+                            "32) vs the C oracle (oracle/sd_oracle.c) on the same generator")}
     del d_staged, h0, h1, b
     torch.cuda.empty_cache()
     assert deterministic, which
@@ -757,8 +842,9 @@ def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool, latency_calls
         del host
         L = lib()
         arr = (ctypes.c_char_p * k)(*[os.fsencode(p) for p in paths])
-        threads = 16
-        nA = all_cores()
+        from spacedrive_amd._native import host_cpu_budget
+        threads = min(16, host_cpu_budget()["budget"])  # the library caps every call at its host budget
+        nA = effective_cpus()
         out = ctypes.create_string_buffer(17 * k)
         st = np.zeros(k, np.int32)
         sz = np.ascontiguousarray(sub_sizes, np.uint64)
@@ -796,6 +882,14 @@ def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool, latency_calls
                         "host_cpu_us_per_file": min(lib_cpu[1:]) / k * 1e6,
                         "note": "sd_cpu_cas_ids_files, best of 2 warm runs"}
         res["gpu_over_cpu_path_16_threads"] = res["gpu"]["files_per_s"] / res["library_cpu_path"]["files_per_s"]
+        # the GPU route's cas_ids against the oracle reading the same files with the reference's
+        # read schedule, on an even-stride sample (the whole set too when with_cpu, below)
+        from oracle import native
+        idx = sample_idx(k)
+        o8, ost = native.cas_ids_files([paths[i] for i in idx], sub_sizes[idx], nthreads=oracle_threads())
+        bad = int(sum((ost[j] != 0) or (o8[j].tobytes().hex() != gpu_ids[i]) for j, i in enumerate(idx)))
+        res["parity"] = parity(len(idx), bad, "cas_ids of an even-stride sample of the files vs the C oracle's "
+                                              "reference read schedule (cas.rs:27-58) + BLAKE3")
         if with_cpu:
             from oracle import native
             ol = native.lib()
@@ -862,9 +956,14 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
             gpu = gpu or got
             assert got == gpu
             res[key] = {"GBps": total / min(runs[1:]) / 1e9, "seconds": min(runs[1:]), "first_run_s": runs[0]}
+        from oracle import native
+        bad = sum(native.checksum_synth_mt(flen, 30_000 + i, 0, nthreads=oracle_threads()).hex() != gpu[i]
+                  for i in range(nf))
+        res["parity"] = parity(nf, bad, "every file's checksum vs the C oracle's chunk-parallel BLAKE3 of the same "
+                                        "content")
         res["gpu"]["note"] = ("sd_file_checksums, GPU route: hash.rs's 1 MiB reads as parallel preads into 256 MiB "
                               "pinned windows, two slots alternating (reads overlap H2D + kernels); best of 2 warm runs")
-        for nt, key in ((16, "library_cpu_path"), (all_cores(), "library_cpu_path_all_cores")):
+        for nt, key in ((16, "library_cpu_path"), (effective_cpus(), "library_cpu_path_all_cores")):
             cpu_runs = []
             for _ in range(2):
                 t0 = time.perf_counter()
@@ -875,7 +974,7 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
         if with_cpu:
             from oracle import native
             cpu = {}
-            for nt in (1, 16, all_cores()):
+            for nt in (1, 16, effective_cpus()):
                 sub = paths[:4] if nt == 1 else paths  # one thread: a bounded sample (1 GiB)
                 t0 = time.perf_counter()
                 got, st = native.file_checksums(sub, nthreads=nt, simd=-1)
@@ -926,14 +1025,14 @@ def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int
         for _ in range(3):
             run()
     torch.cuda.synchronize()
-    if world > 1:
+    if DIST:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
         run()
     torch.cuda.synchronize()
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev if comm is not None else "cpu")
-    if world > 1:
+    if DIST:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     wall_ms = float(dt.item()) / reps * 1e3
     leaves_ms = ev_ms(lambda: sc.leaves(d_slice, cvs, stream), stream, reps=reps)
@@ -941,23 +1040,23 @@ def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int
            "ms_per_file": wall_ms, "GBps": total / (wall_ms * 1e-3) / 1e9, "scaling": "strong",
            "rank0_leaves_ms": leaves_ms, "rank0_bytes": sc.len,
            "rank0_leaves_GBps": sc.len / (leaves_ms * 1e-3) / 1e9 if sc.len else None,
-           "transport": "rccl" if comm is not None else ("none (N=1)" if world == 1 else "gloo via host (rehearsal)"),
+           "transport": "rccl" if comm is not None else ("none (N=1)" if world == 1 else
+                                                         f"{dist.get_backend()} via host (rehearsal)"),
            "note": "one file over all ranks: per-rank block CVs, the CV slots gathered in rank order (in-place "
                    "ncclAllGather inside sd_split_checksum_mgpu over RCCL), reduce on every rank; wall time with "
                    "barriers, max over ranks"}
     h = out32.clone() if comm is not None else out32.cpu()
-    if world > 1:  # every rank must hold the same hash
+    if DIST:  # every rank must hold the same hash
         allh = [torch.zeros_like(h) for _ in range(world)]
         dist.all_gather(allh, h)
         res["ranks_agree"] = all(torch.equal(x, h) for x in allh)
-    else:  # the whole file is here: the same bytes through the regular checksum batch
-        cb = ctx.checksum_batch([0], [total])
-        ref = torch.zeros(32, dtype=torch.uint8, device=dev)
-        cb.run(d_slice, ref, stream)
-        torch.cuda.synchronize()
-        res["equal_to_checksum_batch"] = bool(torch.equal(ref.cpu(), h.cpu()))
-        cb.close()
+        assert res["ranks_agree"], "the ranks' split checksums differ"
     res["hash"] = bytes(h.cpu().numpy()).hex()
+    if rank == 0:  # the file's hash against the oracle's BLAKE3 of the same content
+        from oracle import native
+        want = native.checksum_synth_mt(total, 20_000, 0, nthreads=oracle_threads()).hex()
+        res["parity"] = parity(1, int(want != res["hash"]), "the file's checksum vs the C oracle's chunk-parallel "
+                                                             "BLAKE3 of the same content (rank 0)")
     sc.close()
     del d_slice, cvs
     torch.cuda.empty_cache()
@@ -981,14 +1080,18 @@ def main():
     if args.share_gpu:  # rehearsal of the N-rank path on a box with fewer GPUs
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
-    if world > 1:
+    global DIST
+    if world > 1 or args.force_dist:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(args.dist_backend)
+        DIST = True
+    # collectives' tensors live where the backend wants them
+    cdev = torch.device("cuda", local) if DIST and args.dist_backend == "nccl" else torch.device("cpu")
     transport = args.dedup or ("rccl" if args.dist_backend == "nccl" else "torch")
     import spacedrive_amd as sd
-    from spacedrive_amd import dedup, synth
+    from spacedrive_amd import _native, dedup, synth
 
     ctx = sd.Context(local)
     n = args.files_per_gpu
@@ -1013,16 +1116,15 @@ def main():
             rccl = dedup.RcclDedup(ctx, comm, dev, capacity=n * 5 // 4 + 4096)
         except Exception as e:  # noqa: BLE001 -- recorded in the output line, never silent
             err = f"sd_comm_create failed on rank {rank}: {e}"
-        ok = torch.tensor([0 if err else 1], device=dev)
-        if world > 1:
+        ok = torch.tensor([0 if err else 1], device=cdev)
+        if DIST:
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same transport
         if not int(ok.item()):
             log(f"[rank {rank}] {err or 'a peer rank failed sd_comm_create'}; exchanging through torch.distributed")
             transport, transport_note = "torch", err or "a peer rank failed sd_comm_create"
             comm = rccl = None
     if rccl is None:
-        gloo = world > 1 and dist.get_backend() == "gloo"
-        ascending = dedup.shards_ascend(n, start, None, "cpu" if gloo else dev)
+        ascending = dedup.shards_ascend(n, start, None, cdev)
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: {n} files ({batch.n_sampled} sampled), "
         f"{batch.msg_bytes / 1e9:.2f} GB of messages, {batch.compressions / 1e9:.3f} G compressions, "
@@ -1051,18 +1153,18 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if DIST:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         res = step(k)
     torch.cuda.synchronize()
-    if world > 1:
+    if DIST:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+    if DIST:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -1072,9 +1174,8 @@ def main():
     hash_ms, sampled_ms, dedup_ms = avg(0, 2), avg(0, 1), avg(2, 3)
     recs, rep, n_groups, owners = res
     # every valid file lands on exactly one rank; groups never straddle ranks
-    tot = torch.tensor([recs.shape[0], n_groups, int((sizes != 0).sum())], dtype=torch.int64,
-                       device=dev if args.dist_backend == "nccl" else "cpu")
-    if world > 1:
+    tot = torch.tensor([recs.shape[0], n_groups, int((sizes != 0).sum())], dtype=torch.int64, device=cdev)
+    if DIST:
         dist.all_reduce(tot)
     dedup_totals = {"records": int(tot[0]), "groups": int(tot[1]), "valid_files": int(tot[2]),
                     "records_on_rank0": int(recs.shape[0]),
@@ -1130,19 +1231,19 @@ def main():
 
         pipelined_steps(args.warmup)
         torch.cuda.synchronize()
-        if world > 1:
+        if DIST:
             dist.barrier()
         torch.cuda.synchronize()
         clock = ClockSampler(dev.index if dev.index is not None else 0).start()
         t0 = time.perf_counter()
         pres = pipelined_steps(args.steps, timed=True)
         torch.cuda.synchronize()
-        if world > 1:
+        if DIST:
             dist.barrier()
         p_elapsed = time.perf_counter() - t0
         clock_res = clock.result()
-        if world > 1:
-            t = torch.tensor([p_elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+        if DIST:
+            t = torch.tensor([p_elapsed], dtype=torch.float64, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             p_elapsed = float(t.item())
         # the last batch's exchange gives the serial pass's result exactly
@@ -1206,6 +1307,15 @@ def main():
                                "frac_full_rate": phase_roof["frac_full_rate"],
                                "whole_items_grid": w_grid, "whole_items_traffic": tr_w["bytes"] if tr_w else None}},
         "steps_serial": serial, "steps_pipelined": pipelined,
+        "distributed": {"dist_initialized": DIST, "backend": dist.get_backend() if DIST else None, "world": world,
+                        "force_dist": bool(args.force_dist), "dedup_transport": transport,
+                        "rccl_libs": rccl_libs() if transport == "rccl" or args.dist_backend == "nccl" else None},
+        "host_threads": dict(_native.host_cpu_budget(), cohash_threads=min(sd.get_tuning("host_cohash_threads"),
+                                                                         _native.host_cpu_budget()["budget"] - 1),
+                             read_threads=min(sd.get_tuning("read_threads"), _native.host_cpu_budget()["budget"]),
+                             note="the library's host thread budget (sd_host_cpu_budget): min(affinity, cgroup quota) "
+                                  "/ LOCAL_WORLD_SIZE; every call's readers, CPU-path workers and co-hashing threads "
+                                  "are capped by it"),
         "kernels": {"hash_ms": s_hash_ms, "sampled_ms": s_sampled_ms, "whole_ms": s_hash_ms - s_sampled_ms,
                     "dedup_and_exchange_ms": dedup_ms,
                     "host_overhead_ms": serial["ms_per_step"] - s_hash_ms - dedup_ms,
@@ -1216,28 +1326,26 @@ def main():
     # ---- the timed steps' output, checked (outside the timed regions) --------------------
     # (1) hashes: a fixed sample of every rank's shard against the C oracle
     ps = parity_sample(sizes, cids, twins, d_hash, start)
-    bad = torch.tensor([ps["mismatches"], ps["files"]], dtype=torch.int64,
-                       device=dev if args.dist_backend == "nccl" else "cpu")
-    if world > 1:
+    bad = torch.tensor([ps["mismatches"], ps["files"]], dtype=torch.int64, device=cdev)
+    if DIST:
         dist.all_reduce(bad)
     out["parity_sample"] = dict(ps, files=int(bad[1]), mismatches=int(bad[0]), ranks=world,
                                 rank0_first_bad_global_index=ps["first_bad_global_index"])
     out["parity_sample"].pop("first_bad_global_index")
     # (2) the exchange, grouping and Object owners: a key slice from every rank, on rank 0
-    out["dedup"]["parity_slice"] = dedup_parity(d_hash, d_valid, n, start, recs, rep, owners, world, dev)
+    out["dedup"]["parity_slice"] = dedup_parity(d_hash, d_valid, n, start, recs, rep, owners, world, dev, transport)
     out["dedup"]["parity"] = out["dedup"]["parity_slice"]["parity"]
     # (3) where one exchange's time goes (one more serial call, events at its phases)
     if rccl is not None:
         comm.set_timing(True)
         torch.cuda.synchronize()
-        if world > 1:
+        if DIST:
             dist.barrier()
         rccl(d_hash.view(n, 32), d_valid, n, start, stream=stream)
         ph = comm.last_phases()
         comm.set_timing(False)
-        pt = torch.tensor([ph[k] for k in comm.PHASES], dtype=torch.float64,
-                          device=dev if args.dist_backend == "nccl" else "cpu")
-        if world > 1:
+        pt = torch.tensor([ph[k] for k in comm.PHASES], dtype=torch.float64, device=cdev)
+        if DIST:
             dist.all_reduce(pt, op=dist.ReduceOp.MAX)
         out["dedup"]["phases_ms"] = dict(ph, note="rank 0's call: partition, all-gather of the count rows + their "
                                                   "copy to the host, the stream's idle gap while the host reads them "
@@ -1247,11 +1355,11 @@ def main():
     assert out["parity_sample"]["mismatches"] == 0, out["parity_sample"]
     assert out["dedup"]["parity"], out["dedup"]["parity_slice"]
 
-    solo = rank == 0 and world == 1 and not args.no_extras
+    solo = rank == 0 and not DIST and not args.no_extras
     with_h2d = {}
     if args.host_staged_files > 0 and not args.no_extras:  # every rank: one PCIe link per GPU
-        k_h2d = args.host_staged_files if world == 1 else min(args.host_staged_files, 150_000)
-        with_h2d["cas"] = host_staged(ctx, ext, d_staged, k_h2d, dev, stream, world)
+        k_h2d = args.host_staged_files if not DIST else min(args.host_staged_files, 150_000)
+        with_h2d["cas"] = host_staged(ctx, ext, d_staged, k_h2d, dev, stream, world, lib_=(sizes, cids, twins))
     if solo and args.file_backed_files > 0:
         out["file_backed"] = file_backed(ctx, sizes, ext, d_staged, args.file_backed_files,
                                          with_cpu=not args.no_cpu_baseline, latency_calls=args.latency_calls,
@@ -1277,8 +1385,8 @@ def main():
         ck_ms = ev_ms(lambda: cb.run(d_data, d_sum, stream), stream, reps=args.checksum_steps)
         ck_clock = ck_clock.result()
         gbps = cb.total_bytes / (ck_ms * 1e-3) / 1e9
-        tot = torch.tensor([gbps], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-        if world > 1:
+        tot = torch.tensor([gbps], dtype=torch.float64, device=cdev)
+        if DIST:
             dist.all_reduce(tot)
         roof = valu_roof(cb.compressions, ck_ms)
         tr_ck = pmc_traffic("k_ck_leaf", cb.blocks * 256)
@@ -1295,6 +1403,14 @@ def main():
                                         "hbm": {"achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                                 "frac": gbps / HBM_PEAK_GBPS}},
                            "launch_grid": cb.blocks * 256, "traffic": tr_ck["bytes"] if tr_ck else None}
+        # the timed output against the oracle: two of the 16 files (the first and the last)
+        from oracle import native
+        sums = d_sum.cpu().numpy().reshape(nf, 32)
+        chk = [0, nf - 1]
+        bad = sum(native.checksum_synth_mt(flen, 10_000 + start + i, 0, nthreads=oracle_threads()) != sums[i].tobytes()
+                  for i in chk)
+        out["checksum"]["parity"] = parity(len(chk), bad, "files 0 and 15 of the timed batch vs the C oracle's "
+                                                          "chunk-parallel BLAKE3 of the same content", checked=chk)
         # configs[3]'s mixed variant: files of 2..8 GiB (unaligned lengths) in the same buffer
         rng = np.random.default_rng(7 + start)
         m_offs, m_lens, pos = [], [], 0
@@ -1311,12 +1427,20 @@ def main():
             cbm.run(d_data, d_msum, stream)
             mx_ms = ev_ms(lambda: cbm.run(d_data, d_msum, stream), stream, reps=args.checksum_steps)
             mroof = valu_roof(cbm.compressions, mx_ms)
+            # one mixed file (the first: it spans two generated files) against the oracle
+            # hashing the same bytes, copied to the host
+            host = d_data[m_offs[0]:m_offs[0] + m_lens[0]].cpu().numpy()
+            mbad = int(native.checksum_mt(host, m_lens[0], nthreads=oracle_threads()) !=
+                       d_msum[:32].cpu().numpy().tobytes())
+            del host
             out["checksum"]["mixed"] = {
                 "workload": f"configs[3] mixed: {len(m_lens)} files of 2..8 GiB, unaligned lengths, "
                             f"packed at 128-B (SD_STAGE_ALIGN) starts",
                 "files": len(m_lens), "bytes": cbm.total_bytes, "ms_per_run": mx_ms,
                 "GBps": cbm.total_bytes / (mx_ms * 1e-3) / 1e9, "frac": mroof["frac"],
-                "frac_full_rate": mroof["frac_full_rate"]}
+                "frac_full_rate": mroof["frac_full_rate"],
+                "parity": parity(1, mbad, f"mixed file 0 ({m_lens[0]} B) vs the C oracle's chunk-parallel BLAKE3 of "
+                                          "the same bytes")}
             del cbm, d_msum
         del d_data, cb
         torch.cuda.empty_cache()
@@ -1333,12 +1457,12 @@ def main():
     if with_h2d:
         out["with_h2d"] = with_h2d
 
-    if world == 1 and args.config_files > 0:
+    if not DIST and args.config_files > 0:
         out["configs"] = {k: config_leg(ctx, k, args.config_files, args.config_reps, dev, stream, valu_peak,
                                         args.warm_ms)
                           for k in ("small", "sampled")}
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not DIST and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sizes, cids, twins, args.cpu_seconds)
         if "cpu_reference_schedule" in out.get("file_backed", {}):
             out["cpu_baseline"]["file_backed"] = dict(out["file_backed"]["cpu_reference_schedule"],
@@ -1346,7 +1470,7 @@ def main():
                                                       note="reference read schedule from files (page cache)")
     if comm is not None:
         comm.close()
-    if world > 1:
+    if DIST:
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:

@@ -102,6 +102,13 @@ typedef struct sd_checksum_batch sd_checksum_batch;
 
 /* ---------------------------------------------------------------- context */
 int sd_cas_abi_version(void);
+/* The host thread budget: the most host threads one call of this
+ * process starts -- readers, CPU-path workers and co-hashing threads alike.  Resolved once
+ * as min(CPUs in the affinity mask, the cgroup's CPU quota rounded up) / LOCAL_WORLD_SIZE
+ * (the ranks sharing the node's host; 1 when unset), at least 1; the tuning key
+ * "host_cpu_budget" > 0 replaces it.  out[5]: [0] the budget, [1] affinity CPUs, [2] cgroup
+ * quota in milli-CPUs (0 = none), [3] LOCAL_WORLD_SIZE, [4] 1 if the tuning key set it. */
+int sd_host_cpu_budget(int out[5]);
 /* last error message of the calling thread ("" if none) */
 const char* sd_cas_last_error(void);
 int sd_cas_ctx_create(int device, sd_cas_ctx** out);
@@ -352,6 +359,11 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
  *       them, has queued the exchange (the call's one mid-call sync),
  *   [3] grouped ncclSend / ncclRecv of the records, [4] group + Object owners. */
 #define SD_DEDUP_PHASES 5
+/* The RCCL that serves sd_comm in this process: *version = ncclGetVersion's code (e.g.
+ * 22606 = 2.26.6) and path_out = the shared object its symbols were bound to (librccl.so.1
+ * is one soname: a host that loaded another RCCL first -- torch's ProcessGroupNCCL -- has
+ * libsdcas's communicators served by that one).  path_out may be NULL. */
+int sd_comm_rccl_info(int* version, char* path_out, size_t path_cap);
 int sd_comm_set_timing(sd_comm* comm, int on);
 int sd_comm_last_phases(sd_comm* comm, float* ms_out /* SD_DEDUP_PHASES */);
 
@@ -433,8 +445,10 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * route always); "checksum_hybrid_threads" (0): reader threads of the GPU route when
  * sd_file_checksums splits a large call with the CPU path (0 = never split);
  * "host_cohash_threads" (15): host threads hashing beside the GPU in sd_cas_ids calls of
- * >= 8192 files and sd_checksums calls of >= 1 GiB (0 = the GPU alone).  Unknown keys
- * fail with SD_ERR_INVALID. */
+ * >= 8192 files and sd_checksums calls of >= 1 GiB (0 = the GPU alone; never more than the
+ * host budget less one); "host_cpu_budget" (0 = resolved, see sd_host_cpu_budget): the cap
+ * on every call's host threads -- thread counts callers pass (nthreads) and the knobs above
+ * are clamped to it.  Unknown keys fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);
 int sd_cas_get_tuning(const char* key, int* value);
 /* Read-only probe over d_buf[0, bytes) (bytes a multiple of 4096) for calibrating the

@@ -113,10 +113,13 @@ pub(super) async fn get_orphan_file_paths_ahead(
 }
 
 /// The look-ahead cache of one identifier job: each orphan's FileMetadata::new outcome, by
-/// file_path id, consumed once by the step that processes the row.
+/// file_path id, consumed once by the step that processes the row.  A row whose
+/// IsolatedFilePathData conversion failed is cached too, as `None` (a tombstone): its step
+/// drops it like any other failed row, and `covers` stays true, so such a row does not make
+/// every step that holds it re-query and re-fill the look-ahead.
 #[derive(Default)]
 pub struct LookAhead {
-    cache: HashMap<file_path::id::Type, Result<FileMetadata, FileIOError>>,
+    cache: HashMap<file_path::id::Type, Option<Result<FileMetadata, FileIOError>>>,
 }
 
 impl LookAhead {
@@ -133,21 +136,22 @@ impl LookAhead {
         location_path: &Path,
         ahead: &[file_path_for_file_identifier::Data],
     ) {
-        // mod.rs:110-115, for the uncached rows
-        let entries: Vec<(IsolatedFilePathData<'_>, file_path::id::Type)> = ahead
-            .iter()
-            .filter(|fp| !self.cache.contains_key(&fp.id))
-            .filter_map(|file_path| {
-                IsolatedFilePathData::try_from((location.id, file_path))
-                    .map(|iso_file_path| (iso_file_path, file_path.id))
-                    .map_err(|e| error!("Failed to extract isolated file path data: {e:#?}"))
-                    .ok()
-            })
-            .collect();
+        // mod.rs:110-115, for the uncached rows; a failed conversion is logged once and
+        // cached as a tombstone
+        let mut entries: Vec<(IsolatedFilePathData<'_>, file_path::id::Type)> = Vec::new();
+        for file_path in ahead.iter().filter(|fp| !self.cache.contains_key(&fp.id)) {
+            match IsolatedFilePathData::try_from((location.id, file_path)) {
+                Ok(iso_file_path) => entries.push((iso_file_path, file_path.id)),
+                Err(e) => {
+                    error!("Failed to extract isolated file path data: {e:#?}");
+                    self.cache.insert(file_path.id, None);
+                }
+            }
+        }
         let isos: Vec<&IsolatedFilePathData<'_>> = entries.iter().map(|(iso, _)| iso).collect();
         let metadatas = FileMetadata::new_batch(location_path, &isos).await;
         for ((_, id), metadata) in entries.into_iter().zip(metadatas) {
-            self.cache.insert(id, metadata);
+            self.cache.insert(id, Some(metadata));
         }
     }
 
@@ -162,7 +166,8 @@ impl LookAhead {
             .iter()
             .filter_map(|file_path| {
                 self.cache
-                    .remove(&file_path.id)?
+                    .remove(&file_path.id)
+                    .flatten()?  // uncached, or a tombstone (already logged)
                     .map(|metadata| {
                         (
                             // SAFETY: This should never happen

@@ -17,7 +17,7 @@ use std::io;
 use std::os::raw::{c_char, c_int, c_void};
 use std::os::unix::ffi::OsStrExt;
 use std::path::Path;
-use std::sync::OnceLock;
+use std::sync::{Arc, OnceLock};
 
 #[repr(C)]
 pub struct sd_cas_ctx {
@@ -61,6 +61,9 @@ pub const SD_COMM_ID_BYTES: usize = 128;
 extern "C" {
     pub fn sd_cas_abi_version() -> c_int;
     pub fn sd_cas_last_error() -> *const c_char;
+    // the host thread budget every call is capped by; "host_cpu_budget" sets it
+    pub fn sd_host_cpu_budget(out: *mut c_int) -> c_int;
+    pub fn sd_cas_set_tuning(key: *const c_char, value: c_int) -> c_int;
     pub fn sd_cas_ctx_create(device: c_int, out: *mut *mut sd_cas_ctx) -> c_int;
     pub fn sd_cas_ctx_destroy(ctx: *mut sd_cas_ctx);
     pub fn sd_cas_stage_plan(sizes: *const u64, n: usize, ext: *mut sd_extent, total: *mut u64) -> c_int;
@@ -89,6 +92,7 @@ extern "C" {
     pub fn sd_comm_create(ctx: *mut sd_cas_ctx, id: *const u8, nranks: c_int, rank: c_int,
                           out: *mut *mut sd_comm) -> c_int;
     pub fn sd_comm_destroy(comm: *mut sd_comm);
+    pub fn sd_comm_rccl_info(version: *mut c_int, path_out: *mut c_char, path_cap: usize) -> c_int;
     // the same collectives with the ranks as threads of one process (several GPUs, one process)
     pub fn sd_comm_group_create(nranks: c_int, out: *mut *mut sd_comm_group) -> c_int;
     pub fn sd_comm_group_destroy(group: *mut sd_comm_group);
@@ -242,7 +246,12 @@ pub fn checksum_blocking(path: &Path) -> Result<String, io::Error> {
 }
 
 /// libsdcas's RCCL communicator for a multi-GPU library scan (one process per GPU).
-pub struct Comm(*mut sd_comm);
+/// A member of an in-process group holds a reference to the group, so the group is
+/// destroyed only after its last member (sd_comm_destroy writes to the group).
+pub struct Comm {
+    raw: *mut sd_comm,
+    _group: Option<Arc<GroupHandle>>,
+}
 unsafe impl Send for Comm {}
 
 impl Comm {
@@ -259,48 +268,54 @@ impl Comm {
         let g = ctx()?;
         let mut p = std::ptr::null_mut();
         match unsafe { sd_comm_create(g.0, id.as_ptr(), nranks, rank, &mut p) } {
-            SD_OK => Ok(Comm(p)),
+            SD_OK => Ok(Comm { raw: p, _group: None }),
             _ => Err(io::Error::new(io::ErrorKind::Other, last_error())),
         }
     }
     /// One rank of an in-process group: the ranks are threads of this process, each with its
     /// own context (`ctx`, e.g. one per device from sd_cas_ctx_create); every collective has
-    /// the RCCL communicator's semantics.  Drop every member before the group.
+    /// the RCCL communicator's semantics.  The member keeps the group alive: dropping the
+    /// `CommGroup` first only releases the caller's handle.
     pub fn join_local(group: &CommGroup, ctx: *mut sd_cas_ctx, rank: i32) -> Result<Comm, io::Error> {
         let mut p = std::ptr::null_mut();
-        match unsafe { sd_comm_create_local(ctx, group.0, rank, &mut p) } {
-            SD_OK => Ok(Comm(p)),
+        match unsafe { sd_comm_create_local(ctx, group.0.0, rank, &mut p) } {
+            SD_OK => Ok(Comm { raw: p, _group: Some(Arc::clone(&group.0)) }),
             _ => Err(io::Error::new(io::ErrorKind::Other, last_error())),
         }
     }
     pub fn raw(&self) -> *mut sd_comm {
-        self.0
+        self.raw
     }
 }
 
 impl Drop for Comm {
     fn drop(&mut self) {
-        unsafe { sd_comm_destroy(self.0) }
+        // the communicator first; then the field drops release the group reference
+        unsafe { sd_comm_destroy(self.raw) }
+    }
+}
+
+/// The owned sd_comm_group; destroyed when the group handle and every member are gone.
+pub struct GroupHandle(*mut sd_comm_group);
+unsafe impl Send for GroupHandle {}
+unsafe impl Sync for GroupHandle {}
+
+impl Drop for GroupHandle {
+    fn drop(&mut self) {
+        unsafe { sd_comm_group_destroy(self.0) }
     }
 }
 
 /// The rendezvous of an in-process group of `nranks` ranks (sd_comm_group_create).
-pub struct CommGroup(*mut sd_comm_group);
-unsafe impl Send for CommGroup {}
-unsafe impl Sync for CommGroup {}
+pub struct CommGroup(Arc<GroupHandle>);
 
 impl CommGroup {
     pub fn new(nranks: i32) -> Result<CommGroup, io::Error> {
         let mut p = std::ptr::null_mut();
         match unsafe { sd_comm_group_create(nranks, &mut p) } {
-            SD_OK => Ok(CommGroup(p)),
+            SD_OK => Ok(CommGroup(Arc::new(GroupHandle(p)))),
             _ => Err(io::Error::new(io::ErrorKind::Other, last_error())),
         }
     }
 }
 
-impl Drop for CommGroup {
-    fn drop(&mut self) {
-        unsafe { sd_comm_group_destroy(self.0) }
-    }
-}

@@ -124,7 +124,27 @@ SIGNATURES = [
     ("sd_file_checksums_routes", I32, [P, P]),
     ("sd_cas_ids_stats", I32, [P, P]),
     ("sd_read_probe", I32, [P, P, U64, I32, P]),
+    ("sd_host_cpu_budget", I32, [P]),
+    ("sd_comm_rccl_info", I32, [ctypes.POINTER(I32), ctypes.c_char_p, SZ]),
 ]
+
+
+def host_cpu_budget() -> dict:
+    """The library's host thread budget (sd_host_cpu_budget)."""
+    out = (ctypes.c_int * 5)()
+    check(lib().sd_host_cpu_budget(out))
+    return {"budget": out[0], "affinity": out[1], "cgroup_quota_cpus": out[2] / 1000.0 if out[2] else None,
+            "local_world_size": out[3], "overridden": bool(out[4])}
+
+
+def rccl_info() -> dict:
+    """The RCCL that serves libsdcas's communicators in this process (sd_comm_rccl_info)."""
+    v = ctypes.c_int(0)
+    buf = ctypes.create_string_buffer(4096)
+    check(lib().sd_comm_rccl_info(ctypes.byref(v), buf, len(buf)))
+    code = v.value
+    return {"version_code": code, "version": f"{code // 10000}.{code // 100 % 100}.{code % 100}",
+            "path": os.path.realpath(buf.value.decode()) if buf.value else None}
 
 
 def lib():

@@ -304,8 +304,10 @@ int32_t cpu_cas_id_file(const char* path, uint64_t size, char out_hex17[17]) {
         if (f.fd < 0) return io_status(errno);
         {
             // a seekable file in one call (as stage_one): le64(size), then up to the buffer's
-            // room; a regular file's short count is its end.  A longer file, or a pipe
-            // (ESPIPE, nothing consumed), takes the streaming read below.
+            // room.  Exactly `size` bytes back (the file holds what its stat said) is the
+            // file; any other count -- a longer or shorter file, a filesystem that returns
+            // short counts -- or a pipe (ESPIPE, nothing consumed) takes the streaming read
+            // below, which reads until a read returns 0 as fs::read does.
             constexpr uint64_t ROOM = (128 << 10) - 8;
             uint8_t* msg = scratch(128 << 10);
             for (int i = 0; i < 8; i++) msg[i] = (uint8_t)(size >> (8 * i));
@@ -313,7 +315,7 @@ int32_t cpu_cas_id_file(const char* path, uint64_t size, char out_hex17[17]) {
             do {
                 r = pread(f.fd, msg + 8, ROOM, 0);
             } while (r < 0 && errno == EINTR);
-            if (r >= 0 && (uint64_t)r < ROOM) {
+            if (r >= 0 && (uint64_t)r == size) {
                 cpu_blake3(msg, 8 + (size_t)r, h);
                 hex_lower(h, 8, out_hex17);  // cas.rs:61 to_hex()[..16]
                 return SD_FILE_OK;
@@ -344,7 +346,8 @@ namespace {
 // fn(i) for i in [0, n) on up to nthreads threads (the caller's included)
 template <class F>
 void parallel_for(size_t n, int nthreads, F fn) {
-    nthreads = std::max(1, std::min<int>(nthreads, (int)std::min<size_t>(n, 256)));
+    // never more threads than the process's host budget (sd_host.h), the caller's included
+    nthreads = std::max(1, std::min<int>(cap_host_threads(nthreads), (int)std::min<size_t>(n, 256)));
     if (nthreads == 1) {
         for (size_t i = 0; i < n; i++) fn(i);
         return;
@@ -433,7 +436,6 @@ int sd_cpu_file_checksums(const char* const* paths, size_t n, char* out_hex65, i
     struct Big {
         size_t file;
         uint64_t len, nb;
-        int fd;
         std::vector<uint8_t> cvs;
         std::atomic<bool> failed{false};
     };
@@ -458,26 +460,17 @@ int sd_cpu_file_checksums(const char* const* paths, size_t n, char* out_hex65, i
             tasks.push_back({i, UINT64_MAX});
             continue;
         }
-        const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);  // hash.rs:11
-        if (fd < 0) {
-            tasks.push_back({i, UINT64_MAX});  // the read loop reports the error
-            continue;
-        }
+        // no descriptor is held across the call (a call of many large files would otherwise
+        // hold one per file and could exhaust RLIMIT_NOFILE for the whole process): every
+        // block task opens the path itself, and the end-of-file check reopens it
         auto b = std::make_unique<Big>();
         b->file = i;
         b->len = len[i];
         b->nb = (len[i] + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
-        b->fd = fd;
         b->cvs.resize(b->nb * 32);
         for (uint64_t k = 0; k < b->nb; k++) tasks.push_back({big.size(), k});
         big.push_back(std::move(b));
     }
-    struct Close {
-        std::vector<std::unique_ptr<Big>>& b;
-        ~Close() {
-            for (auto& x : b) close(x->fd);
-        }
-    } closer{big};
     parallel_for(tasks.size(), nthreads, [&](size_t t) {
         const Task& task = tasks[t];
         if (task.block == UINT64_MAX) {
@@ -493,7 +486,7 @@ int sd_cpu_file_checksums(const char* const* paths, size_t n, char* out_hex65, i
         const int fd = open(paths[b.file], O_RDONLY | O_CLOEXEC);
         const int64_t got = fd < 0 ? -1 : pread_full(fd, buf, want, off);
         if (fd >= 0) close(fd);
-        if (got != (int64_t)want) {  // shrank, replaced, or an error: the read loop below
+        if (got != (int64_t)want) {  // shrank, replaced, unopenable: the read loop below reports it
             b.failed.store(true, std::memory_order_relaxed);
             return;
         }
@@ -503,8 +496,13 @@ int sd_cpu_file_checksums(const char* const* paths, size_t n, char* out_hex65, i
     });
     for (auto& bp : big) {
         Big& b = *bp;
-        uint8_t probe;
-        if (!b.failed.load() && pread_full(b.fd, &probe, 1, b.len) == 0) {  // nothing past the stat length
+        bool at_end = false;
+        if (!b.failed.load()) {  // nothing past the stat length: the blocks were the whole file
+            Fd f{open(paths[b.file], O_RDONLY | O_CLOEXEC)};
+            uint8_t probe;
+            at_end = f.fd >= 0 && pread_full(f.fd, &probe, 1, b.len) == 0;
+        }
+        if (at_end) {
             uint8_t h[32];
             cpu_root_from_cvs(b.cvs.data(), b.nb, h);
             hex_lower(h, 32, out_hex65 + 65 * b.file);  // hash.rs:21-23

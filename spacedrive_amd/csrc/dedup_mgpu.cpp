@@ -28,8 +28,10 @@
 // host barrier.  It serves one process driving several GPUs, and it rehearses N ranks on
 // one GPU, which RCCL refuses ("Duplicate GPU detected") -- the partition, the gathered
 // plan, the per-peer offsets and the grouping are the same code either way.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <memory>
@@ -295,6 +297,21 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
     SD_GUARD_END
 }
 
+int sd_comm_rccl_info(int* version, char* path_out, size_t path_cap) {
+    SD_GUARD_BEGIN
+    if (!version) throw sd_failure(SD_ERR_INVALID, "null argument");
+    NCCL_OK(ncclGetVersion(version));
+    if (path_out && path_cap) {
+        // the file the dynamic linker bound this library's RCCL symbols to: librccl.so.1 is
+        // one soname, so a process that loaded another copy first (torch's) serves it here
+        Dl_info di{};
+        const char* f = dladdr(reinterpret_cast<void*>(&ncclGetVersion), &di) && di.dli_fname ? di.dli_fname : "";
+        snprintf(path_out, path_cap, "%s", f);
+    }
+    return SD_OK;
+    SD_GUARD_END
+}
+
 int sd_comm_set_timing(sd_comm* comm, int on) {
     SD_GUARD_BEGIN
     if (!comm) throw sd_failure(SD_ERR_INVALID, "null argument");
@@ -328,7 +345,9 @@ int sd_split_checksum_mgpu(sd_cas_ctx* ctx, sd_comm* comm, sd_split_checksum* sp
     HIP_OK(hipSetDevice(comm->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     check_rc(sd_split_checksum_leaves(ctx, split, d_slice, d_cvs, stream));
-    if (comm->nranks > 1) {
+    // over RCCL the all-gather runs at any rank count (one rank: an in-place copy of its own
+    // slots), so a one-GPU run drives the same collective an 8-GPU node does
+    if (comm->nranks > 1 || !comm->group) {
         const size_t slot_bytes = (size_t)p.q * 32;
         if (comm->group) local_allgather(comm, d_cvs + (size_t)p.rank * slot_bytes, d_cvs, slot_bytes, s);
         else NCCL_OK(ncclAllGather(d_cvs + (size_t)p.rank * slot_bytes, d_cvs, slot_bytes, ncclUint8, comm->comm, s));

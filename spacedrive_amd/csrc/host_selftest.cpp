@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -373,6 +374,98 @@ void test_cpu_batches() {
     CHECK((sa[n - 1] & 0xFFFF) == SD_FILE_IO_ERROR && (ta[n - 1] & 0xFFFF) == SD_FILE_IO_ERROR);
 }
 
+// many large files in one call under a low descriptor limit: sd_cpu_file_checksums holds no
+// descriptor per large file across the call, so every file still hashes
+void test_cpu_checksums_fd_limit() {
+    constexpr int NF = 40;
+    constexpr uint64_t LEN = (8ull << 20) + 4097;  // block-parallel (>= 8 MiB), sparse: zeros
+    std::vector<std::string> names;
+    for (int i = 0; i < NF; i++) {
+        const std::string p = g_dir + "/fdlim" + std::to_string(i);
+        const int fd = open(p.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0600);
+        CHECK(fd >= 0 && ftruncate(fd, (off_t)LEN) == 0);
+        if (fd >= 0) close(fd);
+        names.push_back(p);
+    }
+    std::vector<uint8_t> zeros(LEN, 0);
+    uint8_t want[32];
+    cpu_blake3(zeros.data(), LEN, want);
+    int open_now = 0;  // descriptors this process holds
+    if (DIR* d = opendir("/proc/self/fd")) {
+        while (readdir(d)) open_now++;
+        closedir(d);
+    }
+    struct rlimit old;
+    CHECK(getrlimit(RLIMIT_NOFILE, &old) == 0);
+    struct rlimit low = old;
+    low.rlim_cur = (rlim_t)open_now + 12;  // far fewer than NF
+    CHECK(setrlimit(RLIMIT_NOFILE, &low) == 0);
+    std::vector<const char*> paths;
+    for (auto& s : names) paths.push_back(s.c_str());
+    std::vector<char> out(65 * NF);
+    std::vector<int32_t> st(NF, -1);
+    CHECK(sd_cpu_file_checksums(paths.data(), NF, out.data(), st.data(), 4) == SD_OK);
+    CHECK(setrlimit(RLIMIT_NOFILE, &old) == 0);
+    for (int i = 0; i < NF; i++) {
+        CHECK(st[i] == SD_FILE_OK);
+        CHECK(std::string(&out[65 * i]) == hex(want, 32));
+    }
+}
+
+// ------------------------------------------------------------------ host thread budget
+void test_cpu_budget() {
+    // the rule: min(affinity, quota rounded up) / ranks on the host, at least 1
+    CpuBudget b = cpu_budget_resolve(256, 16.0, 8);  // an 8-GPU node, one 16-CPU quota
+    CHECK(b.budget == 2 && b.affinity == 256 && b.quota_milli == 16000 && b.local_world == 8);
+    CHECK(cpu_budget_resolve(256, 16.0, 1).budget == 16);  // one rank: the whole quota
+    CHECK(cpu_budget_resolve(256, 128.0, 8).budget == 16);
+    CHECK(cpu_budget_resolve(8, 0.0, 1).budget == 8);      // no quota: the affinity mask
+    CHECK(cpu_budget_resolve(8, 0.0, 1).quota_milli == 0);
+    CHECK(cpu_budget_resolve(4, 16.0, 8).budget == 1);     // never below one thread
+    CHECK(cpu_budget_resolve(64, 1.5, 1).budget == 2);     // a fractional quota rounds up
+    CHECK(cpu_budget_resolve(3, 64.0, 0).budget == 3);     // a bogus world size counts as 1
+    // the cgroup readers, on fake cgroup trees
+    const std::string v2 = g_dir + "/cg2", v1 = g_dir + "/cg1", v1c = v1 + "/cpu", none = g_dir + "/cg0";
+    CHECK(mkdir(v2.c_str(), 0700) == 0 && mkdir(v1.c_str(), 0700) == 0 && mkdir(v1c.c_str(), 0700) == 0 &&
+          mkdir(none.c_str(), 0700) == 0);
+    auto put = [](const std::string& p, const char* s) {
+        FILE* f = fopen(p.c_str(), "w");
+        if (!f) abort();
+        fputs(s, f);
+        fclose(f);
+    };
+    put(v2 + "/cpu.max", "1600000 100000\n");
+    CHECK(cgroup_cpu_quota(v2.c_str()) == 16.0);
+    put(v2 + "/cpu.max", "max 100000\n");
+    CHECK(cgroup_cpu_quota(v2.c_str()) == 0.0);
+    put(v1c + "/cpu.cfs_quota_us", "250000\n");
+    put(v1c + "/cpu.cfs_period_us", "100000\n");
+    CHECK(cgroup_cpu_quota(v1.c_str()) == 2.5);
+    put(v1c + "/cpu.cfs_quota_us", "-1\n");
+    CHECK(cgroup_cpu_quota(v1.c_str()) == 0.0);
+    CHECK(cgroup_cpu_quota(none.c_str()) == 0.0);
+    for (const std::string& f : {v2 + "/cpu.max", v1c + "/cpu.cfs_quota_us", v1c + "/cpu.cfs_period_us"})
+        unlink(f.c_str());
+    rmdir(v1c.c_str());
+    for (const std::string& d : {v2, v1, none}) rmdir(d.c_str());
+    // the override caps every call; the results do not depend on it
+    const int resolved = host_cpu_budget();
+    CHECK(resolved >= 1);
+    CHECK(sd_cas_set_tuning("host_cpu_budget", 3) == SD_OK);
+    CHECK(host_cpu_budget() == 3 && cap_host_threads(16) == 3 && cap_host_threads(2) == 2 && cap_host_threads(0) == 1);
+    int out[5];
+    CHECK(sd_host_cpu_budget(out) == SD_OK && out[0] == 3 && out[4] == 1);
+    std::vector<uint8_t> data = content(77, 3 << 20);
+    const uint64_t offs[3] = {0, 1 << 20, 2 << 20}, lens[3] = {1 << 20, 12345, (1 << 20) - 1};
+    uint8_t h3[96], h1[96];
+    CHECK(sd_cpu_checksums(data.data(), offs, lens, 3, h3, 16) == SD_OK);
+    CHECK(sd_cas_set_tuning("host_cpu_budget", 0) == SD_OK);
+    CHECK(host_cpu_budget() == resolved);
+    CHECK(sd_host_cpu_budget(out) == SD_OK && out[0] == resolved && out[4] == 0);
+    CHECK(sd_cpu_checksums(data.data(), offs, lens, 3, h1, 1) == SD_OK);
+    CHECK(memcmp(h3, h1, 96) == 0);
+}
+
 // ------------------------------------------------------------------ coalescer
 void test_coalescer() {
     std::vector<std::string> names;
@@ -554,6 +647,8 @@ int main() {
     test_readers();
     test_pool_growth();
     test_cpu_batches();
+    test_cpu_checksums_fd_limit();
+    test_cpu_budget();
     test_coalescer();
     test_exchange_plan();
     test_comm_group();

@@ -292,7 +292,7 @@ int sd_cas_stage_files(const char* const* paths, sd_extent* extents, size_t n, u
     SD_GUARD_BEGIN
     if (n && (!paths || !extents || !staged || !status)) throw sd_failure(SD_ERR_INVALID, "null argument");
     for (size_t i = 0; i < n; i++) validate_extent(extents[i], i);
-    if (nthreads < 1) nthreads = 1;
+    nthreads = cap_host_threads(nthreads);  // the process's host budget (sd_host.h)
     if ((size_t)nthreads > n) nthreads = n ? (int)n : 1;
     std::atomic<size_t> cursor{0};
     auto work = [&](bool own_table) {
@@ -399,9 +399,8 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
     // call is bound by PCIe; h host threads hash files from the END of the list on the CPU
     // path meanwhile, claiming chunks of files, while the windows for the GPU are claimed
     // from the front -- under one lock, so the two meet wherever their rates put them.
-    // (never more host threads than the machine has cores, less one for this thread)
-    const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS),
-                                             (int)std::thread::hardware_concurrency() - 1}));
+    // (never more host threads than the process's host budget, less one for this thread)
+    const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS), host_cpu_budget() - 1}));
     constexpr size_t COHASH_MIN = 8192, COHASH_CHUNK = 256;
     std::mutex claim_mu;
     size_t back = live.size();  // live[back, end) is claimed by the host threads

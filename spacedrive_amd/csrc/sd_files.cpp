@@ -274,8 +274,7 @@ void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes,
                uint8_t* d_hash32, int32_t* status, int nthreads) {
     ctx->bind();
     if (n == 0) return;
-    if (nthreads < 1) nthreads = 1;
-    if (nthreads > 64) nthreads = 64;
+    nthreads = std::min(64, cap_host_threads(nthreads));  // the process's host budget (sd_host.h)
     // nthreads reader threads stage in the background (start/wait) while this thread plans,
     // launches and harvests the windows
     std::shared_ptr<StagePool> pool = ctx->stage_pool(nthreads + 1);
@@ -344,6 +343,9 @@ void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes,
         std::vector<size_t> files;  // hashed files, in extent order
         bool busy = false;
     } launched[2];
+    // (everything the readers touch is declared before `cleanup`, whose destructor waits for
+    // them: a throw below must not end those lifetimes while a reader still runs)
+    const bool stage_hot = tuning_get(SD_TUNE_FILES_STAGE_HOT) != 0;
     struct Cleanup {  // on any exit: no reader left writing or waiting, no event leaked
         StagePool* pool;
         Shared* sh;
@@ -392,7 +394,6 @@ void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes,
         else HIP_CHECK(hipMemcpy(d_hash32 + 32 * f, h, 32, hipMemcpyHostToDevice));
     };
     // ---- the readers: file i into its window's ring buffer
-    const bool stage_hot = tuning_get(SD_TUNE_FILES_STAGE_HOT) != 0;
     pool->start(n, [&](size_t i) {
         const uint32_t w = win_of[i];
         const int r = (int)(w % (uint32_t)RING);
@@ -741,7 +742,7 @@ void gpu_file_checksums(sd_cas_ctx* ctx, const char* const* paths, char* out_hex
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65, int32_t* status) {
     SD_GUARD_BEGIN
     if (!ctx || (n && (!paths || !out_hex65 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
-    const int threads = std::max(1, std::min(64, tuning_get(SD_TUNE_READ_THREADS)));
+    const int threads = std::min(64, cap_host_threads(tuning_get(SD_TUNE_READ_THREADS)));
     const int cpu_max = std::max(0, tuning_get(SD_TUNE_CHECKSUM_CPU_MAX));
     const int hyb = std::max(0, tuning_get(SD_TUNE_CHECKSUM_HYBRID_THREADS));
     std::vector<uint64_t> hint;
@@ -895,9 +896,8 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     // 64 MiB -- and hashes them with h pool threads on the CPU path (a range of 8 MiB or
     // more block-parallel: its 1 MiB blocks' chaining values on all threads, then the root),
     // while the loop below claims its windows and streamed ranges from the front.
-    // (never more host threads than the machine has cores, less one for this thread)
-    const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS),
-                                             (int)std::thread::hardware_concurrency() - 1}));
+    // (never more host threads than the process's host budget, less one for this thread)
+    const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS), host_cpu_budget() - 1}));
     uint64_t all_bytes = 0;
     for (size_t q = 0; q < n; q++) all_bytes += lens[q];
     std::mutex claim_mu;

@@ -9,6 +9,7 @@
 #include <sys/syscall.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <sys/uio.h>
@@ -37,13 +38,78 @@ thread_local std::string g_err;
 // noise; profiles/r3/r3z_hybrid_checksum_probe.json); 15 host threads hashing beside the GPU in
 // large sd_cas_ids calls (profiles/r3/r3ad_cohash_probe.json: 300 000 files from pinned memory,
 // GPU alone 1.89-1.94 M files/s, CPU path alone 2.24-2.36 M, both at once 3.87-4.08 M)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {0}, {15}};
+// (and no override of the host thread budget: it is resolved from the process's CPUs)
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {0}, {15}, {0}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
                                                "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",
                                                "files_ring",         "checksum_cpu_max", "files_stage_hot",
-                                               "checksum_hybrid_threads", "host_cohash_threads"};
+                                               "checksum_hybrid_threads", "host_cohash_threads",
+                                               "host_cpu_budget"};
+
+bool read_small(const std::string& path, char* buf, size_t cap) {
+    FILE* f = fopen(path.c_str(), "re");
+    if (!f) return false;
+    const size_t got = fread(buf, 1, cap - 1, f);
+    fclose(f);
+    buf[got] = 0;
+    return got > 0;
+}
 }  // namespace
+
+// ------------------------------------------------------------------ host thread budget
+CpuBudget cpu_budget_resolve(int affinity, double quota_cpus, int local_world) {
+    CpuBudget b;
+    b.affinity = std::max(1, affinity);
+    b.quota_milli = quota_cpus > 0 ? (int)std::min(1e9, quota_cpus * 1000.0 + 0.5) : 0;
+    b.local_world = std::max(1, local_world);
+    // a fractional quota still runs that many threads' worth of time: round up, so a quota
+    // of 1.5 CPUs allows 2 threads, but never beyond the affinity mask
+    int cpus = b.affinity;
+    if (quota_cpus > 0) cpus = std::min(cpus, std::max(1, (int)(quota_cpus + 0.999)));
+    b.budget = std::max(1, cpus / b.local_world);
+    return b;
+}
+
+double cgroup_cpu_quota(const char* root) {
+    char buf[128];
+    const std::string r = root ? root : "/sys/fs/cgroup";
+    if (read_small(r + "/cpu.max", buf, sizeof buf)) {  // v2: "<quota|max> <period>"
+        char q[32] = {0};
+        double period = 0;
+        if (sscanf(buf, "%31s %lf", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+            return atof(q) / period;
+        return 0;
+    }
+    char pb[64];  // v1: cfs quota -1 = unlimited
+    if (read_small(r + "/cpu/cpu.cfs_quota_us", buf, sizeof buf) &&
+        read_small(r + "/cpu/cpu.cfs_period_us", pb, sizeof pb)) {
+        const double q = atof(buf), p = atof(pb);
+        if (q > 0 && p > 0) return q / p;
+    }
+    return 0;
+}
+
+CpuBudget host_cpu_budget_detail() {
+    static const CpuBudget resolved = [] {
+        int affinity = 1;
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        if (sched_getaffinity(0, sizeof set, &set) == 0) affinity = CPU_COUNT(&set);
+        int world = 1;
+        if (const char* w = getenv("LOCAL_WORLD_SIZE")) world = std::max(1, atoi(w));
+        return cpu_budget_resolve(affinity, cgroup_cpu_quota(nullptr), world);
+    }();
+    CpuBudget b = resolved;
+    const int o = tuning_get(SD_TUNE_HOST_CPU_BUDGET);
+    if (o > 0) {
+        b.budget = o;
+        b.overridden = 1;
+    }
+    return b;
+}
+
+int host_cpu_budget() { return host_cpu_budget_detail().budget; }
 
 void sd_set_err(const char* fmt, ...) {
     char buf[512];
@@ -104,6 +170,18 @@ ExchangePlan exchange_plan(const uint64_t* rows, int R, int me) {
 extern "C" {
 const char* sd_cas_last_error(void) { return g_err.c_str(); }
 int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }
+int sd_host_cpu_budget(int out[5]) {
+    SD_GUARD_BEGIN
+    if (!out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    const CpuBudget b = host_cpu_budget_detail();
+    out[0] = b.budget;
+    out[1] = b.affinity;
+    out[2] = b.quota_milli;
+    out[3] = b.local_world;
+    out[4] = b.overridden;
+    return SD_OK;
+    SD_GUARD_END
+}
 int sd_shard_plan(const uint64_t* sizes, size_t n, int nranks, uint64_t* bounds_out) {
     SD_GUARD_BEGIN
     if (!bounds_out || (n && !sizes)) throw sd_failure(SD_ERR_INVALID, "null argument");
@@ -412,12 +490,16 @@ int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged, std::vector<u
     if (f.fd < 0) return io_status(errno);
     if (e.kind == SD_KIND_WHOLE) {  // cas.rs:29 fs::read: read_to_end
         const uint64_t room = e.msg_len - 8;
+        uint64_t got = 0;
         {
-            // A seekable file in one call: the planned room plus a probe byte.  For a regular
-            // file a count short of what was asked is its end, so this is read_to_end's
-            // outcome without its final zero-length read; a count past the room means the
-            // file holds more than planned.  A pipe or character device fails with ESPIPE
-            // having consumed nothing, and takes the read loop below.
+            // A seekable file in one call: the planned room plus a probe byte.  Exactly the
+            // room back -- the file holds what its stat said, the common case -- is
+            // read_to_end's outcome without its final zero-length read; a count past the room
+            // means the file holds more than planned.  A count short of the room (a file that
+            // shrank, or a filesystem that returns short counts: FUSE direct_io, network
+            // mounts) continues in the read loop below until a read returns 0, as read_to_end
+            // does.  A pipe or character device fails with ESPIPE having consumed nothing,
+            // and takes the read loop from the start.
             uint8_t probe;
             struct iovec iov[2] = {{dst + 8, (size_t)room}, {&probe, 1}};
             ssize_t r;
@@ -426,13 +508,16 @@ int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged, std::vector<u
             } while (r < 0 && errno == EINTR);
             if (r >= 0) {
                 if ((uint64_t)r > room) return SD_FILE_CHANGED;  // the caller re-reads it whole
-                e.msg_len = (uint32_t)(8 + r);
-                memset(dst + e.msg_len, 0, padded - e.msg_len);
-                return SD_FILE_OK;
+                if ((uint64_t)r == room) {
+                    memset(dst + e.msg_len, 0, padded - e.msg_len);
+                    return SD_FILE_OK;
+                }
+                if (lseek(f.fd, (off_t)r, SEEK_SET) < 0) return io_status(errno);
+                got = (uint64_t)r;
+            } else if (errno != ESPIPE) {
+                return io_status(errno);
             }
-            if (errno != ESPIPE) return io_status(errno);
         }
-        uint64_t got = 0;
         for (;;) {
             if (got == room) {  // planned room full: does the file hold more?
                 uint8_t probe;

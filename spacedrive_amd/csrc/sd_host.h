@@ -63,9 +63,36 @@ enum sd_tune_key {
     SD_TUNE_FILES_STAGE_HOT = 11,   // sd_cas_ids_files: read into a per-thread buffer, stream-copy to the window
     SD_TUNE_CHECKSUM_HYBRID_THREADS = 12,  // sd_file_checksums: reader threads of the GPU route in a hybrid call
     SD_TUNE_HOST_COHASH_THREADS = 13,      // sd_cas_ids: host threads hashing beside the GPU (large calls)
-    SD_TUNE_NKEYS = 14
+    SD_TUNE_HOST_CPU_BUDGET = 14,          // cap on the host threads one call starts (0 = resolve it)
+    SD_TUNE_NKEYS = 15
 };
 int tuning_get(int key);
+
+// ------------------------------------------------------------------ host thread budget
+// The host threads one call of this process may run at once: the
+// CPUs the process may use -- min(its affinity mask, its cgroup's CPU bandwidth quota) --
+// divided by the GPU ranks that share the node's host (LOCAL_WORLD_SIZE, which
+// torch.distributed.run sets; 1 when absent), at least 1.  "host_cpu_budget" > 0 replaces
+// the resolved value (a Rust host that knows its own share sets it).  Every pool size,
+// reader count and co-hash thread count is capped by it.
+struct CpuBudget {
+    int budget = 1;       // the cap
+    int affinity = 1;     // CPUs in sched_getaffinity
+    int quota_milli = 0;  // cgroup CPU quota in milli-CPUs (0 = no limit)
+    int local_world = 1;  // ranks per node sharing the host
+    int overridden = 0;   // 1 when "host_cpu_budget" set the cap
+};
+// pure arithmetic of the rule (host_selftest checks it with fake quotas and world sizes)
+CpuBudget cpu_budget_resolve(int affinity, double quota_cpus, int local_world);
+// the CPU bandwidth limit of the cgroup mounted at `root` (v2 cpu.max, else v1
+// cpu/cpu.cfs_quota_us / cpu.cfs_period_us), in CPUs; 0 when unlimited or unreadable
+double cgroup_cpu_quota(const char* root);
+CpuBudget host_cpu_budget_detail();  // resolved once per process, then the override applied
+int host_cpu_budget();
+inline int cap_host_threads(int n) {
+    const int b = host_cpu_budget();
+    return n < 1 ? 1 : (n > b ? b : n);
+}
 
 // latency path (coalesce.cpp): single-file calls, CPU route or coalesced GPU batches
 struct sd_coalescer;

@@ -28,11 +28,19 @@ def _ptr(x) -> Optional[int]:
 
 
 def _stream(stream) -> Optional[int]:
+    """The HIP stream handle a wrapper passes to the C ABI.  A stream other than the
+    current one is first ordered after the work queued so far on the current stream (an
+    event recorded there, waited on by `stream`): the inputs a caller just produced --
+    torch fills, copies, kernels on the current stream -- are complete before the
+    library's kernels read them, with no manual wait_stream.  The reverse order (the
+    outputs, consumed back on the current stream) stays the caller's, as in torch."""
+    cur = torch.cuda.current_stream()
     if stream is None:
-        return torch.cuda.current_stream().cuda_stream
-    if isinstance(stream, torch.cuda.Stream):
-        return stream.cuda_stream
-    return int(stream)
+        return cur.cuda_stream
+    s = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.ExternalStream(int(stream))
+    if s.cuda_stream != cur.cuda_stream:
+        s.wait_stream(cur)
+    return s.cuda_stream
 
 
 def stage_plan(sizes) -> tuple:
@@ -84,6 +92,9 @@ class Context:
         keep, arr = path_array(paths)
         sz = np.ascontiguousarray(sizes, dtype=np.uint64)
         assert d_hash32.numel() >= 32 * n and (d_valid is None or d_valid.numel() >= n)
+        # the library writes the rows from its own streams: whatever the caller queued on
+        # the current stream (e.g. the buffers' zero fills) must be done first
+        torch.cuda.current_stream().synchronize()
         check(lib().sd_cas_hashes_files(self.handle, arr, _ptr(sz), n, _ptr(d_hash32),
                                         None if d_valid is None else _ptr(d_valid), _ptr(status), nthreads))
         return status[:n]

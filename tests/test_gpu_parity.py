@@ -989,7 +989,6 @@ def test_dedup_of_one_batch_beside_the_next_batchs_hashing(ctx, rccl_comm):
     valid = [torch.from_numpy((lib[0] != 0).astype(np.uint8)).cuda() for lib in libs]
     hs, ds = torch.cuda.Stream(), torch.cuda.Stream()
     bufs = [torch.zeros(n * 32, dtype=torch.uint8, device="cuda") for _ in range(2)]
-    hs.wait_stream(torch.cuda.current_stream())  # the zero fills, queued on the default stream
     e_hash = [torch.cuda.Event() for _ in range(2)]
     e_ded = [torch.cuda.Event() for _ in range(2)]
     runner = dedup.RcclDedup(ctx, rccl_comm, bufs[0].device, capacity=n + 1024)
@@ -1420,7 +1419,6 @@ def test_split_checksum_mgpu_in_process_ranks(ctx, oracle_native):
             cvs = torch.zeros(sc.cv_bytes, dtype=torch.uint8, device="cuda")
             out = torch.zeros(32, dtype=torch.uint8, device="cuda")
             st = torch.cuda.Stream()
-            st.wait_stream(torch.cuda.current_stream())  # the zero fills above, queued on that stream
             sc.mgpu(comms[r], d[sc.offset:], cvs, out, stream=st)
             st.synchronize()
             sc.close()
@@ -1559,3 +1557,47 @@ def test_scan_library_from_files(ctx, tmp_path, oracle_native, rccl_comm):
     assert np.array_equal(r["owner"].cpu().numpy(), own)
     t = scan_library(ctx, paths, sizes)  # the torch.distributed statement of the exchange
     assert t["n_groups"] == gng and np.array_equal(t["records"].cpu().numpy(), gr)
+
+
+def test_wrappers_order_side_streams_after_the_current_stream(ctx, oracle_native, rccl_comm):
+    """The Python wrappers that take a `stream` (CasBatch.run, RcclDedup, SplitChecksum.mgpu)
+    order it after the work queued on the current stream: each input below is produced by
+    a kernel just queued on the current stream, and the wrapper is called on a fresh side
+    stream with no manual wait_stream -- its outputs equal the serial ones."""
+    from spacedrive_amd import dedup
+    from spacedrive_amd.device import SplitChecksum
+    n = 200_000
+    sizes, cids, twins = synth.library(0, n, n, dup_frac=0.2)
+    want = gpu_cas(ctx, sizes, cids, twins)  # serial, synchronised
+    # (1) CasBatch.run: the staged messages are still being generated on the current stream
+    ext, _, d_staged = stage_synth(ctx, sizes, cids, twins)
+    b = ctx.cas_batch(ext)
+    side = torch.cuda.Stream()
+    out = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")  # a fill queued on the current stream
+    b.run(d_staged, out, side)
+    side.synchronize()
+    assert np.array_equal(out.cpu().numpy().reshape(n, 32), want)
+    # (2) RcclDedup: the hashes are being recomputed on the current stream
+    d_hash = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    b.run(d_staged, d_hash)
+    valid = (sizes != 0)
+    d_valid = torch.from_numpy(valid.astype(np.uint8)).cuda()
+    runner = dedup.RcclDedup(ctx, rccl_comm, d_hash.device, capacity=n + 1024)
+    recs, rep, ng, owner = runner(d_hash.view(n, 32), d_valid, n, 0, stream=torch.cuda.Stream())
+    torch.cuda.synchronize()
+    keys = keys_from_hashes(want)
+    gr, grep, gng = group_host(np.stack([keys.view(np.int64), np.arange(n, dtype=np.int64)], 1)[valid])
+    assert ng == gng and np.array_equal(recs.cpu().numpy(), gr) and np.array_equal(rep.cpu().numpy(), grep)
+    # (3) SplitChecksum.mgpu: 1 GiB of file bytes still being generated on the current stream
+    total = (1 << 30) + 333
+    d = torch.empty(total + 128, dtype=torch.uint8, device="cuda")
+    ctx.synth_fill(903, 0, total, d)
+    sc = SplitChecksum(ctx, total, 1, 0)
+    cvs = torch.zeros(sc.cv_bytes, dtype=torch.uint8, device="cuda")
+    h = torch.zeros(32, dtype=torch.uint8, device="cuda")
+    side2 = torch.cuda.Stream()
+    sc.mgpu(rccl_comm, d, cvs, h, stream=side2)
+    side2.synchronize()
+    assert bytes(h.cpu().numpy()).hex() == oracle_native.checksum_synth_mt(total, 903, 0, nthreads=NT).hex()
+    sc.close()
+    b.close()
