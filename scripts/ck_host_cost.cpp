@@ -1,0 +1,269 @@
+// ck_host_cost.cpp -- host CPU cost per byte of the validator's paths from the page cache
+// (VERDICT r3 item 4): what it costs the host to hand file bytes to the GPU, against what
+// it costs to read and hash them on the CPU (sd_file_checksums' two routes, hash.rs:10-24).
+//
+// Files: NF x FL bytes written to /dev/shm (tmpfs: every read is a page-cache copy), then
+// every mode reads all of them with T threads in 64 MiB units claimed from one cursor:
+//   read_pinned    1 MiB preads straight into a pinned window (the GPU route's readers today)
+//   read_hot_nt    256 KiB preads into a per-thread cache-resident buffer, then streaming
+//                  (non-temporal) stores into the pinned window (the cas stager's copy)
+//   read_hash      1 MiB preads into a per-thread buffer + BLAKE3 of it on this thread
+//                  (sd_cpu_checksums, one thread: the CPU path's work per block)
+//   read_hot       256 KiB preads into the per-thread buffer only (the read floor)
+//   hash_hot       BLAKE3 of a cache-resident 1 MiB buffer, no read (the hash alone)
+//   *_dma          the same, each filled 64 MiB unit DMA'd to the device (hipMemcpyAsync on
+//                  the thread's stream, double-buffered): the GPU route's host side at PCIe rate
+//   hybrid_g       g threads read_hot_nt_dma + T-g threads read_hash on one shared cursor:
+//                  sd_file_checksums split between the routes
+// Each line: wall GB/s, and host CPU time per byte (every thread's CLOCK_THREAD_CPUTIME_ID,
+// summed) in ns/B and in cycles/B at the clock given by --ghz (the box's nominal clock).
+//
+// Build (on the CPU container; runs on the GPU box):
+//   hipcc -O2 -std=c++17 -mavx2 -o scripts/ck_host_cost scripts/ck_host_cost.cpp \
+//         -Lspacedrive_amd -lsdcas -Wl,-rpath,'$ORIGIN/../spacedrive_amd' -lpthread
+// Run: scripts/ck_host_cost [NF=32] [FL_MiB=256] [ghz=2.4]  -> JSON lines on stdout
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <immintrin.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <string>
+#include <thread>
+#include <vector>
+
+extern "C" int sd_cpu_checksums(const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
+                                uint8_t* out_hash32, int nthreads);
+
+namespace {
+constexpr uint64_t UNIT = 64ull << 20, MiB = 1ull << 20, HOT = 256ull << 10;
+int NF = 32;
+uint64_t FL = 256 * MiB;
+double GHZ = 2.4;
+std::string DIR = "/dev/shm/sd_ckcost";
+
+#define HIPOK(x)                                                                  \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));               \
+            exit(3);                                                              \
+        }                                                                         \
+    } while (0)
+
+double thread_cpu_s() {
+    timespec t;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
+    return t.tv_sec + t.tv_nsec * 1e-9;
+}
+
+void nt_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    for (uint64_t o = 0; o < n; o += 64) {
+        const __m256i a = _mm256_load_si256(reinterpret_cast<const __m256i*>(src + o));
+        const __m256i b = _mm256_load_si256(reinterpret_cast<const __m256i*>(src + o + 32));
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + o), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + o + 32), b);
+    }
+    _mm_sfence();
+}
+
+int64_t pread_all(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
+    uint64_t got = 0;
+    while (got < n) {
+        const ssize_t r = pread(fd, dst + got, n - got, (off_t)(off + got));
+        if (r <= 0) return r < 0 ? -1 : (int64_t)got;
+        got += (uint64_t)r;
+    }
+    return (int64_t)got;
+}
+
+std::string path_of(int f) { return DIR + "/f" + std::to_string(f); }
+
+void make_files() {
+    mkdir(DIR.c_str(), 0700);
+    std::vector<std::thread> th;
+    for (int t = 0; t < 8; t++)
+        th.emplace_back([t] {
+            std::vector<uint64_t> buf(MiB / 8);
+            for (int f = t; f < NF; f += 8) {
+                const int fd = open(path_of(f).c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0600);
+                uint64_t x = 0x9E3779B97F4A7C15ull * (uint64_t)(f + 1);
+                for (uint64_t o = 0; o < FL; o += MiB) {
+                    for (auto& w : buf) {  // xorshift64*: incompressible, cheap
+                        x ^= x >> 12;
+                        x ^= x << 25;
+                        x ^= x >> 27;
+                        w = x * 0x2545F4914F6CDD1Dull;
+                    }
+                    if (write(fd, buf.data(), MiB) != (ssize_t)MiB) exit(4);
+                }
+                close(fd);
+            }
+        });
+    for (auto& x : th) x.join();
+}
+
+struct Res {
+    double wall = 0, cpu = 0;
+    uint64_t bytes = 0;
+};
+
+enum Kind { READ_PINNED, READ_HOT_NT, READ_HASH, READ_HOT, HASH_HOT };
+const char* NAMES[] = {"read_pinned", "read_hot_nt", "read_hash", "read_hot", "hash_hot"};
+
+struct ThreadBufs {
+    uint8_t* pinned[2] = {nullptr, nullptr};  // two UNIT windows (double buffer for the DMA)
+    uint8_t* hot = nullptr;                   // 1 MiB, cache-resident working buffer
+    void* dev = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool pending[2] = {false, false};
+};
+
+// runs `kinds[t]` on thread t (dma[t]: DMA each filled unit) over all units of all files
+Res run(const std::vector<int>& kinds, const std::vector<int>& dma, std::vector<ThreadBufs>& bufs) {
+    const int T = (int)kinds.size();
+    const uint64_t per_file = FL / UNIT, units = per_file * (uint64_t)NF;
+    std::atomic<uint64_t> cursor{0};
+    std::vector<double> cpu(T, 0);
+    std::atomic<uint64_t> total{0};
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+            const double c0 = thread_cpu_s();
+            ThreadBufs& B = bufs[t];
+            int b = 0;
+            uint8_t hash[32];
+            const int kind = kinds[t];
+            for (;;) {
+                uint64_t u;
+                if (kind == HASH_HOT) {
+                    u = cursor.fetch_add(1);
+                    if (u >= units) break;
+                    for (uint64_t o = 0; o < UNIT; o += MiB) {
+                        const uint64_t off = 0, len = MiB;
+                        sd_cpu_checksums(B.hot, &off, &len, 1, hash, 1);
+                    }
+                    total += UNIT;
+                    continue;
+                }
+                u = cursor.fetch_add(1);
+                if (u >= units) break;
+                const int f = (int)(u / per_file);
+                const uint64_t base = (u % per_file) * UNIT;
+                const int fd = open(path_of(f).c_str(), O_RDONLY);
+                if (fd < 0) exit(5);
+                if (dma[t] && B.pending[b]) {
+                    HIPOK(hipEventSynchronize(B.ev[b]));
+                    B.pending[b] = false;
+                }
+                uint8_t* win = B.pinned[b];
+                for (uint64_t o = 0; o < UNIT;) {
+                    switch (kind) {
+                        case READ_PINNED:
+                            if (pread_all(fd, win + o, MiB, base + o) != (int64_t)MiB) exit(6);
+                            o += MiB;
+                            break;
+                        case READ_HOT_NT:
+                            if (pread_all(fd, B.hot, HOT, base + o) != (int64_t)HOT) exit(6);
+                            nt_copy(win + o, B.hot, HOT);
+                            o += HOT;
+                            break;
+                        case READ_HASH: {
+                            if (pread_all(fd, B.hot, MiB, base + o) != (int64_t)MiB) exit(6);
+                            const uint64_t off = 0, len = MiB;
+                            sd_cpu_checksums(B.hot, &off, &len, 1, hash, 1);
+                            o += MiB;
+                            break;
+                        }
+                        case READ_HOT:
+                            if (pread_all(fd, B.hot, HOT, base + o) != (int64_t)HOT) exit(6);
+                            o += HOT;
+                            break;
+                    }
+                }
+                close(fd);
+                if (dma[t]) {
+                    HIPOK(hipMemcpyAsync(B.dev, win, UNIT, hipMemcpyHostToDevice, B.s));
+                    HIPOK(hipEventRecord(B.ev[b], B.s));
+                    B.pending[b] = true;
+                    b ^= 1;
+                }
+                total += UNIT;
+            }
+            for (int k = 0; k < 2; k++)
+                if (B.pending[k]) {
+                    HIPOK(hipEventSynchronize(B.ev[k]));
+                    B.pending[k] = false;
+                }
+            cpu[t] = thread_cpu_s() - c0;
+        });
+    for (auto& x : th) x.join();
+    Res r;
+    r.wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    for (double c : cpu) r.cpu += c;
+    r.bytes = total.load();
+    return r;
+}
+
+void report(const char* name, int T, int g, const Res& r) {
+    const double ns_b = r.cpu * 1e9 / (double)r.bytes;
+    printf("{\"mode\": \"%s\", \"threads\": %d, \"gpu_route_threads\": %d, \"GBps\": %.2f, \"cpu_ns_per_byte\": %.4f, "
+           "\"cycles_per_byte\": %.3f, \"cpu_s\": %.3f, \"wall_s\": %.3f, \"bytes\": %llu}\n",
+           name, T, g, (double)r.bytes / r.wall / 1e9, ns_b, ns_b * GHZ, r.cpu, r.wall, (unsigned long long)r.bytes);
+    fflush(stdout);
+}
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc > 1) NF = atoi(argv[1]);
+    if (argc > 2) FL = (uint64_t)atoi(argv[2]) * MiB;
+    if (argc > 3) GHZ = atof(argv[3]);
+    if (FL % UNIT) FL = (FL / UNIT + 1) * UNIT;
+    make_files();
+    const int TMAX = 16;
+    std::vector<ThreadBufs> bufs(TMAX);
+    for (auto& B : bufs) {
+        for (int k = 0; k < 2; k++) {
+            HIPOK(hipHostMalloc(reinterpret_cast<void**>(&B.pinned[k]), UNIT, hipHostMallocDefault));
+            memset(B.pinned[k], 0, UNIT);
+            HIPOK(hipEventCreateWithFlags(&B.ev[k], hipEventDisableTiming));
+        }
+        B.hot = static_cast<uint8_t*>(aligned_alloc(4096, MiB));
+        memset(B.hot, 1, MiB);
+        HIPOK(hipMalloc(&B.dev, UNIT));
+        HIPOK(hipStreamCreateWithFlags(&B.s, hipStreamNonBlocking));
+    }
+    // page cache warm (the files were just written) -- one untimed pass anyway
+    run(std::vector<int>(TMAX, READ_HOT), std::vector<int>(TMAX, 0), bufs);
+    for (int T : {1, 4, 8, 16})
+        for (int kind : {READ_PINNED, READ_HOT_NT, READ_HASH, READ_HOT, HASH_HOT})
+            report(NAMES[kind], T, 0, run(std::vector<int>(T, kind), std::vector<int>(T, 0), bufs));
+    for (int T : {2, 4, 8})  // the GPU route's host side at PCIe rate
+        for (int kind : {READ_PINNED, READ_HOT_NT}) {
+            const std::string name = std::string(NAMES[kind]) + "_dma";
+            report(name.c_str(), T, T, run(std::vector<int>(T, kind), std::vector<int>(T, 1), bufs));
+        }
+    for (int g : {0, 2, 3, 4, 6}) {  // 16 threads split between the routes
+        for (int gk : {READ_PINNED, READ_HOT_NT}) {
+            if (g == 0 && gk == READ_HOT_NT) continue;
+            std::vector<int> kinds(TMAX, READ_HASH), dma(TMAX, 0);
+            for (int t = 0; t < g; t++) {
+                kinds[t] = gk;
+                dma[t] = 1;
+            }
+            const std::string name = std::string("hybrid_") + (gk == READ_PINNED ? "pinned" : "hot_nt");
+            report(name.c_str(), TMAX, g, run(kinds, dma, bufs));
+        }
+    }
+    for (int f = 0; f < NF; f++) unlink(path_of(f).c_str());
+    rmdir(DIR.c_str());
+    return 0;
+}
