@@ -232,11 +232,13 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
  * ("read_threads"); a pipe or device sequentially.  Small files are packed many per
  * pinned window, large ones (or ones that grow while read) streamed window by window,
  * whatever their final length; two windows alternate so host reads overlap the H2D
- * copies and the kernels.  Batch policy: with "checksum_hybrid_threads" g > 0 (default 0:
- * off), a call whose regular files of >= 8 MiB add up to >= 512 MiB is split between that
- * GPU route (on g of the "read_threads") and sd_cpu_file_checksums (the rest of the
- * threads), running at once: the large files go to whichever route is free next, the small
- * ones to the CPU path.  Any other call of at most "checksum_cpu_max" files is
+ * copies and the kernels (the readers stream each piece through a cache-resident buffer into
+ * the pinned window, "checksum_stage_hot" 1).  Batch policy: with "checksum_hybrid_threads"
+ * g > 0 (default 4), a call whose regular files of >= 8 MiB add up to >= 512 MiB is split
+ * between that GPU route (on g of the 16 "read_threads"; fewer under a smaller host budget)
+ * and sd_cpu_file_checksums (the rest of the threads), running at once: the large files go
+ * to whichever route is free next, the small ones to the CPU path -- from the page cache
+ * 1.13-1.21x the CPU path alone.  Any other call of at most "checksum_cpu_max" files is
  * hashed by sd_cpu_file_checksums on "read_threads" threads -- by default every such call,
  * because from the page cache the host's threads hash faster than PCIe can carry the bytes
  * to the GPU; "checksum_cpu_max" 0 = the GPU route alone for every call. */
@@ -442,8 +444,10 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * copies; "files_stage_hot" (1): its readers read each file into a per-thread buffer and
  * stream-copy it into the window (0 = read straight into the window); "checksum_cpu_max" (2147483647): sd_file_checksums calls of at most that many
  * files take the CPU path (sd_cpu_file_checksums on "read_threads" threads; 0 = the GPU
- * route always); "checksum_hybrid_threads" (0): reader threads of the GPU route when
+ * route always); "checksum_hybrid_threads" (4): reader threads of the GPU route when
  * sd_file_checksums splits a large call with the CPU path (0 = never split);
+ * "checksum_stage_hot" (1): sd_file_checksums' GPU-route readers deliver through a
+ * cache-resident buffer and streaming stores (0 = pread straight into the pinned window);
  * "host_cohash_threads" (15): host threads hashing beside the GPU in sd_cas_ids calls of
  * >= 8192 files and sd_checksums calls of >= 1 GiB (0 = the GPU alone; never more than the
  * host budget less one); "host_cpu_budget" (0 = resolved, see sd_host_cpu_budget): the cap

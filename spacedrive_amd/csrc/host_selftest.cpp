@@ -276,13 +276,14 @@ void test_readers() {
         const std::string p = write_file("rd" + std::to_string(n), data);
         // par: parallel preads; hint: the EOF probe at the stat length (exact, or stale by
         // one byte short, as for a file that grew after its stat)
-        for (int par = 0; par < 2; par++)
+        for (int par = 0; par < 3; par++)  // 2: pread_stream on at most 3 of the pool's threads
             for (int hint = 0; hint < 3; hint++) {
                 const int fd = open(p.c_str(), O_RDONLY);
                 MsgSource src(fd, MsgSource::CHECKSUM_READS);
-                if (par) src.set_parallel(&pool);
+                if (par == 1) src.set_parallel(&pool);
+                if (par == 2) src.set_parallel(&pool, 3, true);
                 if (hint) src.set_eof_hint(hint == 1 ? n : (n ? n - 1 : 0));
-                std::vector<uint8_t> got, win(2 << 20);
+                std::vector<uint8_t> got, win(2 << 20);  // (malloc'd: 16-byte aligned, as windows are)
                 int reads = 0;
                 for (;;) {
                     const uint64_t k = src.read(win.data(), win.size());
@@ -310,6 +311,65 @@ void test_readers() {
         close(fd);
         CHECK(got.size() == n + 8 && got[0] == 0x88 && got[7] == 0x11);
         CHECK(std::equal(data.begin(), data.end(), got.begin() + 8));
+    }
+}
+
+// pread_stream == pread_full: any length, any file offset, short files, an unaligned target
+void test_pread_stream() {
+    const size_t n = (3ul << 20) + 12345;
+    const auto data = content(4242, n);
+    const std::string p = write_file("pstream", data);
+    const int fd = open(p.c_str(), O_RDONLY);
+    CHECK(fd >= 0);
+    std::vector<uint8_t> a(n + 256), b(n + 256);
+    for (uint64_t off : {0ul, 1ul, 4096ul, (1ul << 20) + 7, n - 100, n, n + 5})
+        for (uint64_t len : {0ul, 15ul, 16ul, 1000ul, 262144ul, 262145ul, (2ul << 20) + 33, n})
+            for (size_t dst : {0ul, 16ul, 3ul}) {
+                memset(a.data(), 0xAA, a.size());
+                memset(b.data(), 0xAA, b.size());
+                const uint64_t room = std::min<uint64_t>(len, a.size() - 64);
+                const int64_t ra = pread_full(fd, a.data() + dst, room, off);
+                const int64_t rb = pread_stream(fd, b.data() + dst, room, off);
+                CHECK(ra == rb && a == b);
+            }
+    close(fd);
+    CHECK(pread_stream(-1, a.data(), 10, 0) < 0);  // errors pass through
+}
+
+// a run limited to k threads runs its tasks on at most k distinct threads, on a larger pool
+void test_pool_limit() {
+    StagePool pool(8);
+    for (int k : {1, 2, 3, 8}) {
+        std::mutex mu;
+        std::vector<std::thread::id> ids;
+        std::atomic<int> sum{0};
+        pool.run(
+            400,
+            [&](size_t i) {
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    if (std::find(ids.begin(), ids.end(), std::this_thread::get_id()) == ids.end())
+                        ids.push_back(std::this_thread::get_id());
+                }
+                volatile int spin = 0;
+                for (int s = 0; s < 2000; s++) spin = spin + s;
+                sum += (int)i;
+            },
+            k);
+        CHECK(sum.load() == 399 * 400 / 2 && (int)ids.size() <= k);
+        std::atomic<int> sum2{0};
+        ids.clear();
+        pool.start(
+            100,
+            [&](size_t i) {
+                std::lock_guard<std::mutex> g(mu);
+                if (std::find(ids.begin(), ids.end(), std::this_thread::get_id()) == ids.end())
+                    ids.push_back(std::this_thread::get_id());
+                sum2 += (int)i;
+            },
+            k);
+        pool.wait();
+        CHECK(sum2.load() == 99 * 100 / 2 && (int)ids.size() <= k);
     }
 }
 
@@ -645,6 +705,8 @@ int main() {
     test_planners();
     test_stager();
     test_readers();
+    test_pread_stream();
+    test_pool_limit();
     test_pool_growth();
     test_cpu_batches();
     test_cpu_checksums_fd_limit();

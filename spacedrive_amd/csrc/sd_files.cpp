@@ -592,6 +592,12 @@ void gpu_file_checksums(sd_cas_ctx* ctx, const char* const* paths, char* out_hex
     // let the next pack's reads overlap this one's H2D and kernels (one 80 MB pack of 100
     // files took 4.7 ms against 2.3 ms for the CPU path, read-bound alike)
     constexpr uint64_t PACK = 32ull << 20;
+    // the readers deliver through pread_stream (page cache -> L2 -> streaming stores into the
+    // pinned window): 0.068 host ns/B against 0.087 for pread straight into the window, and
+    // one DRAM read of the window's lines fewer (profiles/r4/r4b_ck_host_cost.jsonl)
+    const bool stream_hot = tuning_get(SD_TUNE_CHECKSUM_STAGE_HOT) != 0;
+    // the pools may hold more threads than this call's read_threads (a previous call grew
+    // them): every run below is limited to read_threads
     std::shared_ptr<StagePool> pool = ctx->stage_pool(read_threads);  // per-file tasks (packs)
     std::shared_ptr<StagePool> iopool;  // preads of one open file (streamed files), created on first use
     SlotPair slots(ctx);
@@ -626,7 +632,7 @@ void gpu_file_checksums(sd_cas_ctx* ctx, const char* const* paths, char* out_hex
         MsgSource src(fd, MsgSource::CHECKSUM_READS);
         if (reg) {
             if (!iopool) iopool = ctx->io_pool(read_threads);
-            src.set_parallel(iopool.get());
+            src.set_parallel(iopool.get(), read_threads, stream_hot);
             src.set_eof_hint((uint64_t)st.st_size);  // a window-multiple file ends with its last window
         }
         try {
@@ -654,7 +660,8 @@ void gpu_file_checksums(sd_cas_ctx* ctx, const char* const* paths, char* out_hex
                 status[i] = io_status(errno);
                 return;
             }
-            const int64_t got = pread_full(fd, win + pack_off[q], hint[i], 0);
+            const int64_t got = stream_hot ? pread_stream(fd, win + pack_off[q], hint[i], 0)
+                                           : pread_full(fd, win + pack_off[q], hint[i], 0);
             uint8_t probe;
             const int64_t more = got == (int64_t)hint[i] ? pread_full(fd, &probe, 1, hint[i]) : 0;
             close(fd);
@@ -667,7 +674,7 @@ void gpu_file_checksums(sd_cas_ctx* ctx, const char* const* paths, char* out_hex
                 pack_len[q] = (uint64_t)got;  // shrank: hash.rs stops at EOF
                 memset(win + pack_off[q] + got, 0, align_up(got, 64) - got);
             }
-        });
+        }, read_threads);
         std::vector<uint64_t> offs, lens;
         std::vector<size_t> ok;
         for (size_t q = 0; q < pack.size(); q++) {
@@ -725,18 +732,21 @@ void gpu_file_checksums(sd_cas_ctx* ctx, const char* const* paths, char* out_hex
 // file_checksum (hash.rs:10-24) for n paths: the batch policy picks the CPU path, the GPU
 // route (gpu_file_checksums) or both at once.
 //   * "checksum_cpu_max" = 0: the GPU route for every call.
-//   * Hybrid ("checksum_hybrid_threads" = g > 0; off by default): a call whose regular files
-//     of >= 8 MiB add up to >= 512 MiB is split.  From the page cache the GPU route is
-//     PCIe-bound with few reader threads while the CPU path is bound by its threads
-//     (scripts/hybrid_checksum_probe.py), so the GPU route gets g of the "read_threads" and
-//     the CPU path the rest, on a second host thread.  The large files go to whichever
-//     route is free next (one shared cursor, largest first), so neither waits on a static
-//     split; the small and non-regular files go to the CPU path.  Measured from the page
-//     cache (profiles/r3/r3z_hybrid_checksum_probe.json) it is not a reliable win: the GPU
-//     route's reader threads spend about as much CPU copying page-cache bytes into pinned
-//     memory as the CPU path spends reading and hashing them, so the split moves little
-//     work off the host (78-90 GB/s against 81-87 for the CPU path alone).  Kept opt-in for
-//     hosts with fewer cores per GPU.
+//   * Hybrid ("checksum_hybrid_threads" = g, default 4): a call whose regular files of
+//     >= 8 MiB add up to >= 512 MiB is split.  Handing a byte to the GPU costs the host
+//     0.068 ns (pread into a cache-resident buffer, streaming stores into the pinned window:
+//     pread_stream), hashing it on the CPU path 0.172 ns (the pread plus 0.110 ns of
+//     AVX-512 BLAKE3) -- scripts/ck_host_cost.cpp, profiles/r4/r4b_ck_host_cost.jsonl -- so a
+//     few reader threads fill PCIe while the rest hash: the GPU route gets g of the
+//     "read_threads" (g of 16, fewer under a smaller host budget) and the CPU path the rest,
+//     on a second host thread.  The large files go to whichever route is free next (one
+//     shared cursor, largest first; the CPU half takes ~16 MiB per thread at a time), so
+//     neither waits on a static split; the small and non-regular files go to the CPU path.
+//     From the page cache: 1.13-1.21x the CPU path alone at g = 4
+//     (scripts/hybrid_checksum_probe2.py,
+//     profiles/r4/r4c_hybrid_checksum_probe.json).  (Round 3's split ran its GPU half
+//     on pools grown to 16 threads by earlier calls and read straight into pinned memory:
+//     78-90 against 81-87 GB/s, profiles/r3/r3z_hybrid_checksum_probe.json.)
 //   * Otherwise calls of at most "checksum_cpu_max" files (default: all) take the CPU path:
 //     from the page cache the host's threads hash faster than PCIe carries the bytes.
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65, int32_t* status) {
@@ -744,7 +754,10 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
     if (!ctx || (n && (!paths || !out_hex65 || !status))) throw sd_failure(SD_ERR_INVALID, "null argument");
     const int threads = std::min(64, cap_host_threads(tuning_get(SD_TUNE_READ_THREADS)));
     const int cpu_max = std::max(0, tuning_get(SD_TUNE_CHECKSUM_CPU_MAX));
-    const int hyb = std::max(0, tuning_get(SD_TUNE_CHECKSUM_HYBRID_THREADS));
+    // the GPU route's share of the readers in a split call: "checksum_hybrid_threads" g of
+    // 16, scaled down with a smaller host budget (g = 4: 2 of 8 threads, 1 of 4)
+    const int hyb_knob = std::max(0, tuning_get(SD_TUNE_CHECKSUM_HYBRID_THREADS));
+    const int hyb = threads >= 16 ? hyb_knob : std::min(hyb_knob, std::max(1, hyb_knob * threads / 16));
     std::vector<uint64_t> hint;
     std::vector<uint8_t> regular;
     if (cpu_max != 0 && hyb > 0 && hyb < threads && n >= 2) {
@@ -789,12 +802,36 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
                         memcpy(out_hex65 + 65 * rest[q], hex.data() + 65 * q, 65);
                     }
                 }
-                for (size_t i; (i = next_big()) != SIZE_MAX;) {  // then large files, as they come
-                    cpu_rc = sd_cpu_file_checksums(paths + i, 1, out_hex65 + 65 * i, status + i, cpu_threads);
+                // then large files, as they come.  The CPU path hashes a file's 1 MiB blocks on
+                // all its threads and idles them at the file's last blocks, so it claims files
+                // until it holds about 16 MiB per thread (the large ones come first, singly; the
+                // smaller tail of the list a few at a time)
+                const uint64_t group_bytes = (uint64_t)cpu_threads << 24;
+                std::vector<size_t> grp;
+                std::vector<const char*> gp;
+                std::vector<char> ghex;
+                std::vector<int32_t> gst;
+                for (;;) {
+                    grp.clear();
+                    uint64_t bytes = 0;
+                    for (size_t i; bytes < group_bytes && (i = next_big()) != SIZE_MAX;) {
+                        grp.push_back(i);
+                        bytes += hint[i];
+                    }
+                    if (grp.empty()) break;
+                    gp.resize(grp.size());
+                    ghex.resize(grp.size() * 65);
+                    gst.resize(grp.size());
+                    for (size_t q = 0; q < grp.size(); q++) gp[q] = paths[grp[q]];
+                    cpu_rc = sd_cpu_file_checksums(gp.data(), grp.size(), ghex.data(), gst.data(), cpu_threads);
                     if (cpu_rc != SD_OK) {
                         cpu_err = sd_cas_last_error();
                         cursor.store(big.size());
                         return;
+                    }
+                    for (size_t q = 0; q < grp.size(); q++) {
+                        status[grp[q]] = gst[q];
+                        memcpy(out_hex65 + 65 * grp[q], ghex.data() + 65 * q, 65);
                     }
                 }
               } catch (...) {  // an allocation here: nothing may escape a thread

@@ -15,6 +15,8 @@
 #include <sys/uio.h>
 #include <unistd.h>
 
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <atomic>
 
@@ -30,22 +32,22 @@ thread_local std::string g_err;
 // p50 per call from the page cache on 16 threads: GPU route / CPU path 286 / 109 us at 100
 // files, 3.39 / 3.07 ms at 4000, 6.24 / 6.36 ms at 8000, 10.8 / 13.7 ms at 16000 -- a call's
 // fixed GPU-route cost loses below ~8000 files), 4 pinned windows the stager may fill ahead, every
-// sd_file_checksums call on the CPU path (from the page cache the host hashes
-// faster than PCIe carries the bytes), the stager's readers through their cache-resident
-// buffers (profiles/r3/r3n_files_ab_private_fds.json: 1.04 vs 0.84 M files/s), and no split
-// of sd_file_checksums calls between the GPU route and the CPU path (opt-in: from the page
-// cache it measured 78-90 GB/s against 81-87 for the CPU path alone, within the box's
-// noise; profiles/r3/r3z_hybrid_checksum_probe.json); 15 host threads hashing beside the GPU in
+// sd_file_checksums call on the CPU path unless it is large enough to split (DESIGN.md §4:
+// from the page cache the host hashes faster than PCIe carries the bytes), the stager's
+// readers through their cache-resident buffers (profiles/r3/r3n_files_ab_private_fds.json:
+// 1.04 vs 0.84 M files/s), large sd_file_checksums calls split between the GPU route on 4
+// of the 16 readers and the CPU path on the rest, the GPU route's readers through
+// pread_stream (profiles/r4/r4c_hybrid_checksum_probe.json: 1.13-1.21x the CPU path alone
+// from the page cache); no host thread budget override; 15 host threads hashing beside the GPU in
 // large sd_cas_ids calls (profiles/r3/r3ad_cohash_probe.json: 300 000 files from pinned memory,
 // GPU alone 1.89-1.94 M files/s, CPU path alone 2.24-2.36 M, both at once 3.87-4.08 M)
-// (and no override of the host thread budget: it is resolved from the process's CPUs)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {0}, {15}, {0}};
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {4}, {15}, {0}, {1}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
                                                "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",
                                                "files_ring",         "checksum_cpu_max", "files_stage_hot",
                                                "checksum_hybrid_threads", "host_cohash_threads",
-                                               "host_cpu_budget"};
+                                               "host_cpu_budget",    "checksum_stage_hot"};
 
 bool read_small(const std::string& path, char* buf, size_t cap) {
     FILE* f = fopen(path.c_str(), "re");
@@ -481,6 +483,27 @@ int64_t pread_full(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
     return (int64_t)got;
 }
 
+int64_t pread_stream(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
+    constexpr uint64_t HOT = 256 << 10;
+    thread_local std::unique_ptr<uint8_t[]> hot_buf(new uint8_t[HOT + 64]);
+    uint8_t* hot = reinterpret_cast<uint8_t*>(sd_align_up(reinterpret_cast<uintptr_t>(hot_buf.get()), 64));
+    if (reinterpret_cast<uintptr_t>(dst) % 16) return pread_full(fd, dst, n, off);  // (never, for windows)
+    uint64_t got = 0;
+    while (got < n) {
+        const uint64_t want = std::min(HOT, n - got);
+        const int64_t r = pread_full(fd, hot, want, off + got);
+        if (r < 0) return r;
+        const uint64_t body = (uint64_t)r & ~uint64_t(15);
+        for (uint64_t o = 0; o < body; o += 16)
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + got + o), _mm_load_si128(reinterpret_cast<const __m128i*>(hot + o)));
+        memcpy(dst + got + body, hot + body, (uint64_t)r - body);
+        got += (uint64_t)r;
+        if ((uint64_t)r < want) break;  // EOF
+    }
+    _mm_sfence();  // the streamed lines are globally visible before the caller hands dst on
+    return (int64_t)got;
+}
+
 int32_t stage_one(const char* path, sd_extent& e, uint8_t* staged, std::vector<uint8_t>* capture) {
     uint8_t* dst = staged + e.msg_offset;
     const uint64_t size = e.size;
@@ -657,10 +680,15 @@ uint64_t MsgSource::read_impl(uint8_t* dst, uint64_t n) {
 uint64_t MsgSource::read_parallel(uint8_t* dst, uint64_t n) {
     const uint64_t pieces = (n + CHECKSUM_READ - 1) / CHECKSUM_READ;
     std::vector<int64_t> r(pieces, 0);
-    pool_->run(pieces, [&](size_t k) {
-        const uint64_t len = std::min<uint64_t>(CHECKSUM_READ, n - k * CHECKSUM_READ);
-        r[k] = pread_full(fd_, dst + k * CHECKSUM_READ, len, file_pos_ + k * CHECKSUM_READ);
-    });
+    pool_->run(
+        pieces,
+        [&](size_t k) {
+            const uint64_t len = std::min<uint64_t>(CHECKSUM_READ, n - k * CHECKSUM_READ);
+            uint8_t* d = dst + k * CHECKSUM_READ;
+            const uint64_t at = file_pos_ + k * CHECKSUM_READ;
+            r[k] = par_stream_ ? pread_stream(fd_, d, len, at) : pread_full(fd_, d, len, at);
+        },
+        par_threads_);
     uint64_t got = 0;
     for (uint64_t k = 0; k < pieces; k++) {
         if (r[k] < 0) {

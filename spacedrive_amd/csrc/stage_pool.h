@@ -2,7 +2,10 @@
 // windows generate_cas_id reads, cas.rs:27-58).  run(n, f) calls f(0..n-1) on the pool
 // and the calling thread and returns when all are done; start(n, f) / wait() do the same
 // on the worker threads only while the caller goes on with other work.  One run at a time
-// per pool (a start() holds the pool until its wait()).
+// per pool (a start() holds the pool until its wait()).  A pool grows to the largest thread
+// count any call asked for; `limit` makes one run use no more threads than its call asked
+// for (the caller included in run()), so a call sized for 3 readers does not run on the 16
+// a previous call left in the pool.
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -23,7 +26,7 @@ void private_fd_table();
 class StagePool {
 public:
     explicit StagePool(int nthreads, bool private_fds = false) : private_fds_(private_fds) {
-        for (int t = 1; t < nthreads; t++) th_.emplace_back([this] { worker(); });
+        for (int t = 1; t < nthreads; t++) th_.emplace_back([this, t] { worker(t); });
     }
     bool private_fds() const { return private_fds_; }
     ~StagePool() {
@@ -35,7 +38,7 @@ public:
         for (auto& t : th_) t.join();
     }
     int threads() const { return (int)th_.size() + 1; }
-    void run(size_t n, const std::function<void(size_t)>& f) {
+    void run(size_t n, const std::function<void(size_t)>& f, int limit = 1 << 30) {
         std::lock_guard<std::mutex> serial(run_mu_);
         {
             std::lock_guard<std::mutex> g(mu_);
@@ -43,6 +46,7 @@ public:
             n_ = n;
             next_.store(0);
             busy_ = (int)th_.size();
+            active_ = limit;  // workers 1 .. limit-1 take tasks; the caller is thread 0
             gen_++;
         }
         cv_.notify_all();
@@ -52,7 +56,7 @@ public:
         fn_ = nullptr;
     }
 
-    void start(size_t n, std::function<void(size_t)> f) {
+    void start(size_t n, std::function<void(size_t)> f, int limit = 1 << 30) {
         run_mu_.lock();  // held until wait(), on this thread
         async_fn_ = std::move(f);
         {
@@ -61,6 +65,7 @@ public:
             n_ = n;
             next_.store(0);
             busy_ = (int)th_.size();
+            active_ = limit < 1 ? 2 : limit + 1;  // the caller takes no tasks here: workers 1 .. limit
             gen_++;
         }
         cv_.notify_all();
@@ -84,7 +89,7 @@ private:
             (*fn_)(i);
         }
     }
-    void worker() {
+    void worker(int idx) {
         if (private_fds_) private_fd_table();
         uint64_t seen = 0;
         std::unique_lock<std::mutex> g(mu_);
@@ -92,8 +97,9 @@ private:
             cv_.wait(g, [&] { return stop_ || gen_ != seen; });
             if (stop_) return;
             seen = gen_;
+            const bool take = idx < active_;
             g.unlock();
-            drain();
+            if (take) drain();
             g.lock();
             if (--busy_ == 0) done_.notify_all();
         }
@@ -106,6 +112,7 @@ private:
     size_t n_ = 0;
     std::atomic<size_t> next_{0};
     int busy_ = 0;
+    int active_ = 1 << 30;  // this run's thread limit (worker index < active_ takes tasks)
     uint64_t gen_ = 0;
     bool stop_ = false;
     const bool private_fds_;

@@ -268,3 +268,47 @@ def test_path_array_and_hex_results(tmp_path):
             assert r == cpu.generate_cas_id(f, s)
         else:
             assert isinstance(r, OSError) and r.filename == f
+
+
+def test_host_cpu_budget_caps_and_override():
+    """The host thread budget: resolved from this process's CPUs, at
+    least 1 and at most its affinity mask; "host_cpu_budget" > 0 replaces it and 0 restores
+    the resolved value; a CPU-path call with more threads than the budget gives the same
+    results (it is clamped, not refused)."""
+    import spacedrive_amd as sd
+    b = sd.host_cpu_budget()
+    assert 1 <= b["budget"] <= b["affinity"] == len(os.sched_getaffinity(0)) and not b["overridden"]
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    assert b["local_world_size"] == max(1, lw)
+    data = np.random.default_rng(3).integers(0, 256, 5 << 20, dtype=np.uint8)
+    offs = np.array([0, 1 << 20, 3 << 20], np.uint64)
+    lens = np.array([1 << 20, (2 << 20) + 7, 12345], np.uint64)
+    want = np.zeros((3, 32), np.uint8)
+    check(lib().sd_cpu_checksums(data.ctypes.data, offs.ctypes.data, lens.ctypes.data, 3, want.ctypes.data, 1))
+    try:
+        sd.set_tuning("host_cpu_budget", 2)
+        assert sd.host_cpu_budget()["budget"] == 2 and sd.host_cpu_budget()["overridden"]
+        got = np.zeros((3, 32), np.uint8)
+        check(lib().sd_cpu_checksums(data.ctypes.data, offs.ctypes.data, lens.ctypes.data, 3, got.ctypes.data, 64))
+        assert np.array_equal(got, want)
+    finally:
+        sd.set_tuning("host_cpu_budget", 0)
+    assert sd.host_cpu_budget() == b
+
+
+def test_host_cpu_budget_divides_by_local_world_size():
+    """Each of the node's ranks gets its share: a process started as one of 4 local ranks
+    (LOCAL_WORLD_SIZE=4, as torch.distributed.run sets it) resolves min(affinity, quota) / 4."""
+    import math
+    import sys
+    code = ("import os, json, spacedrive_amd as sd; "
+            "print(json.dumps(sd.host_cpu_budget()))")
+    env = dict(os.environ, LOCAL_WORLD_SIZE="4")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__)))).stdout
+    import json
+    b = json.loads(out.strip().splitlines()[-1])
+    cpus = b["affinity"]
+    if b["cgroup_quota_cpus"]:
+        cpus = min(cpus, max(1, math.ceil(b["cgroup_quota_cpus"] - 1e-9)))
+    assert b["local_world_size"] == 4 and b["budget"] == max(1, cpus // 4)

@@ -495,7 +495,7 @@ def test_file_checksums_packing_and_streaming(ctx, tmp_path):
 
 
 def test_file_checksums_hybrid_split(ctx, tmp_path):
-    """sd_file_checksums' split policy (opt-in "checksum_hybrid_threads"): a call whose regular
+    """sd_file_checksums' split policy ("checksum_hybrid_threads", default 4): a call whose regular
     files of >= 8 MiB total >= 512 MiB runs the GPU route and the CPU path at once, the large
     files going to whichever is free, the small ones and a FIFO to the CPU path.  Every
     result equals the oracle's read schedule (hash.rs:10-24), an unreadable path keeps its
@@ -529,7 +529,7 @@ def test_file_checksums_hybrid_split(ctx, tmp_path):
     want = dict(zip([p for p in paths if p != fifo], zip(want_h, want_st)))
     keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads")}
     sd.set_tuning("checksum_cpu_max", 2147483647)  # the library default (the module sets 0)
-    sd.set_tuning("checksum_hybrid_threads", 6)  # opt-in
+    sd.set_tuning("checksum_hybrid_threads", 4)  # the library default
     try:
         before = sd.file_checksums_stats()
         t = threading.Thread(target=feed)
