@@ -920,10 +920,13 @@ def file_backed(ctx, sizes, ext, d_staged, k: int, with_cpu: bool, latency_calls
 
 def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
     """file_checksum from files on tmpfs (hash.rs:10-24): 256 MiB files through the drop-in
-    sd_file_checksums (1 MiB reads into pinned windows overlapped with H2D + kernels; the
-    GPU route, "checksum_cpu_max" = 0) and through its default policy, beside the
-    reference's read schedule + the SIMD C restatement (oracle, 1, 16 and all threads) and
-    the library's CPU path (16 and all threads); outputs asserted equal."""
+    sd_file_checksums -- its GPU route alone ("checksum_cpu_max" = 0: 1 MiB reads streamed
+    into pinned windows, overlapped with H2D + kernels) and its default policy (a call this
+    large is split between the GPU route on 4 readers and the CPU path on the rest) -- and
+    the library's CPU path on 16 threads, interleaved over 4 rounds (the first warms; the
+    host's load drifts, so the routes alternate), medians reported; then the CPU path on
+    every usable CPU and the reference's read schedule + the SIMD C restatement (oracle, 1,
+    16 and all threads).  Outputs asserted equal, and checked against the oracle."""
     import shutil
     import spacedrive_amd as sd
     nf = max(1, mib // 256)
@@ -941,29 +944,47 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
         del buf
         total = nf * flen
         res = {"files": nf, "bytes": total, "dir_fs": _fs_type(d)}
-        gpu = None
         default_cpu_max = sd.get_tuning("checksum_cpu_max")
-        for key, cpu_max in (("gpu", 0), ("policy_default", default_cpu_max)):
-            sd.set_tuning("checksum_cpu_max", cpu_max)
-            try:
-                runs = []
-                for _ in range(3):  # the first run warms the slots' pinned windows and the page cache
-                    t0 = time.perf_counter()
-                    got = sd.file_checksums(paths)
-                    runs.append(time.perf_counter() - t0)
-            finally:
-                sd.set_tuning("checksum_cpu_max", default_cpu_max)
-            gpu = gpu or got
-            assert got == gpu
-            res[key] = {"GBps": total / min(runs[1:]) / 1e9, "seconds": min(runs[1:]), "first_run_s": runs[0]}
+        gpu = sd.cpu.file_checksums(paths, nthreads=16)
+
+        def route(cpu_max):
+            def f():
+                sd.set_tuning("checksum_cpu_max", cpu_max)
+                try:
+                    return sd.file_checksums(paths)
+                finally:
+                    sd.set_tuning("checksum_cpu_max", default_cpu_max)
+            return f
+        legs = {"gpu": route(0), "policy_default": route(default_cpu_max),
+                "library_cpu_path": lambda: sd.cpu.file_checksums(paths, nthreads=16)}
+        runs = {k: [] for k in legs}
+        routes0 = sd.file_checksums_stats()
+        for rnd in range(4):  # round 0 warms the windows, the pools and the page cache
+            for k, f in legs.items():
+                t0 = time.perf_counter()
+                got = f()
+                dt = time.perf_counter() - t0
+                assert got == gpu, k
+                if rnd:
+                    runs[k].append(dt)
+        routes1 = sd.file_checksums_stats()
+        for k in legs:
+            res[k] = {"GBps": total / float(np.median(runs[k])) / 1e9, "GBps_best": total / min(runs[k]) / 1e9,
+                      "seconds_median": float(np.median(runs[k])), "rounds": len(runs[k])}
+        res["library_cpu_path"]["threads"] = 16
+        res["policy_default"]["route"] = {k: routes1[k] - routes0[k] for k in routes1}
+        res["policy_default"]["hybrid_threads"] = sd.get_tuning("checksum_hybrid_threads")
+        res["policy_default_over_cpu_path"] = res["policy_default"]["GBps"] / res["library_cpu_path"]["GBps"]
+        res["note"] = ("medians of 3 interleaved rounds after a warm one; policy_default splits this call between "
+                       "the GPU route (hybrid_threads readers) and the CPU path (DESIGN.md §4.1)")
         from oracle import native
         bad = sum(native.checksum_synth_mt(flen, 30_000 + i, 0, nthreads=oracle_threads()).hex() != gpu[i]
                   for i in range(nf))
         res["parity"] = parity(nf, bad, "every file's checksum vs the C oracle's chunk-parallel BLAKE3 of the same "
                                         "content")
-        res["gpu"]["note"] = ("sd_file_checksums, GPU route: hash.rs's 1 MiB reads as parallel preads into 256 MiB "
-                              "pinned windows, two slots alternating (reads overlap H2D + kernels); best of 2 warm runs")
-        for nt, key in ((16, "library_cpu_path"), (effective_cpus(), "library_cpu_path_all_cores")):
+        res["gpu"]["note"] = ("sd_file_checksums, GPU route: hash.rs's 1 MiB reads as parallel preads streamed into "
+                              "256 MiB pinned windows, two slots alternating (reads overlap H2D + kernels)")
+        for nt, key in ((effective_cpus(), "library_cpu_path_all_cores"),):
             cpu_runs = []
             for _ in range(2):
                 t0 = time.perf_counter()

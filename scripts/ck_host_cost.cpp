@@ -13,8 +13,11 @@
 //   hash_hot       BLAKE3 of a cache-resident 1 MiB buffer, no read (the hash alone)
 //   *_dma          the same, each filled 64 MiB unit DMA'd to the device (hipMemcpyAsync on
 //                  the thread's stream, double-buffered): the GPU route's host side at PCIe rate
-//   hybrid_g       g threads read_hot_nt_dma + T-g threads read_hash on one shared cursor:
-//                  sd_file_checksums split between the routes
+//   zero_copy_dma  no host copy at all: each 64 MiB unit of the file mmap'ed read-only,
+//                  page-locked in place (hipHostRegister, read-only) and DMA'd from the page
+//                  cache itself; the next unit is registered while the previous one's DMA runs
+//   hybrid_g       g threads read_hot_nt_dma (or zero_copy_dma) + T-g threads read_hash on
+//                  one shared cursor: sd_file_checksums split between the routes
 // Each line: wall GB/s, and host CPU time per byte (every thread's CLOCK_THREAD_CPUTIME_ID,
 // summed) in ns/B and in cycles/B at the clock given by --ghz (the box's nominal clock).
 //
@@ -28,6 +31,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
@@ -114,8 +118,8 @@ struct Res {
     uint64_t bytes = 0;
 };
 
-enum Kind { READ_PINNED, READ_HOT_NT, READ_HASH, READ_HOT, HASH_HOT };
-const char* NAMES[] = {"read_pinned", "read_hot_nt", "read_hash", "read_hot", "hash_hot"};
+enum Kind { READ_PINNED, READ_HOT_NT, READ_HASH, READ_HOT, HASH_HOT, ZERO_COPY };
+const char* NAMES[] = {"read_pinned", "read_hot_nt", "read_hash", "read_hot", "hash_hot", "zero_copy"};
 
 struct ThreadBufs {
     uint8_t* pinned[2] = {nullptr, nullptr};  // two UNIT windows (double buffer for the DMA)
@@ -124,7 +128,18 @@ struct ThreadBufs {
     hipStream_t s = nullptr;
     hipEvent_t ev[2] = {nullptr, nullptr};
     bool pending[2] = {false, false};
+    void* map[2] = {nullptr, nullptr};  // zero copy: the registered mapping behind ev[k]
 };
+
+// zero copy: release mapping k once its DMA is done
+void zc_release(ThreadBufs& B, int k) {
+    if (!B.map[k]) return;
+    HIPOK(hipEventSynchronize(B.ev[k]));
+    HIPOK(hipHostUnregister(B.map[k]));
+    munmap(B.map[k], UNIT);
+    B.map[k] = nullptr;
+    B.pending[k] = false;
+}
 
 // runs `kinds[t]` on thread t (dma[t]: DMA each filled unit) over all units of all files
 Res run(const std::vector<int>& kinds, const std::vector<int>& dma, std::vector<ThreadBufs>& bufs) {
@@ -160,6 +175,20 @@ Res run(const std::vector<int>& kinds, const std::vector<int>& dma, std::vector<
                 const uint64_t base = (u % per_file) * UNIT;
                 const int fd = open(path_of(f).c_str(), O_RDONLY);
                 if (fd < 0) exit(5);
+                if (kind == ZERO_COPY) {  // map + pin this unit, DMA it, release the one before
+                    void* m = mmap(nullptr, UNIT, PROT_READ, MAP_SHARED, fd, (off_t)base);
+                    close(fd);
+                    if (m == MAP_FAILED) exit(7);
+                    zc_release(B, b);  // two units in flight at most
+                    HIPOK(hipHostRegister(m, UNIT, hipHostRegisterReadOnly));
+                    HIPOK(hipMemcpyAsync(B.dev, m, UNIT, hipMemcpyHostToDevice, B.s));
+                    HIPOK(hipEventRecord(B.ev[b], B.s));
+                    B.map[b] = m;
+                    B.pending[b] = true;
+                    b ^= 1;
+                    total += UNIT;
+                    continue;
+                }
                 if (dma[t] && B.pending[b]) {
                     HIPOK(hipEventSynchronize(B.ev[b]));
                     B.pending[b] = false;
@@ -198,11 +227,13 @@ Res run(const std::vector<int>& kinds, const std::vector<int>& dma, std::vector<
                 }
                 total += UNIT;
             }
-            for (int k = 0; k < 2; k++)
+            for (int k = 0; k < 2; k++) {
+                zc_release(B, k);
                 if (B.pending[k]) {
                     HIPOK(hipEventSynchronize(B.ev[k]));
                     B.pending[k] = false;
                 }
+            }
             cpu[t] = thread_cpu_s() - c0;
         });
     for (auto& x : th) x.join();
@@ -251,15 +282,18 @@ int main(int argc, char** argv) {
             const std::string name = std::string(NAMES[kind]) + "_dma";
             report(name.c_str(), T, T, run(std::vector<int>(T, kind), std::vector<int>(T, 1), bufs));
         }
+    for (int T : {1, 2, 4, 8})  // the GPU route with no host copy
+        report("zero_copy_dma", T, T, run(std::vector<int>(T, ZERO_COPY), std::vector<int>(T, 1), bufs));
     for (int g : {0, 2, 3, 4, 6}) {  // 16 threads split between the routes
-        for (int gk : {READ_PINNED, READ_HOT_NT}) {
-            if (g == 0 && gk == READ_HOT_NT) continue;
+        for (int gk : {READ_PINNED, READ_HOT_NT, ZERO_COPY}) {
+            if (g == 0 && gk != READ_PINNED) continue;
             std::vector<int> kinds(TMAX, READ_HASH), dma(TMAX, 0);
             for (int t = 0; t < g; t++) {
                 kinds[t] = gk;
                 dma[t] = 1;
             }
-            const std::string name = std::string("hybrid_") + (gk == READ_PINNED ? "pinned" : "hot_nt");
+            const std::string name = std::string("hybrid_") +
+                                     (gk == READ_PINNED ? "pinned" : gk == READ_HOT_NT ? "hot_nt" : "zero_copy");
             report(name.c_str(), TMAX, g, run(kinds, dma, bufs));
         }
     }

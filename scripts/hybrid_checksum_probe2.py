@@ -8,7 +8,7 @@ rounds on two tmpfs file sets (the bench's 32 x 256 MiB, and 48 files of 8..320 
   gpu_16[_hot0]          the GPU route alone ("checksum_cpu_max" 0), pread_stream on / off
   hybrid_g[_hot0]        the policy's split, "checksum_hybrid_threads" g
 Every call's output is asserted equal to the CPU path's.
-python scripts/hybrid_checksum_probe2.py -> one JSON line (per-round rows on stderr)"""
+python scripts/hybrid_checksum_probe2.py [rounds] [legs,...] -> one JSON line (per-round rows on stderr)"""
 import ctypes
 import json
 import os
@@ -87,8 +87,10 @@ def main():
             legs = [("cpu_16", cpu16), ("gpu_16", policy(0, 0, 1)), ("gpu_16_hot0", policy(0, 0, 0))]
             legs += [(f"hybrid_{g}", policy(2147483647, g, 1)) for g in (2, 3, 4, 5, 6, 8)]
             legs += [("hybrid_3_hot0", policy(2147483647, 3, 0))]
+            if len(sys.argv) > 2:
+                legs = [lg for lg in legs if lg[0] in sys.argv[2].split(",")]
             rounds = []
-            for rnd in range(3):  # interleaved: the box's host load drifts
+            for rnd in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):  # interleaved: host load drifts
                 r = {k: timed(f) for k, f in legs}
                 rounds.append(r)
                 print(json.dumps({"set": name, "round": rnd, **r}), file=sys.stderr, flush=True)
