@@ -343,8 +343,10 @@ def cpu_baseline(sizes, cids, twins, seconds: float):
 
 # ------------------------------------------------------------------ parity of the timed steps
 def oracle_threads() -> int:
-    """host threads for the oracle checks: the CPUs this process may use, at most 16"""
-    return max(1, min(16, effective_cpus()))
+    """host threads for the oracle checks: this rank's share of the host (the library's host
+    thread budget, min(affinity, quota) / LOCAL_WORLD_SIZE), at most 16"""
+    from spacedrive_amd._native import host_cpu_budget
+    return max(1, min(16, host_cpu_budget()["budget"]))
 
 
 def sample_idx(n: int, k: int = 4096, head: int = 32) -> np.ndarray:
@@ -959,14 +961,20 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
                 "library_cpu_path": lambda: sd.cpu.file_checksums(paths, nthreads=16)}
         runs = {k: [] for k in legs}
         routes0 = sd.file_checksums_stats()
+        split_bytes = {"gpu": 0, "cpu_in_split": 0}
         for rnd in range(4):  # round 0 warms the windows, the pools and the page cache
             for k, f in legs.items():
+                b0 = sd.file_checksums_bytes()
                 t0 = time.perf_counter()
                 got = f()
                 dt = time.perf_counter() - t0
                 assert got == gpu, k
                 if rnd:
                     runs[k].append(dt)
+                    if k == "policy_default":
+                        b1 = sd.file_checksums_bytes()
+                        for x in split_bytes:
+                            split_bytes[x] += b1[x] - b0[x]
         routes1 = sd.file_checksums_stats()
         for k in legs:
             res[k] = {"GBps": total / float(np.median(runs[k])) / 1e9, "GBps_best": total / min(runs[k]) / 1e9,
@@ -974,6 +982,8 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
         res["library_cpu_path"]["threads"] = 16
         res["policy_default"]["route"] = {k: routes1[k] - routes0[k] for k in routes1}
         res["policy_default"]["hybrid_threads"] = sd.get_tuning("checksum_hybrid_threads")
+        tot = split_bytes["gpu"] + split_bytes["cpu_in_split"]
+        res["policy_default"]["gpu_share"] = split_bytes["gpu"] / tot if tot else None
         res["policy_default_over_cpu_path"] = res["policy_default"]["GBps"] / res["library_cpu_path"]["GBps"]
         res["note"] = ("medians of 3 interleaved rounds after a warm one; policy_default splits this call between "
                        "the GPU route (hybrid_threads readers) and the CPU path (DESIGN.md §4.1)")
@@ -1063,9 +1073,11 @@ def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int
            "rank0_leaves_GBps": sc.len / (leaves_ms * 1e-3) / 1e9 if sc.len else None,
            "transport": "rccl" if comm is not None else ("none (N=1)" if world == 1 else
                                                          f"{dist.get_backend()} via host (rehearsal)"),
-           "note": "one file over all ranks: per-rank block CVs, the CV slots gathered in rank order (in-place "
-                   "ncclAllGather inside sd_split_checksum_mgpu over RCCL), reduce on every rank; wall time with "
-                   "barriers, max over ranks"}
+           "note": "one file over all ranks: per-rank block CVs, the CV slots gathered in rank order ("
+                   + ("in-place ncclAllGather inside sd_split_checksum_mgpu over RCCL" if comm is not None else
+                      "no gather at N = 1" if world == 1 else
+                      "through host memory over the process group: a rehearsal transport, not RCCL")
+                   + "), reduce on every rank; wall time with barriers, max over ranks"}
     h = out32.clone() if comm is not None else out32.cpu()
     if DIST:  # every rank must hold the same hash
         allh = [torch.zeros_like(h) for _ in range(world)]
@@ -1448,11 +1460,12 @@ def main():
             cbm.run(d_data, d_msum, stream)
             mx_ms = ev_ms(lambda: cbm.run(d_data, d_msum, stream), stream, reps=args.checksum_steps)
             mroof = valu_roof(cbm.compressions, mx_ms)
-            # one mixed file (the first: it spans two generated files) against the oracle
-            # hashing the same bytes, copied to the host
-            host = d_data[m_offs[0]:m_offs[0] + m_lens[0]].cpu().numpy()
-            mbad = int(native.checksum_mt(host, m_lens[0], nthreads=oracle_threads()) !=
-                       d_msum[:32].cpu().numpy().tobytes())
+            # one mixed file (the shortest: each spans parts of two generated files) against
+            # the oracle hashing the same bytes, copied to the host
+            mi = int(np.argmin(m_lens))
+            host = d_data[m_offs[mi]:m_offs[mi] + m_lens[mi]].cpu().numpy()
+            mbad = int(native.checksum_mt(host, m_lens[mi], nthreads=oracle_threads()) !=
+                       d_msum[32 * mi:32 * mi + 32].cpu().numpy().tobytes())
             del host
             out["checksum"]["mixed"] = {
                 "workload": f"configs[3] mixed: {len(m_lens)} files of 2..8 GiB, unaligned lengths, "
@@ -1460,8 +1473,8 @@ def main():
                 "files": len(m_lens), "bytes": cbm.total_bytes, "ms_per_run": mx_ms,
                 "GBps": cbm.total_bytes / (mx_ms * 1e-3) / 1e9, "frac": mroof["frac"],
                 "frac_full_rate": mroof["frac_full_rate"],
-                "parity": parity(1, mbad, f"mixed file 0 ({m_lens[0]} B) vs the C oracle's chunk-parallel BLAKE3 of "
-                                          "the same bytes")}
+                "parity": parity(1, mbad, f"mixed file {mi} ({m_lens[mi]} B, the shortest) vs the C oracle's "
+                                          "chunk-parallel BLAKE3 of the same bytes")}
             del cbm, d_msum
         del d_data, cb
         torch.cuda.empty_cache()

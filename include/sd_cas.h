@@ -244,6 +244,9 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
  * to the GPU; "checksum_cpu_max" 0 = the GPU route alone for every call. */
 int sd_file_checksums_stats(sd_cas_ctx* ctx, uint64_t out[2]);  /* calls: [0] CPU path, [1] GPU */
 int sd_file_checksums_routes(sd_cas_ctx* ctx, uint64_t out[3]); /* [0] CPU path, [1] GPU, [2] split */
+/* bytes (stat lengths) of the files [0] the GPU route hashed (GPU-only and split calls) and
+ * [1] the CPU path hashed inside split calls: the split's share on this host */
+int sd_file_checksums_bytes(sd_cas_ctx* ctx, uint64_t out[2]);
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65,
                       int32_t* status);
 

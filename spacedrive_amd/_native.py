@@ -122,6 +122,7 @@ SIGNATURES = [
     ("sd_cas_get_tuning", I32, [ctypes.c_char_p, ctypes.POINTER(I32)]),
     ("sd_file_checksums_stats", I32, [P, P]),
     ("sd_file_checksums_routes", I32, [P, P]),
+    ("sd_file_checksums_bytes", I32, [P, P]),
     ("sd_cas_ids_stats", I32, [P, P]),
     ("sd_read_probe", I32, [P, P, U64, I32, P]),
     ("sd_host_cpu_budget", I32, [P]),

@@ -152,6 +152,13 @@ def file_checksums_stats(device: Optional[int] = None) -> dict:
     return {"cpu": int(v[0]), "gpu": int(v[1]), "hybrid": int(v[2])}
 
 
+def file_checksums_bytes(device: Optional[int] = None) -> dict:
+    """sd_file_checksums_bytes: file bytes the GPU route hashed, and the CPU path inside split calls."""
+    v = np.zeros(2, np.uint64)
+    check(lib().sd_file_checksums_bytes(default_context(device).handle, _ptr(v)))
+    return {"gpu": int(v[0]), "cpu_in_split": int(v[1])}
+
+
 def set_tuning(key: str, value: int) -> None:
     """sd_cas_set_tuning (process-wide knobs, include/sd_cas.h)."""
     check(lib().sd_cas_set_tuning(key.encode(), int(value)))

@@ -206,6 +206,9 @@ struct sd_cas_ctx {
     std::atomic<uint64_t> files_calls_cpu{0}, files_calls_gpu{0};  // sd_cas_ids_files routes
     std::atomic<uint64_t> checksum_calls_cpu{0}, checksum_calls_gpu{0},  // sd_file_checksums routes
         checksum_calls_hybrid{0};
+    // bytes (stat lengths) of the files sd_file_checksums gave the GPU route, and the CPU path
+    // in split calls
+    std::atomic<uint64_t> checksum_bytes_gpu{0}, checksum_bytes_cpu_split{0};
     std::atomic<uint64_t> cas_ids_gpu_files{0}, cas_ids_host_files{0};  // sd_cas_ids: who hashed
     std::mutex pool_mu;
     // Reader threads.  stage_pool: tasks that open and close their own files (the cas

@@ -560,6 +560,15 @@ int sd_file_checksums_routes(sd_cas_ctx* ctx, uint64_t out[3]) {
     SD_GUARD_END
 }
 
+int sd_file_checksums_bytes(sd_cas_ctx* ctx, uint64_t out[2]) {
+    SD_GUARD_BEGIN
+    if (!ctx || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    out[0] = ctx->checksum_bytes_gpu.load(std::memory_order_relaxed);
+    out[1] = ctx->checksum_bytes_cpu_split.load(std::memory_order_relaxed);
+    return SD_OK;
+    SD_GUARD_END
+}
+
 // ---------------------------------------------------------------------- checksums
 int sd_checksum_batch_create(sd_cas_ctx* ctx, const uint64_t* offsets, const uint64_t* lens, size_t n,
                              sd_checksum_batch** out) {

@@ -790,7 +790,12 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
                     std::vector<const char*> p(rest.size());
                     std::vector<char> hex(rest.size() * 65);
                     std::vector<int32_t> st(rest.size());
-                    for (size_t q = 0; q < rest.size(); q++) p[q] = paths[rest[q]];
+                    uint64_t rest_bytes = 0;
+                    for (size_t q = 0; q < rest.size(); q++) {
+                        p[q] = paths[rest[q]];
+                        rest_bytes += hint[rest[q]];
+                    }
+                    ctx->checksum_bytes_cpu_split.fetch_add(rest_bytes, std::memory_order_relaxed);
                     cpu_rc = sd_cpu_file_checksums(p.data(), rest.size(), hex.data(), st.data(), cpu_threads);
                     if (cpu_rc != SD_OK) {
                         cpu_err = sd_cas_last_error();
@@ -819,6 +824,7 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
                         bytes += hint[i];
                     }
                     if (grp.empty()) break;
+                    ctx->checksum_bytes_cpu_split.fetch_add(bytes, std::memory_order_relaxed);
                     gp.resize(grp.size());
                     ghex.resize(grp.size() * 65);
                     gst.resize(grp.size());
@@ -841,7 +847,11 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
               }
             });
             try {
-                gpu_file_checksums(ctx, paths, out_hex65, status, hyb, hint, regular, next_big);
+                gpu_file_checksums(ctx, paths, out_hex65, status, hyb, hint, regular, [&]() -> size_t {
+                    const size_t i = next_big();
+                    if (i != SIZE_MAX) ctx->checksum_bytes_gpu.fetch_add(hint[i], std::memory_order_relaxed);
+                    return i;
+                });
             } catch (...) {
                 cursor.store(big.size());  // the CPU thread takes no further file
                 cpu.join();
@@ -859,6 +869,9 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
     ctx->checksum_calls_gpu.fetch_add(1, std::memory_order_relaxed);
     if (hint.size() != n) stat_files(*ctx->stage_pool(threads), paths, n, hint, regular);
     size_t i = 0;
+    uint64_t all = 0;
+    for (size_t q = 0; q < n; q++) all += hint[q];
+    ctx->checksum_bytes_gpu.fetch_add(all, std::memory_order_relaxed);
     gpu_file_checksums(ctx, paths, out_hex65, status, threads, hint, regular,
                        [&]() -> size_t { return i < n ? i++ : SIZE_MAX; });
     return SD_OK;
