@@ -24,7 +24,9 @@
 // Build (on the CPU container; runs on the GPU box):
 //   hipcc -O2 -std=c++17 -mavx2 -o scripts/ck_host_cost scripts/ck_host_cost.cpp \
 //         -Lspacedrive_amd -lsdcas -Wl,-rpath,'$ORIGIN/../spacedrive_amd' -lpthread
-// Run: scripts/ck_host_cost [NF=32] [FL_MiB=256] [ghz=2.4]  -> JSON lines on stdout
+// Run: scripts/ck_host_cost [NF=32] [FL_MiB=256] [ghz=2.4] [quick]  -> JSON lines on stdout
+// ("quick": read_hash, read_hot_nt_dma and the hot_nt split at 16 threads only, for A/Bs
+// such as scripts/numa_probe.sh's thread placements)
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
@@ -257,6 +259,7 @@ int main(int argc, char** argv) {
     if (argc > 1) NF = atoi(argv[1]);
     if (argc > 2) FL = (uint64_t)atoi(argv[2]) * MiB;
     if (argc > 3) GHZ = atof(argv[3]);
+    const bool quick = argc > 4 && strcmp(argv[4], "quick") == 0;
     if (FL % UNIT) FL = (FL / UNIT + 1) * UNIT;
     make_files();
     const int TMAX = 16;
@@ -274,6 +277,18 @@ int main(int argc, char** argv) {
     }
     // page cache warm (the files were just written) -- one untimed pass anyway
     run(std::vector<int>(TMAX, READ_HOT), std::vector<int>(TMAX, 0), bufs);
+    if (quick) {
+        for (int rep = 0; rep < 3; rep++) {
+            report("read_hash", TMAX, 0, run(std::vector<int>(TMAX, READ_HASH), std::vector<int>(TMAX, 0), bufs));
+            report("read_hot_nt_dma", 8, 8, run(std::vector<int>(8, READ_HOT_NT), std::vector<int>(8, 1), bufs));
+            std::vector<int> kinds(TMAX, READ_HASH), dma(TMAX, 0);
+            for (int t = 0; t < 4; t++) kinds[t] = READ_HOT_NT, dma[t] = 1;
+            report("hybrid_hot_nt", TMAX, 4, run(kinds, dma, bufs));
+        }
+        for (int f = 0; f < NF; f++) unlink(path_of(f).c_str());
+        rmdir(DIR.c_str());
+        return 0;
+    }
     for (int T : {1, 4, 8, 16})
         for (int kind : {READ_PINNED, READ_HOT_NT, READ_HASH, READ_HOT, HASH_HOT})
             report(NAMES[kind], T, 0, run(std::vector<int>(T, kind), std::vector<int>(T, 0), bufs));
