@@ -602,11 +602,35 @@ def checksum_host(ctx, gib: int, dev, stream):
     from oracle import native
     bad = sum(native.checksum_synth_mt(flen, 20_000 + i, 0, nthreads=oracle_threads()).hex() != got[i]
               for i in range(nf))
+    # the same bytes as ONE range: shared by the GPU and the host threads block by block
+    one_off = np.zeros(1, np.uint64)
+    one_len = np.array([total], np.uint64)
+    one = {}
+    for mode, h in (("gpu_only", 0), ("default", keep)):
+        sd.set_tuning("host_cohash_threads", h)
+        try:
+            runs = []
+            for _ in range(3):
+                ctypes.memset(out, 0, 65)
+                t0 = time.perf_counter()
+                check(lib().sd_checksums(ctx.handle, host.data_ptr(), one_off.ctypes.data, one_len.ctypes.data, 1, out))
+                runs.append(time.perf_counter() - t0)
+        finally:
+            sd.set_tuning("host_cohash_threads", keep)
+        one[mode] = (min(runs), out.raw[:64].decode())
+    one_want = native.checksum_mt(host.numpy(), total, nthreads=oracle_threads()).hex()
+    one_bad = sum(v[1] != one_want for v in one.values())
     par = parity(nf, bad, "every file's 64-hex checksum vs the C oracle's chunk-parallel BLAKE3 of the same content")
     return {"files": nf, "bytes": total, "h2d_ms": h2d_ms, "h2d_GBps": total / (h2d_ms * 1e-3) / 1e9, "parity": par,
             "kernel_ms": kernel_ms, "kernel_GBps": total / (kernel_ms * 1e-3) / 1e9,
             "end_to_end_ms": e2e_s * 1e3, "end_to_end_GBps": total / e2e_s / 1e9, "host_cohash_threads": keep,
             "gpu_only": {"end_to_end_ms": e2e["gpu_only"] * 1e3, "end_to_end_GBps": total / e2e["gpu_only"] / 1e9},
+            "one_range": {"bytes": total, "end_to_end_GBps": total / one["default"][0] / 1e9,
+                          "gpu_only_GBps": total / one["gpu_only"][0] / 1e9,
+                          "parity": parity(2, one_bad, "the one range's checksum (default and GPU only) vs the C "
+                                                       "oracle's chunk-parallel BLAKE3 of the same bytes"),
+                          "note": "the same bytes as one range: its 1 MiB blocks shared between the GPU (windows "
+                                  "from the front) and the host threads (from the back), best of 3"},
             "note": f"sd_checksums over {nf} x 1 GiB of pinned host memory (best of 3): 256 MiB windows, H2D on one "
                     "copy queue overlapping the kernels on two slot streams, with the library default of "
                     "host_cohash_threads host threads hashing ranges from the end meanwhile (gpu_only: 0); "

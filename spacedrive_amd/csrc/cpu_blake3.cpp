@@ -523,6 +523,20 @@ int sd_cpu_cas_id_path(const char* path, uint64_t size, char* out_hex17, int32_t
     SD_GUARD_END
 }
 
+}  // extern "C"
+
+void cpu_block_cvs(const uint8_t* msg, uint64_t total_len, uint64_t b0, uint64_t b1, uint8_t* cvs, int nthreads) {
+    parallel_for(b1 - b0, nthreads, [&](size_t k) {
+        const uint64_t b = b0 + k;
+        const uint64_t len = std::min<uint64_t>(SD_CK_BLOCK, total_len - b * SD_CK_BLOCK);
+        CpuHasher h(b * (SD_CK_BLOCK / 1024));
+        h.update(msg + b * SD_CK_BLOCK, len);
+        h.finalize_cv(cvs + 32 * b);
+    });
+}
+
+extern "C" {
+
 int sd_cpu_split_leaves(const uint8_t* slice, uint64_t total_len, int nranks, int rank, uint8_t* cvs,
                         int nthreads) {
     SD_GUARD_BEGIN

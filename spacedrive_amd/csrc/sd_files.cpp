@@ -946,12 +946,27 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     // 64 MiB -- and hashes them with h pool threads on the CPU path (a range of 8 MiB or
     // more block-parallel: its 1 MiB blocks' chaining values on all threads, then the root),
     // while the loop below claims its windows and streamed ranges from the front.
+    // A range of >= 1 GiB is shared at block granularity instead of claimed whole (a call of
+    // one huge range would otherwise go to whichever side claims it first): the first such
+    // range the host thread reaches from the end becomes `sh`; the GPU loop claims its 1 MiB
+    // blocks a window at a time from the front, the host 64 blocks at a time from the back,
+    // into a host CV table; where they meet, the GPU loop uploads the host's CVs next to its
+    // own and runs the reduce passes.
     // (never more host threads than the process's host budget, less one for this thread)
     const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS), host_cpu_budget() - 1}));
     uint64_t all_bytes = 0;
     for (size_t q = 0; q < n; q++) all_bytes += lens[q];
     std::mutex claim_mu;
     size_t back = n, front = 0;  // [back, n) claimed by the host, [0, front) by the GPU loop
+    constexpr uint64_t SHARED_MIN = 1ull << 30, HOST_UNIT = 64;  // bytes; blocks per host claim
+    struct SharedRange {
+        bool used = false;     // one shared range per call
+        size_t idx = SIZE_MAX;  // the range
+        uint64_t nb = 0, sf = 0, sb = 0;  // its blocks: [0, sf) the GPU's, [sb, nb) the host's
+        int inflight = 0;      // host claims being hashed
+        std::vector<uint8_t> cvs;  // the host's block CVs, 32 B at 32 * block
+        std::condition_variable cv;
+    } sh;
     int host_rc = SD_OK;
     std::string host_err;
     std::thread host;
@@ -959,24 +974,61 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         std::thread& t;
         std::mutex& mu;
         size_t& back;
+        SharedRange& sh;
         ~JoinHost() {
             {
                 std::lock_guard<std::mutex> g(mu);
                 back = 0;
+                sh.sb = sh.sf;  // the host takes no further block
             }
             if (t.joinable()) t.join();
         }
-    } join_host{host, claim_mu, back};
+    } join_host{host, claim_mu, back, sh};
     if (cohash > 0 && n && all_bytes >= (1ull << 30)) {
         host = std::thread([&] {
             try {
                 std::vector<uint8_t> h32, cvs;
                 for (;;) {
                     size_t b0, b1;
+                    uint64_t u0 = 0, u1 = 0;  // a claim of the shared range's blocks
+                    {
+                        std::lock_guard<std::mutex> g(claim_mu);
+                        if (sh.idx != SIZE_MAX && sh.sb > sh.sf) {
+                            u1 = sh.sb;
+                            u0 = std::max(sh.sf, u1 > HOST_UNIT ? u1 - HOST_UNIT : 0);
+                            sh.sb = u0;
+                            sh.inflight++;
+                        }
+                    }
+                    if (u1 > u0) {
+                        struct Done {  // on every exit, so the GPU loop's wait ends
+                            SharedRange& s;
+                            std::mutex& mu;
+                            ~Done() {
+                                {
+                                    std::lock_guard<std::mutex> g(mu);
+                                    s.inflight--;
+                                }
+                                s.cv.notify_all();
+                            }
+                        } done{sh, claim_mu};
+                        cpu_block_cvs(data + offsets[sh.idx], lens[sh.idx], u0, u1, sh.cvs.data(), cohash);
+                        continue;
+                    }
                     {
                         std::lock_guard<std::mutex> g(claim_mu);
                         if (back <= front) return;
                         b1 = back;
+                        if (!sh.used && lens[b1 - 1] >= SHARED_MIN) {  // share it, block by block
+                            sh.used = true;
+                            sh.idx = b1 - 1;
+                            sh.nb = (lens[b1 - 1] + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
+                            sh.sf = 0;
+                            sh.sb = sh.nb;
+                            sh.cvs.resize(sh.nb * 32);
+                            back = b1 - 1;  // not the host's whole: the GPU loop may still claim it
+                            continue;
+                        }
                         b0 = b1 - 1;
                         uint64_t sum = lens[b0];
                         while (b0 > front && lens[b0] < SD_CPU_SPLIT_MIN && lens[b0 - 1] < SD_CPU_SPLIT_MIN &&
@@ -1012,12 +1064,54 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     // the GPU loop's claims: range i is the GPU's if no host thread took it
     auto claim = [&](size_t i) -> bool {
         std::lock_guard<std::mutex> g(claim_mu);
-        if (i >= back) return false;
+        if (i >= back && i != sh.idx) return false;
         front = std::max(front, i + 1);
         return true;
     };
     for (size_t i = 0; i < n;) {
         if (!claim(i)) break;
+        if (i == sh.idx) {  // the shared range: windows of blocks from the front until the host's
+            harvest(0);
+            harvest(1);
+            const uint64_t off0 = 0, L = lens[i];
+            plan_checksum_batch(&big, &off0, &L, 1, nullptr);
+            constexpr uint64_t BPW = W / SD_CK_BLOCK;
+            for (;;) {
+                uint64_t w0, w1;
+                {
+                    std::lock_guard<std::mutex> g(claim_mu);
+                    if (sh.sf >= sh.sb) break;
+                    w0 = sh.sf;
+                    w1 = std::min(sh.sb, w0 + BPW);
+                    sh.sf = w1;
+                }
+                const int k = cur;
+                cur ^= 1;
+                const uint64_t pos = w0 * SD_CK_BLOCK, here = std::min(w1 * SD_CK_BLOCK, L) - pos;
+                copy_in(k, data + offsets[i] + pos, here);
+                HIP_CHECK(sdk::launch_ck_leaf(slots[k].staged.as<uint8_t>(), pos, 0, big.d_files(),
+                                              big.d_map() + w0, (uint32_t)(w1 - w0), big.lvl[0].as<uint32_t>(),
+                                              slots[k].hashes.as<uint32_t>(), slots[k].stream));
+                done_with(k);
+            }
+            uint64_t hb0;
+            {
+                std::unique_lock<std::mutex> lk(claim_mu);
+                sh.cv.wait(lk, [&] { return sh.inflight == 0; });  // the host's claims are hashed
+                hb0 = sh.sb;
+            }
+            slots.sync_all();
+            Slot& sl = slots[0];
+            if (hb0 < sh.nb)  // the host's block CVs beside the GPU's, then the reduce passes
+                HIP_CHECK(hipMemcpyAsync(big.lvl[0].as<uint8_t>() + 32 * hb0, sh.cvs.data() + 32 * hb0,
+                                         32 * (sh.nb - hb0), hipMemcpyHostToDevice, sl.stream));
+            run_checksum_reduce(&big, sl.hashes.as<uint32_t>(), sl.stream);
+            HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, 32, hipMemcpyDeviceToHost, sl.stream));
+            HIP_CHECK(hipStreamSynchronize(sl.stream));
+            to_hex(sl.host_hashes.u8(), 32, out_hex65 + 65 * i);
+            i++;
+            continue;
+        }
         if (lens[i] + 128 > W) {  // one large range, streamed
             harvest(0);
             harvest(1);

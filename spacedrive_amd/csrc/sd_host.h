@@ -358,6 +358,9 @@ private:
 void cpu_blake3(const uint8_t* p, size_t n, uint8_t out[32]);
 // BLAKE3 root of a message from its nb >= 2 consecutive 1 MiB block CVs (32 B each)
 void cpu_root_from_cvs(const uint8_t* cvs, uint64_t nb, uint8_t out[32]);
+// the (non-root) chaining values of 1 MiB blocks [b0, b1) of a message of total_len >= 2
+// blocks, on nthreads threads: block b's 32 bytes at cvs + 32 * b
+void cpu_block_cvs(const uint8_t* msg, uint64_t total_len, uint64_t b0, uint64_t b1, uint8_t* cvs, int nthreads);
 // lanes of the SIMD chunk hasher this CPU runs (16, 8 or 1)
 int cpu_lanes();
 // generate_cas_id / file_checksum of one file on the calling thread -> sd_file_status

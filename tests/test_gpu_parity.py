@@ -1091,6 +1091,46 @@ def test_checksums_from_host_memory_cohashed(ctx, oracle_native, cohash):
         assert raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), (i, lens[i])
 
 
+@pytest.mark.parametrize("cohash", [0, 15])
+def test_checksums_one_huge_range_shared(ctx, oracle_native, cohash):
+    """sd_checksums with a range of >= 1 GiB: with host co-hashing its 1 MiB blocks are shared
+    -- the GPU takes windows from the front, the host 64-block claims from the back, the
+    host's chaining values are uploaded beside the GPU's and one reduce gives the hash --;
+    alone, and among small ranges before and after it, with a second huge range (claimed
+    whole by one side).  Every hash equals the oracle's."""
+    import ctypes
+    import spacedrive_amd as sd
+    from spacedrive_amd._native import check, lib
+    MiB = 1 << 20
+    cases = [[(1 << 30) + 12345],
+             [3000, 5 * MiB + 1, (2 << 30) + 777, 64, (1 << 30) + (1 << 20), 1025]]
+    for lens in cases:
+        offs, off = [], 0
+        for L in lens:
+            offs.append(off)
+            off = (off + L + 127) // 128 * 128
+        d = torch.randint(0, 256, (off + 64,), dtype=torch.uint8, device="cuda")
+        host = torch.empty(off + 64, dtype=torch.uint8, pin_memory=True)
+        host.copy_(d)
+        del d
+        arr_o = np.array(offs, np.uint64)
+        arr_l = np.array(lens, np.uint64)
+        out = ctypes.create_string_buffer(65 * len(lens))
+        keep = sd.get_tuning("host_cohash_threads")
+        sd.set_tuning("host_cohash_threads", cohash)
+        try:
+            check(lib().sd_checksums(ctx.handle, host.data_ptr(), arr_o.ctypes.data, arr_l.ctypes.data, len(lens),
+                                     out))
+        finally:
+            sd.set_tuning("host_cohash_threads", keep)
+        hn = host.numpy()
+        raw = out.raw
+        for i, (o, L) in enumerate(zip(offs, lens)):
+            want = oracle_native.checksum_mt(hn[o:o + L], L, nthreads=NT).hex()
+            assert raw[65 * i:65 * i + 64].decode() == want, (lens, i, L)
+        del host
+
+
 def test_checksums_host_ranges_any_layout(ctx, oracle_native):
     """sd_checksums over host ranges laid out every way a caller may: 16-byte starts (leaf-
     sized ranges then start a new copy run on a 128-B device line), gaps,
