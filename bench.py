@@ -1367,7 +1367,8 @@ def main():
         "distributed": {"dist_initialized": DIST, "backend": dist.get_backend() if DIST else None, "world": world,
                         "force_dist": bool(args.force_dist), "dedup_transport": transport,
                         "rccl_libs": rccl_libs() if transport == "rccl" or args.dist_backend == "nccl" else None},
-        "host_threads": dict(_native.host_cpu_budget(), cohash_threads=min(sd.get_tuning("host_cohash_threads"),
+        "host_threads": dict(_native.host_cpu_budget(), numa=_native.host_numa(),
+                             cohash_threads=min(sd.get_tuning("host_cohash_threads"),
                                                                          _native.host_cpu_budget()["budget"] - 1),
                              read_threads=min(sd.get_tuning("read_threads"), _native.host_cpu_budget()["budget"]),
                              note="the library's host thread budget (sd_host_cpu_budget): min(affinity, cgroup quota) "

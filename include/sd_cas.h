@@ -109,6 +109,11 @@ int sd_cas_abi_version(void);
  * "host_cpu_budget" > 0 replaces it.  out[5]: [0] the budget, [1] affinity CPUs, [2] cgroup
  * quota in milli-CPUs (0 = none), [3] LOCAL_WORLD_SIZE, [4] 1 if the tuning key set it. */
 int sd_host_cpu_budget(int out[5]);
+/* Where the library's own threads run: out[0] = 1 when they are placed on the CPUs of the
+ * NUMA node of the first context's device (within the affinity mask; tuning "numa_pin",
+ * default 1), out[1] = those CPUs, out[2] = the device's node (-1 unknown).  Callers'
+ * threads are never moved. */
+int sd_host_numa(int out[3]);
 /* last error message of the calling thread ("" if none) */
 const char* sd_cas_last_error(void);
 int sd_cas_ctx_create(int device, sd_cas_ctx** out);

@@ -126,6 +126,7 @@ SIGNATURES = [
     ("sd_cas_ids_stats", I32, [P, P]),
     ("sd_read_probe", I32, [P, P, U64, I32, P]),
     ("sd_host_cpu_budget", I32, [P]),
+    ("sd_host_numa", I32, [P]),
     ("sd_comm_rccl_info", I32, [ctypes.POINTER(I32), ctypes.c_char_p, SZ]),
 ]
 
@@ -136,6 +137,13 @@ def host_cpu_budget() -> dict:
     check(lib().sd_host_cpu_budget(out))
     return {"budget": out[0], "affinity": out[1], "cgroup_quota_cpus": out[2] / 1000.0 if out[2] else None,
             "local_world_size": out[3], "overridden": bool(out[4])}
+
+
+def host_numa() -> dict:
+    """Where the library's own threads run (sd_host_numa)."""
+    out = (ctypes.c_int * 3)()
+    check(lib().sd_host_numa(out))
+    return {"placed": bool(out[0]), "cpus": out[1], "device_node": out[2]}
 
 
 def rccl_info() -> dict:

@@ -10,6 +10,7 @@
 // build); everything else is the library's own code.  Prints "host_selftest: ok" or the
 // failed checks and exits non-zero.
 #include <dirent.h>
+#include <sched.h>
 #include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -526,6 +527,49 @@ void test_cpu_budget() {
     CHECK(memcmp(h3, h1, 96) == 0);
 }
 
+// NUMA placement: a preferred CPU list moves the pools' worker threads onto it (within the
+// affinity mask) at their next run, "numa_pin" 0 moves them back, and the caller's own
+// thread is never moved
+void test_numa_placement() {
+    cpu_set_t all;
+    CPU_ZERO(&all);
+    CHECK(sched_getaffinity(0, sizeof all, &all) == 0);
+    if (CPU_COUNT(&all) < 2) return;  // nothing to prefer on one CPU
+    int first = -1;
+    for (int c = 0; c < CPU_SETSIZE && first < 0; c++)
+        if (CPU_ISSET(c, &all)) first = c;
+    CHECK(numa_prefer_cpus("") == 0);                 // an empty list prefers nothing
+    CHECK(numa_prefer_cpus("100000-100001") == 0);    // nor CPUs outside the mask
+    const std::string one = std::to_string(first) + "-" + std::to_string(first) + ",100000\n";
+    CHECK(numa_prefer_cpus(one.c_str()) == 1);
+    int ncpu = 0, node = 0;
+    CHECK(numa_placement(&ncpu, &node) == 1 && ncpu == 1);
+    StagePool pool(4);
+    auto workers_on = [&](int want_count) {
+        std::mutex mu;
+        std::vector<int> counts;
+        pool.run(64, [&](size_t) {
+            cpu_set_t s;
+            CPU_ZERO(&s);
+            sched_getaffinity(0, sizeof s, &s);
+            std::lock_guard<std::mutex> g(mu);
+            counts.push_back(CPU_COUNT(&s));
+        });
+        cpu_set_t me;
+        CPU_ZERO(&me);
+        sched_getaffinity(0, sizeof me, &me);
+        CHECK(CPU_COUNT(&me) == CPU_COUNT(&all));  // the caller runs tasks too and stays where it was
+        bool any = false;
+        for (int c : counts) any |= c == want_count;
+        return any;
+    };
+    CHECK(workers_on(1));  // some task ran on a placed worker
+    CHECK(sd_cas_set_tuning("numa_pin", 0) == SD_OK);
+    CHECK(numa_placement(nullptr, nullptr) == 0);
+    CHECK(!workers_on(1));  // every thread back on the whole mask
+    CHECK(sd_cas_set_tuning("numa_pin", 1) == SD_OK);
+}
+
 // ------------------------------------------------------------------ coalescer
 void test_coalescer() {
     std::vector<std::string> names;
@@ -715,6 +759,7 @@ int main() {
     test_exchange_plan();
     test_comm_group();
     test_private_fd_tables();
+    test_numa_placement();  // last: it moves the pools' threads
     // clean up the scratch directory
     if (DIR* d = opendir(g_dir.c_str())) {
         while (dirent* e = readdir(d))

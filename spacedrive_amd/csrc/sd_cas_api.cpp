@@ -11,6 +11,7 @@
 // This file: the context, staging and device batches, the latency path, dedup, synthetic
 // data and device utilities; the file-reading pipelines and the streaming hash are in
 // sd_files.cpp, the types both share in sd_api_impl.h.
+#include <ctype.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
@@ -229,6 +230,16 @@ int sd_cas_ctx_create(int device, sd_cas_ctx** out) {
     auto c = std::make_unique<sd_cas_ctx>();
     c->device = device;
     c->bind();
+    {  // the library's threads go to the device's NUMA node (sd_host.h, "numa_pin")
+        char bdf[64] = {0};
+        if (hipDeviceGetPCIBusId(bdf, sizeof bdf, device) == hipSuccess) {
+            for (char* q = bdf; *q; q++) *q = (char)tolower(*q);
+            const int node = pci_numa_node(bdf);
+            numa_note_node(node);
+            const std::string cpus = numa_node_cpulist(node);
+            if (!cpus.empty()) numa_prefer_cpus(cpus.c_str());
+        }
+    }
     HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     *out = c.release();
     return SD_OK;
@@ -427,6 +438,7 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
         window = 128ull << 20;
         for (int t = 0; t < cohash; t++)
             hosts.emplace_back([&] {
+                library_thread_place();  // the device's NUMA node (sd_host.h)
                 for (;;) {
                     size_t a, b;
                     {

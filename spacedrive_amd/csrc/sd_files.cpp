@@ -785,6 +785,7 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
             int cpu_rc = SD_OK;
             std::string cpu_err;
             std::thread cpu([&] {
+              library_thread_place();  // the device's NUMA node (sd_host.h)
               try {
                 if (!rest.empty()) {  // the small and non-regular files: one CPU-path call
                     std::vector<const char*> p(rest.size());
@@ -986,6 +987,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     } join_host{host, claim_mu, back, sh};
     if (cohash > 0 && n && all_bytes >= (1ull << 30)) {
         host = std::thread([&] {
+            library_thread_place();  // the device's NUMA node (sd_host.h)
             try {
                 std::vector<uint8_t> h32, cvs;
                 for (;;) {
@@ -1069,7 +1071,20 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         return true;
     };
     for (size_t i = 0; i < n;) {
-        if (!claim(i)) break;
+        if (!claim(i)) {
+            // the host took range i and everything after it -- except the shared range,
+            // which may lie beyond ranges the host claimed whole after sharing it
+            size_t s;
+            {
+                std::lock_guard<std::mutex> g(claim_mu);
+                s = sh.idx;
+            }
+            if (s != SIZE_MAX && s > i) {
+                i = s;
+                continue;
+            }
+            break;
+        }
         if (i == sh.idx) {  // the shared range: windows of blocks from the front until the host's
             harvest(0);
             harvest(1);

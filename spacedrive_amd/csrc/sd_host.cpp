@@ -41,13 +41,13 @@ thread_local std::string g_err;
 // from the page cache); no host thread budget override; 15 host threads hashing beside the GPU in
 // large sd_cas_ids calls (profiles/r3/r3ad_cohash_probe.json: 300 000 files from pinned memory,
 // GPU alone 1.89-1.94 M files/s, CPU path alone 2.24-2.36 M, both at once 3.87-4.08 M)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {4}, {15}, {0}, {1}};
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {4}, {15}, {0}, {1}, {1}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
                                                "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",
                                                "files_ring",         "checksum_cpu_max", "files_stage_hot",
                                                "checksum_hybrid_threads", "host_cohash_threads",
-                                               "host_cpu_budget",    "checksum_stage_hot"};
+                                               "host_cpu_budget",    "checksum_stage_hot", "numa_pin"};
 
 bool read_small(const std::string& path, char* buf, size_t cap) {
     FILE* f = fopen(path.c_str(), "re");
@@ -113,6 +113,86 @@ CpuBudget host_cpu_budget_detail() {
 
 int host_cpu_budget() { return host_cpu_budget_detail().budget; }
 
+// ------------------------------------------------------------------ NUMA placement
+namespace {
+std::mutex g_numa_mu;
+cpu_set_t g_numa_set, g_numa_all;  // the preferred CPUs; the process's mask when they were set
+int g_numa_count = 0;             // CPUs in g_numa_set (0 = no preference)
+int g_numa_node = -1;             // the node they belong to
+std::atomic<int> g_numa_gen{0};   // bumped when the preference changes
+thread_local int t_numa_gen = 0;  // the generation this thread applied
+}  // namespace
+
+int numa_prefer_cpus(const char* list) {
+    cpu_set_t allowed, want;
+    CPU_ZERO(&allowed);
+    CPU_ZERO(&want);
+    if (!list || sched_getaffinity(0, sizeof allowed, &allowed) != 0) return 0;
+    for (const char* p = list; *p;) {  // "a-b,c,d-e"
+        char* end;
+        const long a = strtol(p, &end, 10);
+        if (end == p) break;
+        long b = a;
+        p = end;
+        if (*p == '-') {
+            b = strtol(p + 1, &end, 10);
+            p = end;
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; c++)
+            if (c >= 0 && CPU_ISSET(c, &allowed)) CPU_SET(c, &want);
+        while (*p == ',' || *p == '\n' || *p == ' ') p++;
+    }
+    const int n = CPU_COUNT(&want);
+    // nothing of the node is ours, or all of our CPUs are on it: nothing to prefer
+    if (n == 0 || n == CPU_COUNT(&allowed)) return 0;
+    std::lock_guard<std::mutex> g(g_numa_mu);
+    if (g_numa_count) return g_numa_count;  // the first context's node stays
+    g_numa_set = want;
+    g_numa_all = allowed;
+    g_numa_count = n;
+    g_numa_gen.fetch_add(1);
+    return n;
+}
+
+void numa_note_node(int node) {
+    std::lock_guard<std::mutex> g(g_numa_mu);
+    if (g_numa_node < 0) g_numa_node = node;
+}
+
+int pci_numa_node(const char* bdf) {
+    char buf[32];
+    if (!bdf || !read_small(std::string("/sys/bus/pci/devices/") + bdf + "/numa_node", buf, sizeof buf)) return -1;
+    return atoi(buf);
+}
+
+std::string numa_node_cpulist(int node) {
+    char buf[1024];
+    if (node < 0 || !read_small("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist", buf, sizeof buf))
+        return "";
+    return buf;
+}
+
+int numa_placement(int* ncpus, int* node) {
+    std::lock_guard<std::mutex> g(g_numa_mu);
+    if (ncpus) *ncpus = g_numa_count;
+    if (node) *node = g_numa_node;
+    return g_numa_count > 0 && tuning_get(SD_TUNE_NUMA_PIN) != 0;
+}
+
+void library_thread_place() {
+    const int gen = g_numa_gen.load(std::memory_order_acquire);
+    if (gen == t_numa_gen) return;
+    t_numa_gen = gen;
+    cpu_set_t s;
+    {
+        std::lock_guard<std::mutex> g(g_numa_mu);
+        if (!g_numa_count) return;
+        // "numa_pin" 0 after threads were placed: back onto every CPU the process had
+        s = tuning_get(SD_TUNE_NUMA_PIN) != 0 ? g_numa_set : g_numa_all;
+    }
+    (void)sched_setaffinity(0, sizeof s, &s);  // best effort: a refused mask leaves the thread as it was
+}
+
 void sd_set_err(const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -172,6 +252,14 @@ ExchangePlan exchange_plan(const uint64_t* rows, int R, int me) {
 extern "C" {
 const char* sd_cas_last_error(void) { return g_err.c_str(); }
 int sd_cas_abi_version(void) { return SD_CAS_ABI_VERSION; }
+int sd_host_numa(int out[3]) {
+    SD_GUARD_BEGIN
+    if (!out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    out[0] = numa_placement(&out[1], &out[2]);
+    return SD_OK;
+    SD_GUARD_END
+}
+
 int sd_host_cpu_budget(int out[5]) {
     SD_GUARD_BEGIN
     if (!out) throw sd_failure(SD_ERR_INVALID, "null argument");
@@ -223,6 +311,7 @@ int sd_cas_set_tuning(const char* key, int value) {
     for (int k = 0; k < SD_TUNE_NKEYS; k++)
         if (strcmp(key, TUNE_NAMES[k]) == 0) {
             g_tune[k].store(value, std::memory_order_relaxed);
+            if (k == SD_TUNE_NUMA_PIN) g_numa_gen.fetch_add(1);  // threads re-place at their next run
             return SD_OK;
         }
     throw sd_failure(SD_ERR_INVALID, std::string("unknown tuning key ") + key);

@@ -65,7 +65,8 @@ enum sd_tune_key {
     SD_TUNE_HOST_COHASH_THREADS = 13,      // sd_cas_ids: host threads hashing beside the GPU (large calls)
     SD_TUNE_HOST_CPU_BUDGET = 14,          // cap on the host threads one call starts (0 = resolve it)
     SD_TUNE_CHECKSUM_STAGE_HOT = 15,       // sd_file_checksums' GPU route: pread_stream into the windows
-    SD_TUNE_NKEYS = 16
+    SD_TUNE_NUMA_PIN = 16,                 // library threads on the GPU's NUMA node (0 = float)
+    SD_TUNE_NKEYS = 17
 };
 int tuning_get(int key);
 
@@ -94,6 +95,23 @@ inline int cap_host_threads(int n) {
     const int b = host_cpu_budget();
     return n < 1 ? 1 : (n > b ? b : n);
 }
+
+// ------------------------------------------------------------------ NUMA placement
+// The library's own threads (pool workers, co-hashing threads) run on the CPUs of the GPU's
+// NUMA node, within the process's affinity mask: their page-cache reads, pinned windows and
+// DMA stay on the socket the device hangs off (scripts/numa_probe.sh: the CPU path 90 vs 77
+// GB/s and the split checksum 106 vs 100 GB/s against the same threads left to float over
+// both sockets of the box).  `node_cpulist` is the node's sysfs cpulist ("0-63,128-191");
+// the first context sets the preference, "numa_pin" 0 turns it off.  Returns the CPUs kept.
+int numa_prefer_cpus(const char* node_cpulist);
+// the node of a PCI device ("0000:23:00.0") from sysfs, or -1
+int pci_numa_node(const char* bdf);
+// the sysfs cpulist of a NUMA node ("" when absent)
+std::string numa_node_cpulist(int node);
+// 1 when library threads are placed on a preferred CPU set; the set's CPU count in *ncpus,
+// the first context's device node in *node (-1 unknown)
+int numa_placement(int* ncpus, int* node);
+void numa_note_node(int node);
 
 // latency path (coalesce.cpp): single-file calls, CPU route or coalesced GPU batches
 struct sd_coalescer;

@@ -22,6 +22,11 @@
 // (scripts/stage_bench.c mode 5).  Tasks on such a pool must open and
 // close their own files: a descriptor opened by another thread is not valid there.
 void private_fd_table();
+// Places the calling library thread on the process's preferred CPUs (the GPU's NUMA node,
+// set when a context is created; sd_host.h numa_prefer_device_cpus) if they changed since
+// this thread last applied them.  Worker threads call it before each run's tasks; a pool's
+// caller thread is never moved.
+void library_thread_place();
 
 class StagePool {
 public:
@@ -99,6 +104,7 @@ private:
             seen = gen_;
             const bool take = idx < active_;
             g.unlock();
+            library_thread_place();
             if (take) drain();
             g.lock();
             if (--busy_ == 0) done_.notify_all();
