@@ -63,6 +63,8 @@ extern "C" {
     pub fn sd_cas_last_error() -> *const c_char;
     // the host thread budget every call is capped by; "host_cpu_budget" sets it
     pub fn sd_host_cpu_budget(out: *mut c_int) -> c_int;
+    // where the library's own threads run (the device's NUMA node; tuning "numa_pin")
+    pub fn sd_host_numa(out: *mut c_int) -> c_int;
     pub fn sd_cas_set_tuning(key: *const c_char, value: c_int) -> c_int;
     pub fn sd_cas_ctx_create(device: c_int, out: *mut *mut sd_cas_ctx) -> c_int;
     pub fn sd_cas_ctx_destroy(ctx: *mut sd_cas_ctx);
@@ -79,6 +81,8 @@ extern "C" {
                                  status: *mut i32) -> c_int;
     pub fn sd_checksums(ctx: *mut sd_cas_ctx, data: *const u8, offsets: *const u64, lens: *const u64, n: usize,
                         out_hex65: *mut c_char) -> c_int;
+    // the validator's split: bytes the GPU route and the CPU path hashed
+    pub fn sd_file_checksums_bytes(ctx: *mut sd_cas_ctx, out: *mut u64) -> c_int;
     // the CPU path (no device)
     pub fn sd_cpu_simd_lanes() -> c_int;
     pub fn sd_cpu_cas_ids_files(paths: *const *const c_char, sizes: *const u64, n: usize, out_hex17: *mut c_char,
