@@ -312,3 +312,18 @@ def test_host_cpu_budget_divides_by_local_world_size():
     if b["cgroup_quota_cpus"]:
         cpus = min(cpus, max(1, math.ceil(b["cgroup_quota_cpus"] - 1e-9)))
     assert b["local_world_size"] == 4 and b["budget"] == max(1, cpus // 4)
+
+
+def test_host_numa_without_a_context_places_nothing():
+    """The library's threads are placed on a device's NUMA node only once a context exists
+    (sd_cas_ctx_create reads the node); the CPU path alone leaves them where they are, and
+    "numa_pin" is an ordinary tuning key."""
+    import spacedrive_amd as sd
+    from spacedrive_amd._native import host_numa
+    if os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK):
+        pytest.skip("GPU present: a context may exist")
+    assert host_numa() == {"placed": False, "cpus": 0, "device_node": -1}
+    keep = sd.get_tuning("numa_pin")
+    assert keep == 1
+    sd.set_tuning("numa_pin", 0)
+    sd.set_tuning("numa_pin", keep)
