@@ -111,8 +111,8 @@ int sd_cas_abi_version(void);
 int sd_host_cpu_budget(int out[5]);
 /* Where the library's own threads run: out[0] = 1 when they are placed on the CPUs of the
  * NUMA node of the first context's device (within the affinity mask; tuning "numa_pin",
- * default 1), out[1] = those CPUs, out[2] = the device's node (-1 unknown).  Callers'
- * threads are never moved. */
+ * default 0 = not placed), out[1] = those CPUs, out[2] = the device's node (-1 unknown).
+ * Callers' threads are never moved. */
 int sd_host_numa(int out[3]);
 /* last error message of the calling thread ("" if none) */
 const char* sd_cas_last_error(void);

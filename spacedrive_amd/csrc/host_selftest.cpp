@@ -542,6 +542,8 @@ void test_numa_placement() {
     CHECK(numa_prefer_cpus("100000-100001") == 0);    // nor CPUs outside the mask
     const std::string one = std::to_string(first) + "-" + std::to_string(first) + ",100000\n";
     CHECK(numa_prefer_cpus(one.c_str()) == 1);
+    CHECK(numa_placement(nullptr, nullptr) == 0);  // opt-in: nothing placed yet
+    CHECK(sd_cas_set_tuning("numa_pin", 1) == SD_OK);
     int ncpu = 0, node = 0;
     CHECK(numa_placement(&ncpu, &node) == 1 && ncpu == 1);
     StagePool pool(4);
@@ -567,7 +569,6 @@ void test_numa_placement() {
     CHECK(sd_cas_set_tuning("numa_pin", 0) == SD_OK);
     CHECK(numa_placement(nullptr, nullptr) == 0);
     CHECK(!workers_on(1));  // every thread back on the whole mask
-    CHECK(sd_cas_set_tuning("numa_pin", 1) == SD_OK);
 }
 
 // ------------------------------------------------------------------ coalescer

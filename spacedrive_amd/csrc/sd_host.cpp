@@ -38,10 +38,12 @@ thread_local std::string g_err;
 // 1.04 vs 0.84 M files/s), large sd_file_checksums calls split between the GPU route on 4
 // of the 16 readers and the CPU path on the rest, the GPU route's readers through
 // pread_stream (profiles/r4/r4c_hybrid_checksum_probe.json: 1.13-1.21x the CPU path alone
-// from the page cache); no host thread budget override; 15 host threads hashing beside the GPU in
+// from the page cache); no host thread budget override; library threads left unplaced
+// ("numa_pin" 0: placing them on the GPU's node measured neutral with the page cache where
+// the writer left it, profiles/r4/r4h_numa_lib_probe.json); 15 host threads hashing beside the GPU in
 // large sd_cas_ids calls (profiles/r3/r3ad_cohash_probe.json: 300 000 files from pinned memory,
 // GPU alone 1.89-1.94 M files/s, CPU path alone 2.24-2.36 M, both at once 3.87-4.08 M)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {4}, {15}, {0}, {1}, {1}};
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {4}, {15}, {0}, {1}, {0}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
                                                "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",

@@ -97,12 +97,13 @@ inline int cap_host_threads(int n) {
 }
 
 // ------------------------------------------------------------------ NUMA placement
-// The library's own threads (pool workers, co-hashing threads) run on the CPUs of the GPU's
-// NUMA node, within the process's affinity mask: their page-cache reads, pinned windows and
-// DMA stay on the socket the device hangs off (scripts/numa_probe.sh: the CPU path 90 vs 77
-// GB/s and the split checksum 106 vs 100 GB/s against the same threads left to float over
-// both sockets of the box).  `node_cpulist` is the node's sysfs cpulist ("0-63,128-191");
-// the first context sets the preference, "numa_pin" 0 turns it off.  Returns the CPUs kept.
+// With "numa_pin" 1 (opt-in) the library's own threads (pool workers, co-hashing threads)
+// run on the CPUs of the GPU's NUMA node, within the process's affinity mask.  When the
+// files' page cache was written on that node too, it pays (scripts/numa_probe.sh: the CPU
+// path 90 vs 77 GB/s, the split checksum 106 vs 100 GB/s); with the page cache where an
+// unplaced writer left it -- the usual case -- it measured neutral (0.93-1.04x,
+// scripts/numa_lib_probe.py), so it is off by default.  `node_cpulist` is the node's sysfs
+// cpulist ("0-63,128-191"); the first context sets the preference.  Returns the CPUs kept.
 int numa_prefer_cpus(const char* node_cpulist);
 // the node of a PCI device ("0000:23:00.0") from sysfs, or -1
 int pci_numa_node(const char* bdf);

@@ -324,6 +324,6 @@ def test_host_numa_without_a_context_places_nothing():
         pytest.skip("GPU present: a context may exist")
     assert host_numa() == {"placed": False, "cpus": 0, "device_node": -1}
     keep = sd.get_tuning("numa_pin")
-    assert keep == 1
-    sd.set_tuning("numa_pin", 0)
+    assert keep == 0  # opt-in
+    sd.set_tuning("numa_pin", 1)
     sd.set_tuning("numa_pin", keep)
