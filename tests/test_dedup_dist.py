@@ -49,7 +49,7 @@ def _worker(rank, world, port, n_per, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])  # 8: the driver's node, rehearsed on gloo
 def test_distributed_grouping_equals_single_process(tmp_path, world):
     n_per = 4000
     mp.start_processes(_worker, args=(world, _free_port(), n_per, str(tmp_path)), nprocs=world, join=True,

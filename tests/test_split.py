@@ -88,7 +88,7 @@ def _worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])  # 8: the driver's node, rehearsed on gloo
 def test_checksum_split_over_gloo(tmp_path, world):
     fdata = _data(5 * BLOCK + 999, seed=9)[:5 * BLOCK + 999]
     (tmp_path / "file.bin").write_bytes(fdata.tobytes())
