@@ -971,7 +971,7 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
         total = nf * flen
         res = {"files": nf, "bytes": total, "dir_fs": _fs_type(d)}
         default_cpu_max = sd.get_tuning("checksum_cpu_max")
-        gpu = sd.cpu.file_checksums(paths, nthreads=16)
+        want = sd.cpu.file_checksums(paths, nthreads=16)  # every leg must return these (and the oracle)
 
         def route(cpu_max):
             def f():
@@ -992,7 +992,7 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
                 t0 = time.perf_counter()
                 got = f()
                 dt = time.perf_counter() - t0
-                assert got == gpu, k
+                assert got == want, k
                 if rnd:
                     runs[k].append(dt)
                     if k == "policy_default":
@@ -1012,7 +1012,7 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
         res["note"] = ("medians of 3 interleaved rounds after a warm one; policy_default splits this call between "
                        "the GPU route (hybrid_threads readers) and the CPU path (DESIGN.md §4.1)")
         from oracle import native
-        bad = sum(native.checksum_synth_mt(flen, 30_000 + i, 0, nthreads=oracle_threads()).hex() != gpu[i]
+        bad = sum(native.checksum_synth_mt(flen, 30_000 + i, 0, nthreads=oracle_threads()).hex() != want[i]
                   for i in range(nf))
         res["parity"] = parity(nf, bad, "every file's checksum vs the C oracle's chunk-parallel BLAKE3 of the same "
                                         "content")
@@ -1025,7 +1025,7 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
                 lib_cpu = sd.cpu.file_checksums(paths, nthreads=nt)
                 cpu_runs.append(time.perf_counter() - t0)
             res[key] = {"GBps": total / min(cpu_runs) / 1e9, "threads": nt, "note": "best of 2"}
-            assert lib_cpu == gpu
+            assert lib_cpu == want
         if with_cpu:
             from oracle import native
             cpu = {}
@@ -1035,7 +1035,7 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
                 got, st = native.file_checksums(sub, nthreads=nt, simd=-1)
                 dt = time.perf_counter() - t0
                 cpu[f"threads_{nt}"] = {"GBps": len(sub) * flen / dt / 1e9, "seconds": dt, "files": len(sub)}
-                assert (st == 0).all() and [g.tobytes().hex() for g in got] == gpu[:len(sub)]
+                assert (st == 0).all() and [g.tobytes().hex() for g in got] == want[:len(sub)]
             res["cpu_reference_schedule"] = cpu
         return res
     finally:
