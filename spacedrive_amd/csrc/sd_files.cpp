@@ -948,11 +948,12 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     // more block-parallel: its 1 MiB blocks' chaining values on all threads, then the root),
     // while the loop below claims its windows and streamed ranges from the front.
     // A range of >= 1 GiB is shared at block granularity instead of claimed whole (a call of
-    // one huge range would otherwise go to whichever side claims it first): the first such
-    // range the host thread reaches from the end becomes `sh`; the GPU loop claims its 1 MiB
-    // blocks a window at a time from the front, the host 64 blocks at a time from the back,
-    // into a host CV table; where they meet, the GPU loop uploads the host's CVs next to its
-    // own and runs the reduce passes.
+    // one huge range would otherwise go to whichever side claims it first -- the GPU loop,
+    // which starts before the host thread): the last such range of the call becomes `sh`,
+    // chosen before either side starts; the GPU loop claims its 1 MiB blocks a window at a
+    // time from the front, the host thread 64 blocks at a time from the back into a host CV
+    // table (before it claims anything else); where they meet, the GPU loop uploads the
+    // host's CVs next to its own and runs the reduce passes.
     // (never more host threads than the process's host budget, less one for this thread)
     const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS), host_cpu_budget() - 1}));
     uint64_t all_bytes = 0;
@@ -961,8 +962,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     size_t back = n, front = 0;  // [back, n) claimed by the host, [0, front) by the GPU loop
     constexpr uint64_t SHARED_MIN = 1ull << 30, HOST_UNIT = 64;  // bytes; blocks per host claim
     struct SharedRange {
-        bool used = false;     // one shared range per call
-        size_t idx = SIZE_MAX;  // the range
+        size_t idx = SIZE_MAX;  // the range (one per call)
         uint64_t nb = 0, sf = 0, sb = 0;  // its blocks: [0, sf) the GPU's, [sb, nb) the host's
         int inflight = 0;      // host claims being hashed
         std::vector<uint8_t> cvs;  // the host's block CVs, 32 B at 32 * block
@@ -986,6 +986,15 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         }
     } join_host{host, claim_mu, back, sh};
     if (cohash > 0 && n && all_bytes >= (1ull << 30)) {
+        for (size_t q = n; q-- > 0;)
+            if (lens[q] >= SHARED_MIN) {
+                sh.idx = q;
+                sh.nb = (lens[q] + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
+                sh.sf = 0;
+                sh.sb = sh.nb;
+                sh.cvs.resize(sh.nb * 32);
+                break;
+            }
         host = std::thread([&] {
             library_thread_place();  // the device's NUMA node (sd_host.h)
             try {
@@ -1021,14 +1030,8 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
                         std::lock_guard<std::mutex> g(claim_mu);
                         if (back <= front) return;
                         b1 = back;
-                        if (!sh.used && lens[b1 - 1] >= SHARED_MIN) {  // share it, block by block
-                            sh.used = true;
-                            sh.idx = b1 - 1;
-                            sh.nb = (lens[b1 - 1] + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
-                            sh.sf = 0;
-                            sh.sb = sh.nb;
-                            sh.cvs.resize(sh.nb * 32);
-                            back = b1 - 1;  // not the host's whole: the GPU loop may still claim it
+                        if (b1 - 1 == sh.idx) {  // the shared range: its blocks only, above
+                            back = sh.idx;
                             continue;
                         }
                         b0 = b1 - 1;
