@@ -416,7 +416,41 @@ int sd_cpu_checksums(const uint8_t* data, const uint64_t* offsets, const uint64_
                      int nthreads) {
     SD_GUARD_BEGIN
     if (n && (!data || !offsets || !lens || !out_hash32)) throw sd_failure(SD_ERR_INVALID, "null argument");
-    parallel_for(n, nthreads, [&](size_t i) { cpu_blake3(data + offsets[i], lens[i], out_hash32 + 32 * i); });
+    // a range of 8 MiB or more is hashed block-parallel (as sd_cpu_file_checksums below): its
+    // 1 MiB blocks are tasks of their own beside the small ranges' tasks, and its root is
+    // merged from the block CVs -- else one huge range ran on one thread
+    constexpr uint64_t SPLIT_MIN = 8ull << 20;
+    struct Task {
+        size_t range;
+        uint64_t block;  // UINT64_MAX: the whole range
+    };
+    std::vector<Task> tasks;
+    std::vector<size_t> big;
+    std::vector<std::vector<uint8_t>> cvs;
+    tasks.reserve(n);
+    for (size_t i = 0; i < n; i++) {
+        if (nthreads > 1 && lens[i] >= SPLIT_MIN) {
+            const uint64_t nb = (lens[i] + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
+            for (uint64_t b = 0; b < nb; b++) tasks.push_back({big.size(), b});
+            big.push_back(i);
+            cvs.emplace_back(nb * 32);
+        } else {
+            tasks.push_back({i, UINT64_MAX});
+        }
+    }
+    parallel_for(tasks.size(), nthreads, [&](size_t t) {
+        const Task& k = tasks[t];
+        if (k.block == UINT64_MAX) {
+            cpu_blake3(data + offsets[k.range], lens[k.range], out_hash32 + 32 * k.range);
+            return;
+        }
+        const size_t i = big[k.range];
+        const uint64_t pos = k.block * SD_CK_BLOCK, len = std::min<uint64_t>(SD_CK_BLOCK, lens[i] - pos);
+        CpuHasher h(k.block * (SD_CK_BLOCK / 1024));
+        h.update(data + offsets[i] + pos, len);
+        h.finalize_cv(cvs[k.range].data() + 32 * k.block);
+    });
+    for (size_t q = 0; q < big.size(); q++) cpu_root_from_cvs(cvs[q].data(), cvs[q].size() / 32, out_hash32 + 32 * big[q]);
     return SD_OK;
     SD_GUARD_END
 }

@@ -947,20 +947,26 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     // 64 MiB -- and hashes them with h pool threads on the CPU path (a range of 8 MiB or
     // more block-parallel: its 1 MiB blocks' chaining values on all threads, then the root),
     // while the loop below claims its windows and streamed ranges from the front.
-    // A range of >= 1 GiB is shared at block granularity instead of claimed whole (a call of
-    // one huge range would otherwise go to whichever side claims it first -- the GPU loop,
-    // which starts before the host thread): the last such range of the call becomes `sh`,
-    // chosen before either side starts; the GPU loop claims its 1 MiB blocks a window at a
-    // time from the front, the host thread 64 blocks at a time from the back into a host CV
-    // table (before it claims anything else); where they meet, the GPU loop uploads the
-    // host's CVs next to its own and runs the reduce passes.
+    // One range of >= 256 MiB is shared at block granularity instead of claimed whole, so the
+    // two sides finish together (a whole claim leaves the other side idle for up to one
+    // range's time; a call of one huge range would go to whichever side claims it first):
+    // `sh`, chosen before either side starts, is the range holding the byte where the two
+    // are predicted to meet (the GPU at the H2D rate, the host at h threads' hashing rate),
+    // or the large range nearest it.  Each side claims whole ranges until it reaches `sh`;
+    // there the GPU loop claims its 1 MiB blocks a window at a time from the front, the
+    // host thread 64 blocks at a time from the back into a host CV table; when none is
+    // left, the GPU loop uploads the host's CVs next to its own and runs the reduce passes.
     // (never more host threads than the process's host budget, less one for this thread)
     const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS), host_cpu_budget() - 1}));
     uint64_t all_bytes = 0;
     for (size_t q = 0; q < n; q++) all_bytes += lens[q];
     std::mutex claim_mu;
     size_t back = n, front = 0;  // [back, n) claimed by the host, [0, front) by the GPU loop
-    constexpr uint64_t SHARED_MIN = 1ull << 30, HOST_UNIT = 64;  // bytes; blocks per host claim
+    constexpr uint64_t SHARED_MIN = 256ull << 20, HOST_UNIT = 64;  // bytes; blocks per host claim
+    // the meet prediction's rates: the H2D copy bounds the GPU side, ~5.5 GB/s a host thread
+    // (BLAKE3 with AVX-512, profiles/r4/r4j_shared_range_probe.json); only the split point
+    // depends on them, never a result
+    constexpr double GPU_GBPS = 55.0, HOST_THREAD_GBPS = 5.5;
     struct SharedRange {
         size_t idx = SIZE_MAX;  // the range (one per call)
         uint64_t nb = 0, sf = 0, sb = 0;  // its blocks: [0, sf) the GPU's, [sb, nb) the host's
@@ -986,15 +992,24 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         }
     } join_host{host, claim_mu, back, sh};
     if (cohash > 0 && n && all_bytes >= (1ull << 30)) {
-        for (size_t q = n; q-- > 0;)
-            if (lens[q] >= SHARED_MIN) {
+        const double meet = (double)all_bytes * GPU_GBPS / (GPU_GBPS + HOST_THREAD_GBPS * cohash);
+        double best = 0;
+        uint64_t pos = 0;
+        for (size_t q = 0; q < n; pos += lens[q], q++) {
+            if (lens[q] < SHARED_MIN) continue;
+            const double lo = (double)pos, hi = (double)(pos + lens[q]);
+            const double dist = meet < lo ? lo - meet : meet > hi ? meet - hi : 0;
+            if (sh.idx == SIZE_MAX || dist < best) {
                 sh.idx = q;
-                sh.nb = (lens[q] + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
-                sh.sf = 0;
-                sh.sb = sh.nb;
-                sh.cvs.resize(sh.nb * 32);
-                break;
+                best = dist;
             }
+        }
+        if (sh.idx != SIZE_MAX) {
+            sh.nb = (lens[sh.idx] + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
+            sh.sf = 0;
+            sh.sb = sh.nb;
+            sh.cvs.resize(sh.nb * 32);
+        }
         host = std::thread([&] {
             library_thread_place();  // the device's NUMA node (sd_host.h)
             try {
@@ -1004,7 +1019,8 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
                     uint64_t u0 = 0, u1 = 0;  // a claim of the shared range's blocks
                     {
                         std::lock_guard<std::mutex> g(claim_mu);
-                        if (sh.idx != SIZE_MAX && sh.sb > sh.sf) {
+                        // the shared range's blocks once every range after it is claimed
+                        if (sh.idx != SIZE_MAX && back <= sh.idx + 1 && sh.sb > sh.sf) {
                             u1 = sh.sb;
                             u0 = std::max(sh.sf, u1 > HOST_UNIT ? u1 - HOST_UNIT : 0);
                             sh.sb = u0;
@@ -1034,6 +1050,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
                             back = sh.idx;
                             continue;
                         }
+                        // (the host reaches ranges before `sh` only once its blocks are gone)
                         b0 = b1 - 1;
                         uint64_t sum = lens[b0];
                         while (b0 > front && lens[b0] < SD_CPU_SPLIT_MIN && lens[b0 - 1] < SD_CPU_SPLIT_MIN &&
@@ -1096,11 +1113,17 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
             constexpr uint64_t BPW = W / SD_CK_BLOCK;
             for (;;) {
                 uint64_t w0, w1;
+                // claim at the device's pace, not the enqueue rate (the copies are async from
+                // pinned memory): slot cur's previous window must have been hashed first, so
+                // at most two windows are the GPU's ahead of the host's claims
+                if (used_set[cur]) HIP_CHECK(hipEventSynchronize(used[cur]));
                 {
                     std::lock_guard<std::mutex> g(claim_mu);
                     if (sh.sf >= sh.sb) break;
+                    // windows shrink to a third of what is left (>= 32 blocks), so the
+                    // GPU's last windows in flight are short when the two sides meet
                     w0 = sh.sf;
-                    w1 = std::min(sh.sb, w0 + BPW);
+                    w1 = std::min(sh.sb, w0 + std::min<uint64_t>(BPW, std::max<uint64_t>(32, (sh.sb - w0) / 3)));
                     sh.sf = w1;
                 }
                 const int k = cur;

@@ -72,6 +72,27 @@ def test_cpu_cas_ids_staged_goldens(golden, oracle_native):
     assert got == [f["cas_id"] for f in files]
 
 
+def test_cpu_checksums_block_parallel_ranges(oracle_native):
+    """sd_cpu_checksums splits a range of >= 8 MiB into 1 MiB block tasks beside the small
+    ranges' tasks (one huge range no longer runs on one thread): ranges either side of the
+    split threshold, a ragged tail, an odd offset and an empty range, on 1 and 8 threads,
+    against the oracle's BLAKE3 of each range."""
+    rng = np.random.default_rng(11)
+    lens = [(8 << 20) - 1, 8 << 20, (8 << 20) + 1, 12345, 0, (9 << 20) + 777, 64]
+    offs, o = [], 0
+    for L in lens:
+        offs.append(o)
+        o += L + 3  # odd starts
+    data = rng.integers(0, 256, o + 64, dtype=np.uint8)
+    offs_a, lens_a = np.array(offs, np.uint64), np.array(lens, np.uint64)
+    want = [oracle_native.blake3(data[a:a + L].tobytes()) for a, L in zip(offs, lens)]
+    for nt in (1, 8):
+        out = np.zeros((len(lens), 32), np.uint8)
+        check(lib().sd_cpu_checksums(data.ctypes.data, offs_a.ctypes.data, lens_a.ctypes.data, len(lens),
+                                     out.ctypes.data, nt))
+        assert [r.tobytes() for r in out] == want, nt
+
+
 def _write(tmp_path, name, content):
     p = tmp_path / name
     p.write_bytes(content)
