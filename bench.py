@@ -620,11 +620,25 @@ def checksum_host(ctx, gib: int, dev, stream):
         one[mode] = (min(runs), out.raw[:64].decode())
     one_want = native.checksum_mt(host.numpy(), total, nthreads=oracle_threads()).hex()
     one_bad = sum(v[1] != one_want for v in one.values())
+    # the library's CPU path over the same ranges on the host budget's threads (no device)
+    cpu_t = effective_cpus()
+    h32 = np.zeros((nf, 32), np.uint8)
+    cpu_runs = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        check(lib().sd_cpu_checksums(host.data_ptr(), offs.ctypes.data, lens.ctypes.data, nf, h32.ctypes.data, cpu_t))
+        cpu_runs.append(time.perf_counter() - t0)
+    cpu_bad = sum(h32[i].tobytes().hex() != got[i] for i in range(nf))
     par = parity(nf, bad, "every file's 64-hex checksum vs the C oracle's chunk-parallel BLAKE3 of the same content")
     return {"files": nf, "bytes": total, "h2d_ms": h2d_ms, "h2d_GBps": total / (h2d_ms * 1e-3) / 1e9, "parity": par,
             "kernel_ms": kernel_ms, "kernel_GBps": total / (kernel_ms * 1e-3) / 1e9,
             "end_to_end_ms": e2e_s * 1e3, "end_to_end_GBps": total / e2e_s / 1e9, "host_cohash_threads": keep,
             "gpu_only": {"end_to_end_ms": e2e["gpu_only"] * 1e3, "end_to_end_GBps": total / e2e["gpu_only"] / 1e9},
+            "library_cpu_path": {"threads": cpu_t, "GBps": total / min(cpu_runs) / 1e9,
+                                 "parity": parity(nf, cpu_bad, "sd_cpu_checksums of each range vs sd_checksums' "
+                                                               "oracle-checked output"),
+                                 "note": "sd_cpu_checksums over the same ranges (1 MiB blocks as tasks), best of 3"},
+            "default_over_cpu_path": min(cpu_runs) / e2e_s,
             "one_range": {"bytes": total, "end_to_end_GBps": total / one["default"][0] / 1e9,
                           "gpu_only_GBps": total / one["gpu_only"][0] / 1e9,
                           "parity": parity(2, one_bad, "the one range's checksum (default and GPU only) vs the C "
@@ -633,7 +647,8 @@ def checksum_host(ctx, gib: int, dev, stream):
                                   "from the front) and the host threads (from the back), best of 3"},
             "note": f"sd_checksums over {nf} x 1 GiB of pinned host memory (best of 3): 256 MiB windows, H2D on one "
                     "copy queue overlapping the kernels on two slot streams, with the library default of "
-                    "host_cohash_threads host threads hashing ranges from the end meanwhile (gpu_only: 0); "
+                    "host_cohash_threads host threads hashing ranges from the end meanwhile, one range shared "
+                    "block by block where the two sides meet (gpu_only: 0); "
                     "h2d_ms = one raw copy; kernel_ms = device-resident"}
 
 

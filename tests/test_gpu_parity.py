@@ -1093,17 +1093,22 @@ def test_checksums_from_host_memory_cohashed(ctx, oracle_native, cohash):
 
 @pytest.mark.parametrize("cohash", [0, 15])
 def test_checksums_one_huge_range_shared(ctx, oracle_native, cohash):
-    """sd_checksums with a range of >= 1 GiB: with host co-hashing its 1 MiB blocks are shared
-    -- the GPU takes windows from the front, the host 64-block claims from the back, the
-    host's chaining values are uploaded beside the GPU's and one reduce gives the hash --;
-    alone, and among small ranges before and after it, with a second huge range (claimed
-    whole by one side).  Every hash equals the oracle's."""
+    """sd_checksums with ranges of >= 256 MiB: with host co-hashing the one nearest the
+    predicted meeting point has its 1 MiB blocks shared -- the GPU takes windows from the
+    front, the host 64-block claims from the back, the host's chaining values are uploaded
+    beside the GPU's and one reduce gives the hash; the other ranges are claimed whole.
+    Cases: one huge range alone; huge ranges among small ones before and after; six 300 MiB
+    ranges (the shared one in the middle); and a 2 GiB range first, then four of 64 MiB
+    (the shared range is the GPU's first, the host reaches it last).  Every hash equals
+    the oracle's."""
     import ctypes
     import spacedrive_amd as sd
     from spacedrive_amd._native import check, lib
     MiB = 1 << 20
     cases = [[(1 << 30) + 12345],
-             [3000, 5 * MiB + 1, (2 << 30) + 777, 64, (1 << 30) + (1 << 20), 1025]]
+             [3000, 5 * MiB + 1, (2 << 30) + 777, 64, (1 << 30) + (1 << 20), 1025],
+             [300 * MiB + 17 * i for i in range(6)],
+             [(2 << 30) + 3] + [64 * MiB] * 4]
     for lens in cases:
         offs, off = [], 0
         for L in lens:
