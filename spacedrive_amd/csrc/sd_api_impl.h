@@ -193,6 +193,22 @@ struct Slot {
     PinnedBuf host_hashes, window;
     sd_cas_batch cas;
     sd_checksum_batch ck;
+    hipEvent_t drained = nullptr;  // sync()'s blocking-sync event
+    Slot() = default;
+    Slot(const Slot&) = delete;
+    Slot& operator=(const Slot&) = delete;
+    ~Slot() {
+        if (drained) (void)hipEventDestroy(drained);
+    }
+    // Waits for the stream's queued work with the thread asleep (a blocking-sync event), as
+    // the file stager's waits do: the reader and co-hash threads beside it share the host
+    // budget.  (A/B against hipStreamSynchronize, profiles/r4/r4l_sync_ab/: no difference
+    // beyond the box's noise -- the runtime's own wait already sleeps after a short poll.)
+    void sync() {
+        if (!drained) HIP_CHECK(hipEventCreateWithFlags(&drained, hipEventDisableTiming | hipEventBlockingSync));
+        HIP_CHECK(hipEventRecord(drained, stream));
+        HIP_CHECK(hipEventSynchronize(drained));
+    }
 };
 
 }  // namespace sdi
@@ -283,8 +299,8 @@ struct SlotPair {
     }
     Slot& operator[](int k) { return *s[k]; }
     void sync_all() {
-        HIP_CHECK(hipStreamSynchronize(s[0]->stream));
-        HIP_CHECK(hipStreamSynchronize(s[1]->stream));
+        s[0]->sync();
+        s[1]->sync();
     }
 };
 

@@ -397,7 +397,7 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
     Win wins[2];
     auto harvest = [&](int k) {
         if (!wins[k].busy) return;
-        HIP_CHECK(hipStreamSynchronize(slots[k].stream));
+        slots[k].sync();
         const uint8_t* h = slots[k].host_hashes.u8();
         for (size_t q = wins[k].gi; q < wins[k].gj; q++) {
             to_hex(h + (q - wins[k].gi) * 32, 8, out_hex17 + live[q] * 17);  // cas.rs:61 to_hex()[..16]

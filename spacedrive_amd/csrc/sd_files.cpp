@@ -92,7 +92,7 @@ struct Streamer {
         rtag[k].clear();
     }
     void sync_collect(SlotPair& sl, int k) {
-        HIP_CHECK(hipStreamSynchronize(sl[k].stream));
+        sl[k].sync();
         collect(k);
     }
     void finish(SlotPair& sl) {
@@ -610,7 +610,7 @@ void gpu_file_checksums(sd_cas_ctx* ctx, const char* const* paths, char* out_hex
     Streamer streamer([&](size_t i, const uint8_t* h) { to_hex(h, 32, out_hex65 + i * 65); });  // hash.rs:21-23
     int cur = 0;
     auto harvest = [&](int k) {  // slot k idle: its window is free, its results delivered
-        HIP_CHECK(hipStreamSynchronize(slots[k].stream));
+        slots[k].sync();
         streamer.collect(k);
         if (!pend[k].busy) return;
         const uint8_t* h = slots[k].host_hashes.u8();
@@ -900,7 +900,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     } pend[2];
     auto harvest = [&](int k) {
         if (!pend[k].busy) return;
-        HIP_CHECK(hipStreamSynchronize(slots[k].stream));
+        slots[k].sync();
         const uint8_t* h = slots[k].host_hashes.u8();
         for (size_t i = pend[k].i0; i < pend[k].i1; i++) to_hex(h + 32 * (i - pend[k].i0), 32, out_hex65 + 65 * i);
         pend[k].busy = false;
@@ -920,7 +920,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     } ev_guard{{copied, used}};
     for (int k = 0; k < 2; k++) {
         HIP_CHECK(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&used[k], hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&used[k], hipEventDisableTiming | hipEventBlockingSync));
     }
     // H2D of `bytes` from `src` to byte `dst` of slot k's device window, after its previous
     // kernels (first piece of a window) / before its next kernels (last piece)
@@ -1148,7 +1148,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
                                          32 * (sh.nb - hb0), hipMemcpyHostToDevice, sl.stream));
             run_checksum_reduce(&big, sl.hashes.as<uint32_t>(), sl.stream);
             HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, 32, hipMemcpyDeviceToHost, sl.stream));
-            HIP_CHECK(hipStreamSynchronize(sl.stream));
+            sl.sync();
             to_hex(sl.host_hashes.u8(), 32, out_hex65 + 65 * i);
             i++;
             continue;
@@ -1176,7 +1176,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
             Slot& sl = slots[0];
             run_checksum_reduce(&big, sl.hashes.as<uint32_t>(), sl.stream);
             HIP_CHECK(hipMemcpyAsync(sl.host_hashes.p, sl.hashes.p, 32, hipMemcpyDeviceToHost, sl.stream));
-            HIP_CHECK(hipStreamSynchronize(sl.stream));
+            sl.sync();
             to_hex(sl.host_hashes.u8(), 32, out_hex65 + 65 * i);
             i++;
             continue;
