@@ -228,7 +228,8 @@ int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
  * ranges stream; two windows alternate so the H2D copies overlap the kernels.  In calls of
  * >= 1 GiB, "host_cohash_threads" host threads (default 15; 0 = GPU only) hash ranges from
  * the end on the CPU path meanwhile (ranges of >= 8 MiB block-parallel), the GPU taking
- * them from the front until the two meet. */
+ * them from the front until the two meet; one range of >= 256 MiB, the one nearest the
+ * predicted meeting point, is shared 1 MiB block by block. */
 int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
                  char* out_hex65);
 /* Drop-in: checksums of n files on disk -> 65-byte lowercase hex each (hash.rs:21-23);
@@ -243,7 +244,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
  * between that GPU route (on g of the 16 "read_threads"; fewer under a smaller host budget)
  * and sd_cpu_file_checksums (the rest of the threads), running at once: the large files go
  * to whichever route is free next, the small ones to the CPU path -- from the page cache
- * 1.13-1.21x the CPU path alone.  Any other call of at most "checksum_cpu_max" files is
+ * 1.04-1.21x the CPU path alone, by box.  Any other call of at most "checksum_cpu_max" files is
  * hashed by sd_cpu_file_checksums on "read_threads" threads -- by default every such call,
  * because from the page cache the host's threads hash faster than PCIe can carry the bytes
  * to the GPU; "checksum_cpu_max" 0 = the GPU route alone for every call. */
@@ -286,7 +287,8 @@ int sd_cpu_cas_ids(const uint8_t* staged, uint64_t staged_bytes, const sd_extent
 /* sd_cas_ids_files on the host: (path, size) pairs -> cas_ids; status[n] required */
 int sd_cpu_cas_ids_files(const char* const* paths, const uint64_t* sizes, size_t n, char* out_hex17,
                          int32_t* status, int nthreads);
-/* full BLAKE3 of n byte ranges of one host buffer -> 32 raw bytes each */
+/* full BLAKE3 of n byte ranges of one host buffer -> 32 raw bytes each (the 1 MiB blocks
+ * of a range of >= 8 MiB are tasks of their own when nthreads > 1) */
 int sd_cpu_checksums(const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
                      uint8_t* out_hash32, int nthreads);
 /* sd_file_checksums on the host: paths -> 65-byte hex; status[n] required */
