@@ -25,6 +25,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -551,6 +552,9 @@ void test_numa_placement() {
         std::mutex mu;
         std::vector<int> counts;
         pool.run(64, [&](size_t) {
+            // each task takes a while, so the workers take some of them even where they are
+            // slow to wake (under TSan the caller could run all 64 alone)
+            std::this_thread::sleep_for(std::chrono::microseconds(500));
             cpu_set_t s;
             CPU_ZERO(&s);
             sched_getaffinity(0, sizeof s, &s);
@@ -742,6 +746,26 @@ void test_exchange_plan() {
         }
 }
 
+// sd_checksums' shared range: the range nearest the predicted meeting byte, among the
+// ranges of >= 256 MiB
+void test_shared_range_pick() {
+    const uint64_t M = 1ull << 20, G = 1ull << 30, MIN = 256 * M;
+    auto pick = [&](std::vector<uint64_t> l, int h) { return shared_range_pick(l.data(), l.size(), MIN, h, 55.0, 5.5); };
+    CHECK(pick({4 * G}, 15) == 0);                                   // one range: it
+    CHECK(pick({G, G, G, G}, 15) == 1);                              // meet at 40%: the second
+    CHECK(pick({G, G, G, G}, 1) == 3);                               // one host thread: meet at 91%
+    CHECK(pick({G, G, G, G}, 0) == 3);                               // no host threads: the end
+    CHECK(pick({2 * G + 3, 64 * M, 64 * M, 64 * M, 64 * M}, 15) == 0);  // the GPU's first
+    CHECK(pick({64 * M, 100 * M, 200 * M}, 15) == SIZE_MAX);          // none long enough
+    CHECK(pick({}, 15) == SIZE_MAX);
+    // meet at 40% of 3372 MiB = 1349 MiB: inside the third range (it starts at 1324 MiB)
+    CHECK(pick({G, 300 * M, 2 * G}, 15) == 2);
+    CHECK(pick({300 * M, 4 * G, 300 * M}, 15) == 1);
+    // equally near (meet exactly between two large ranges): the first
+    std::vector<uint64_t> two{G, G};
+    CHECK(shared_range_pick(two.data(), 2, MIN, 10, 55.0, 5.5) == 0);
+}
+
 int main() {
     char tmpl[] = "/tmp/sd_selftest_XXXXXX";
     if (!mkdtemp(tmpl)) return 2;
@@ -758,6 +782,7 @@ int main() {
     test_cpu_budget();
     test_coalescer();
     test_exchange_plan();
+    test_shared_range_pick();
     test_comm_group();
     test_private_fd_tables();
     test_numa_placement();  // last: it moves the pools' threads

@@ -992,18 +992,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
         }
     } join_host{host, claim_mu, back, sh};
     if (cohash > 0 && n && all_bytes >= (1ull << 30)) {
-        const double meet = (double)all_bytes * GPU_GBPS / (GPU_GBPS + HOST_THREAD_GBPS * cohash);
-        double best = 0;
-        uint64_t pos = 0;
-        for (size_t q = 0; q < n; pos += lens[q], q++) {
-            if (lens[q] < SHARED_MIN) continue;
-            const double lo = (double)pos, hi = (double)(pos + lens[q]);
-            const double dist = meet < lo ? lo - meet : meet > hi ? meet - hi : 0;
-            if (sh.idx == SIZE_MAX || dist < best) {
-                sh.idx = q;
-                best = dist;
-            }
-        }
+        sh.idx = shared_range_pick(lens, n, SHARED_MIN, cohash, GPU_GBPS, HOST_THREAD_GBPS);
         if (sh.idx != SIZE_MAX) {
             sh.nb = (lens[sh.idx] + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
             sh.sf = 0;

@@ -795,3 +795,22 @@ uint64_t MsgSource::read_parallel(uint8_t* dst, uint64_t n) {
     file_pos_ += got;
     return got;
 }
+
+size_t shared_range_pick(const uint64_t* lens, size_t n, uint64_t min_len, int host_threads, double gpu_gbps,
+                         double thread_gbps) {
+    double all = 0;
+    for (size_t q = 0; q < n; q++) all += (double)lens[q];
+    const double meet = all * gpu_gbps / (gpu_gbps + thread_gbps * std::max(0, host_threads));
+    size_t pick = SIZE_MAX;
+    double best = 0, pos = 0;
+    for (size_t q = 0; q < n; pos += (double)lens[q], q++) {
+        if (lens[q] < min_len) continue;
+        const double lo = pos, hi = pos + (double)lens[q];
+        const double dist = meet < lo ? lo - meet : meet > hi ? meet - hi : 0;
+        if (pick == SIZE_MAX || dist < best) {
+            pick = q;
+            best = dist;
+        }
+    }
+    return pick;
+}

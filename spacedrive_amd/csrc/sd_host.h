@@ -380,6 +380,12 @@ void cpu_root_from_cvs(const uint8_t* cvs, uint64_t nb, uint8_t out[32]);
 // the (non-root) chaining values of 1 MiB blocks [b0, b1) of a message of total_len >= 2
 // blocks, on nthreads threads: block b's 32 bytes at cvs + 32 * b
 void cpu_block_cvs(const uint8_t* msg, uint64_t total_len, uint64_t b0, uint64_t b1, uint8_t* cvs, int nthreads);
+// sd_checksums' co-hashing: the index of the range of >= min_len bytes
+// nearest the byte where the GPU (gpu_gbps, from the front) and host_threads host threads
+// (thread_gbps each, from the back) are predicted to meet; the first of equally near ones;
+// SIZE_MAX if no range is that long
+size_t shared_range_pick(const uint64_t* lens, size_t n, uint64_t min_len, int host_threads, double gpu_gbps,
+                         double thread_gbps);
 // lanes of the SIMD chunk hasher this CPU runs (16, 8 or 1)
 int cpu_lanes();
 // generate_cas_id / file_checksum of one file on the calling thread -> sd_file_status
