@@ -528,6 +528,20 @@ def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1, lib_=None):
         w8 = oracle_hashes(*lib_, idx)[:, :8]
         par = parity(len(idx), int((got[idx] != w8).any(axis=1).sum()),
                      "cas_ids of an even-stride sample (+ the first 32) vs the C oracle on the same generator")
+    cpu_row = None
+    if not DIST:  # the library's CPU path over the same messages (one process: no other rank's load)
+        from spacedrive_amd._native import host_cpu_budget
+        nt = min(16, host_cpu_budget()["budget"])
+        cout = ctypes.create_string_buffer(17 * k)
+        runs = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            check(lib().sd_cpu_cas_ids(host.data_ptr(), nbytes, sub.ctypes.data, k, cout, None, nt))
+            runs.append(time.perf_counter() - t0)
+        assert cout.raw == raw, "sd_cpu_cas_ids differs from sd_cas_ids"
+        cpu_row = {"files_per_s": k / min(runs[1:]), "threads": nt,
+                   "default_over_cpu_path": min(runs[1:]) / e2e_s,
+                   "note": "sd_cpu_cas_ids over the same pinned messages, best of 2 after a warm run"}
     res = {"files": k, "bytes": nbytes, "h2d_ms": h2d_ms, "h2d_GBps": nbytes / (h2d_ms * 1e-3) / 1e9,
            "kernel_ms": kernel_ms, "kernel_files_per_s": k / (kernel_ms * 1e-3),
            "end_to_end_ms": e2e_s * 1e3, "end_to_end_files_per_s": k / e2e_s,
@@ -537,6 +551,7 @@ def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1, lib_=None):
                         "end_to_end_files_per_s": k / e2e["gpu_only"][0],
                         "end_to_end_GBps": nbytes / e2e["gpu_only"][0] / 1e9},
            "parity": par,
+           "library_cpu_path": cpu_row,
            "note": "sd_cas_ids from pinned host memory (mean of 2 calls after a warm one, all ranks at once): "
                    "plan + H2D + kernels + D2H + hex, 512 MiB windows on two streams, with the library default "
                    "of host_cohash_threads host threads hashing files from the end of the list meanwhile "
