@@ -358,7 +358,9 @@ int sd_comm_create_local(sd_cas_ctx* ctx, sd_comm_group* group, int rank, sd_com
  * SD_ERR_CAPACITY before the record exchange, with *m_out = its own requirement (and
  * SD_ERR_INTERNAL together if any rank's partition counts disagree with its valid records:
  * the gathered rows carry both, so no rank is left waiting in the exchange).  Runs on
- * `stream`; returns after the group counts are known (host sync). */
+ * `stream`; returns after the group counts are known (host sync).  Overlapping it with the
+ * next batch's hashing (a second stream) pays only with the hashing stream at the higher
+ * priority (107.5 vs 103.9-104.3 M files/s with equal priorities). */
 int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, const uint8_t* d_valid, uint64_t n,
                       uint64_t global_index_base, uint64_t chunk_size, uint64_t* d_records_out, uint64_t* d_rep_out,
                       uint64_t* d_owner_out, uint64_t capacity, uint64_t* m_out, uint64_t* n_groups_out,
