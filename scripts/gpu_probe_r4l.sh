@@ -1,7 +1,8 @@
 #!/bin/bash
 # round 4: slot waits asleep (blocking-sync events) vs polling (SD_AB_SPIN=1), in separate
 # processes, alternated twice: the co-hashed in-memory checksums, the split file checksums,
-# and the co-hashed sd_cas_ids
+# and the co-hashed sd_cas_ids.  SD_AB_SPIN was a temporary switch in sd_api_impl.h, removed
+# once this A/B (profiles/r4/r4l_sync_ab/) showed no difference; the script records how it ran
 set -u
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
