@@ -93,6 +93,30 @@ def test_cpu_checksums_block_parallel_ranges(oracle_native):
         assert [r.tobytes() for r in out] == want, nt
 
 
+def test_cpu_paths_of_a_directory(tmp_path):
+    """A directory given as a file: File::open succeeds on Linux and the first read fails
+    with EISDIR, so generate_cas_id (whole or sampled size) and file_checksum return that
+    io::Error (cas.rs:29,36; hash.rs:16): SD_FILE_IO_ERROR with errno 21, on either side of a
+    regular file hashed as usual."""
+    import errno
+    content = bytes(i % 251 for i in range(200_000))
+    (tmp_path / "sub").mkdir()
+    (tmp_path / "f").write_bytes(content)
+    paths = [str(tmp_path / "sub"), str(tmp_path / "f"), str(tmp_path / "sub")]
+    sizes = np.array([4096, 200_000, 200_000], np.uint64)
+    arr = (ctypes.c_char_p * 3)(*[os.fsencode(p) for p in paths])
+    want = {"cas": cs.generate_cas_id_file(content, 200_000), "checksum": cs.file_checksum(content)}
+    for name, call, width in (
+            ("cas", lambda o, st: lib().sd_cpu_cas_ids_files(arr, sizes.ctypes.data, 3, o, st.ctypes.data, 2), 17),
+            ("checksum", lambda o, st: lib().sd_cpu_file_checksums(arr, 3, o, st.ctypes.data, 2), 65)):
+        out = ctypes.create_string_buffer(width * 3)
+        st = np.zeros(3, np.int32)
+        check(call(out, st))
+        assert [(int(x) & 0xFFFF, int(x) >> 16) for x in st] == [
+            (2, errno.EISDIR), (SD_FILE_OK, 0), (2, errno.EISDIR)], name
+        assert out.raw[width:2 * width - 1].decode() == want[name], name
+
+
 def _write(tmp_path, name, content):
     p = tmp_path / name
     p.write_bytes(content)

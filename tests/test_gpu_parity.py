@@ -939,6 +939,36 @@ def test_batch_policy_routes_small_calls_to_the_cpu_path(ctx, tmp_path):
     assert s2["gpu"] - s1["gpu"] == 1 and s2["cpu"] == s1["cpu"]
 
 
+def test_directory_paths_fail_like_the_reference(ctx, tmp_path, oracle_native):
+    """Directories among the files of a GPU-route call: File::open succeeds on Linux and the
+    first read fails with EISDIR (cas.rs:29,36; hash.rs:16), so each directory gets
+    OSError(EISDIR) -- with a whole-kind and a sampled-kind size, and in a checksum call
+    beside packed small files and a streamed large one -- while every regular file's result
+    equals the oracle's."""
+    import errno
+    import spacedrive_amd as sd
+    (tmp_path / "d1").mkdir()
+    (tmp_path / "d2").mkdir()
+    sizes = [3000, 150_000, 9 << 20, 1]
+    files = []
+    for i, n in enumerate(sizes):
+        p = tmp_path / f"r{i}"
+        p.write_bytes(cs.synth_bytes(900 + i, 0, 0, n))
+        files.append(str(p))
+    paths = [str(tmp_path / "d1"), files[0], str(tmp_path / "d2"), files[1], files[2], str(tmp_path / "d1"), files[3]]
+    cas_sizes = [4096, 3000, 200_000, 150_000, 9 << 20, 102_400, 1]
+    got = sd.generate_cas_ids(paths, cas_sizes)
+    got_ck = sd.file_checksums(paths)
+    for j, p in enumerate(paths):
+        if p in files:
+            content = open(p, "rb").read()
+            assert got[j] == cs.generate_cas_id_file(content, cas_sizes[j]), j
+            assert got_ck[j] == oracle_native.blake3(content).hex(), j
+        else:
+            for r in (got[j], got_ck[j]):
+                assert isinstance(r, OSError) and r.errno == errno.EISDIR, (j, r)
+
+
 def test_dedup_mgpu_through_rccl_single_rank(ctx, rccl_comm):
     """sd_cas_dedup_mgpu through a real RCCL communicator (1 rank: the
     all-gather and the grouped send/recv to self run; no world == 1 short-circuit) equals
