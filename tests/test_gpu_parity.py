@@ -969,6 +969,37 @@ def test_directory_paths_fail_like_the_reference(ctx, tmp_path, oracle_native):
                 assert isinstance(r, OSError) and r.errno == errno.EISDIR, (j, r)
 
 
+def test_symlinks_and_unreadable_files(ctx, tmp_path, oracle_native):
+    """File::open follows symlinks: a link to a regular file hashes as the file, a dangling
+    link fails with ENOENT; a file without read permission fails with EACCES (checked only
+    when not running as root, who may read it anyway).  GPU routes, one call each."""
+    import errno
+    import spacedrive_amd as sd
+    content = cs.synth_bytes(950, 0, 0, 250_000)
+    real = tmp_path / "real"
+    real.write_bytes(content)
+    (tmp_path / "link").symlink_to(real)
+    (tmp_path / "dangling").symlink_to(tmp_path / "nowhere")
+    locked = tmp_path / "locked"
+    locked.write_bytes(content)
+    locked.chmod(0)
+    paths = [str(tmp_path / "link"), str(tmp_path / "dangling"), str(locked), str(real)]
+    try:
+        ids = sd.generate_cas_ids(paths, [250_000] * 4)
+        cks = sd.file_checksums(paths)
+    finally:
+        locked.chmod(0o644)
+    want_id, want_ck = cs.generate_cas_id_file(content, 250_000), oracle_native.blake3(content).hex()
+    for r in (ids, cks):
+        w = want_id if r is ids else want_ck
+        assert r[0] == w and r[3] == w
+        assert isinstance(r[1], OSError) and r[1].errno == errno.ENOENT
+        if os.geteuid() != 0:
+            assert isinstance(r[2], OSError) and r[2].errno == errno.EACCES
+        else:
+            assert r[2] == w
+
+
 def test_dedup_mgpu_through_rccl_single_rank(ctx, rccl_comm):
     """sd_cas_dedup_mgpu through a real RCCL communicator (1 rank: the
     all-gather and the grouped send/recv to self run; no world == 1 short-circuit) equals
