@@ -36,6 +36,12 @@ void cpu_hash_chunks_x4(const uint8_t* const* in, int n, uint64_t ctr0, uint32_t
 void cpu_hash_parents_x16(const uint32_t (*cvs)[8], int n, uint32_t (*out)[8]);
 void cpu_hash_parents_x8(const uint32_t (*cvs)[8], int n, uint32_t (*out)[8]);
 void cpu_hash_parents_x4(const uint32_t (*cvs)[8], int n, uint32_t (*out)[8]);
+void cpu_hash_chunks_var_x16(const uint8_t* const* in, const uint32_t* len, const uint64_t* ctr, const uint8_t* root,
+                             int n, uint32_t (*cv)[8]);
+void cpu_hash_chunks_var_x8(const uint8_t* const* in, const uint32_t* len, const uint64_t* ctr, const uint8_t* root,
+                            int n, uint32_t (*cv)[8]);
+void cpu_hash_chunks_var_x4(const uint8_t* const* in, const uint32_t* len, const uint64_t* ctr, const uint8_t* root,
+                            int n, uint32_t (*cv)[8]);
 
 namespace {
 
@@ -103,19 +109,23 @@ void chunk_cv(const uint8_t* p, uint32_t len, uint64_t counter, bool root, uint3
 
 using chunks_fn = void (*)(const uint8_t* const*, int, uint64_t, uint32_t (*)[8]);
 using parents_fn = void (*)(const uint32_t (*)[8], int, uint32_t (*)[8]);
+using var_fn = void (*)(const uint8_t* const*, const uint32_t*, const uint64_t*, const uint8_t*, int, uint32_t (*)[8]);
 struct Simd {
     chunks_fn fn;
     int lanes;
     parents_fn parents;
+    var_fn var;  // chunks of any length, one per lane (cpu_blake3_batch)
 };
 Simd pick_simd() {
     __builtin_cpu_init();
     // SD_CPU_LANES=4/8 caps the width (tests run every width the CPU has)
     const char* cap = getenv("SD_CPU_LANES");
     const int lim = cap ? atoi(cap) : 16;
-    if (lim >= 16 && __builtin_cpu_supports("avx512f")) return {cpu_hash_chunks_x16, 16, cpu_hash_parents_x16};
-    if (lim >= 8 && __builtin_cpu_supports("avx2")) return {cpu_hash_chunks_x8, 8, cpu_hash_parents_x8};
-    return {cpu_hash_chunks_x4, 4, cpu_hash_parents_x4};
+    if (lim >= 16 && __builtin_cpu_supports("avx512f"))
+        return {cpu_hash_chunks_x16, 16, cpu_hash_parents_x16, cpu_hash_chunks_var_x16};
+    if (lim >= 8 && __builtin_cpu_supports("avx2"))
+        return {cpu_hash_chunks_x8, 8, cpu_hash_parents_x8, cpu_hash_chunks_var_x8};
+    return {cpu_hash_chunks_x4, 4, cpu_hash_parents_x4, cpu_hash_chunks_var_x4};
 }
 const Simd& simd() {
     static const Simd s = pick_simd();
@@ -149,12 +159,16 @@ CpuHasher::CpuHasher() {}
 CpuHasher::CpuHasher(uint64_t chunk0) : ctr0_(chunk0) {}
 
 void CpuHasher::push_chunk_cv(const uint32_t cv[8]) {
-    memcpy(blk_[nblk_++], cv, 32);
+    if (nblk_ == SMALL_CHUNKS && !big_) {
+        big_.reset(new uint32_t[BLOCK_CHUNKS][8]);
+        memcpy(big_.get(), small_, sizeof small_);
+    }
+    memcpy(blk()[nblk_++], cv, 32);
     chunks_++;
     if (nblk_ < BLOCK_CHUNKS) return;
     // a complete 1 MiB block (never the message's last: its last chunk stays buffered)
     uint32_t cur[8];
-    merge_levels(blk_.get(), nblk_, false, cur);
+    merge_levels(blk(), nblk_, false, cur);
     nblk_ = 0;
     uint64_t total = ++blocks_;
     while ((total & 1) == 0) {  // this block completes a subtree: merge it with its left half
@@ -204,7 +218,7 @@ void CpuHasher::finish(uint8_t out[32], bool root) const {
         return;
     }
     // the last block: its chunk CVs and the buffered last chunk, merged level-wise
-    uint32_t (*cv)[8] = blk_.get();
+    const uint32_t (*cv)[8] = blk();
     uint32_t last[8];
     chunk_cv(buf_, buf_len_, ctr0_ + chunks_, false, last);
     const bool whole = sp_ == 0;  // the message is this one block
@@ -246,6 +260,85 @@ void cpu_blake3(const uint8_t* p, size_t n, uint8_t out[32]) {
     CpuHasher h;
     h.update(p, n);
     h.finalize(out);
+}
+
+// BLAKE3 of n messages at once.  A message of a few chunks fills few SIMD lanes on its own
+// (most cas messages: 60% of a library's small files are one partial chunk, a sampled
+// message is 56 chunks and an 8-byte one), so the chunks of all n messages are packed
+// across the lanes: every chunk is a job (its bytes, its counter in its message, ROOT if it
+// is its message's only chunk), jobs are grouped by block count, full chunks first, and
+// each message's chunk CVs are then merged into its root.  A message over 1 MiB goes
+// through CpuHasher on its own.
+void cpu_blake3_batch(const uint8_t* const* msg, const uint64_t* len, size_t n, uint8_t (*out)[32]) {
+    constexpr uint64_t BATCH_MAX = 1ull << 20;
+    const Simd& s = simd();
+    std::vector<uint64_t> first(n + 1);  // message i's chunk CVs: slots [first[i], first[i + 1])
+    uint64_t total = 0;
+    size_t per_nb[17] = {0};  // jobs by block count (1..16)
+    for (size_t i = 0; i < n; i++) {
+        first[i] = total;
+        if (len[i] > BATCH_MAX) continue;
+        const uint64_t C = len[i] == 0 ? 1 : (len[i] + 1023) / 1024;
+        per_nb[16] += C - 1;  // the chunks before the last are full
+        const uint64_t last = len[i] - 1024 * (C - 1);
+        per_nb[last == 0 ? 1 : (last + 63) / 64]++;
+        total += C;
+    }
+    first[n] = total;
+    struct Job {
+        const uint8_t* p;
+        uint64_t ctr, slot;
+        uint32_t len;
+        uint8_t root;
+    };
+    std::vector<Job> jobs(total);
+    size_t at[17];
+    for (size_t k = 16, pos = 0; k >= 1; k--) {  // longest first
+        at[k] = pos;
+        pos += per_nb[k];
+    }
+    for (size_t i = 0; i < n; i++) {
+        if (len[i] > BATCH_MAX) continue;
+        const uint64_t C = first[i + 1] - first[i];
+        for (uint64_t c = 0; c < C; c++) {
+            const uint32_t L = (uint32_t)(c + 1 < C ? 1024 : len[i] - 1024 * c);
+            const size_t k = L == 0 ? 1 : (L + 63) / 64;
+            jobs[at[k]++] = Job{msg[i] + 1024 * c, c, first[i] + c, L, (uint8_t)(C == 1)};
+        }
+    }
+    std::vector<uint32_t> cvbuf(total * 8);
+    auto cvs = reinterpret_cast<uint32_t(*)[8]>(cvbuf.data());
+    for (size_t j = 0; j < total; j += (size_t)s.lanes) {
+        const int g = (int)std::min<size_t>((size_t)s.lanes, total - j);
+        const uint8_t* ptr[16];
+        uint32_t lens[16];
+        uint64_t ctr[16];
+        uint8_t root[16];
+        uint32_t tmp[16][8];
+        for (int l = 0; l < g; l++) {
+            const Job& b = jobs[j + (size_t)l];
+            ptr[l] = b.p;
+            lens[l] = b.len;
+            ctr[l] = b.ctr;
+            root[l] = b.root;
+        }
+        s.var(ptr, lens, ctr, root, g, tmp);
+        for (int l = 0; l < g; l++) memcpy(cvs[jobs[j + (size_t)l].slot], tmp[l], 32);
+    }
+    for (size_t i = 0; i < n; i++) {
+        if (len[i] > BATCH_MAX) {
+            cpu_blake3(msg[i], len[i], out[i]);
+            continue;
+        }
+        const uint64_t C = first[i + 1] - first[i];
+        if (C == 1) {  // its one chunk, hashed with ROOT
+            memcpy(out[i], cvs[first[i]], 32);
+            continue;
+        }
+        uint32_t o[8];
+        merge_levels(cvs + first[i], C, true, o);
+        memcpy(out[i], o, 32);
+    }
 }
 
 void hex_lower(const uint8_t* h, int nbytes, char* out) {
@@ -393,11 +486,23 @@ int sd_cpu_cas_ids(const uint8_t* staged, uint64_t staged_bytes, const sd_extent
         if (extents[i].msg_offset + extents[i].msg_len > staged_bytes)
             throw sd_failure(SD_ERR_INVALID, "extent beyond staged_bytes");
     }
-    parallel_for(n, nthreads, [&](size_t i) {
-        if (status && status[i] != SD_FILE_OK) return;
-        uint8_t h[32];
-        cpu_blake3(staged + extents[i].msg_offset, extents[i].msg_len, h);
-        hex_lower(h, 8, out_hex17 + 17 * i);
+    // groups of up to 64 messages, their chunks packed across the SIMD lanes together
+    // (cpu_blake3_batch); at least ~4 groups per thread
+    const size_t G = std::max<size_t>(1, std::min<size_t>(64, n / ((size_t)std::max(1, nthreads) * 4)));
+    parallel_for((n + G - 1) / G, nthreads, [&](size_t t) {
+        const size_t a = t * G, b = std::min(n, a + G);
+        const uint8_t* m[64] = {};
+        uint64_t l[64] = {};
+        size_t idx[64], k = 0;
+        for (size_t i = a; i < b; i++) {
+            if (status && status[i] != SD_FILE_OK) continue;
+            m[k] = staged + extents[i].msg_offset;
+            l[k] = extents[i].msg_len;
+            idx[k++] = i;
+        }
+        uint8_t h[64][32];
+        cpu_blake3_batch(m, l, k, h);
+        for (size_t q = 0; q < k; q++) hex_lower(h[q], 8, out_hex17 + 17 * idx[q]);
     });
     return SD_OK;
     SD_GUARD_END

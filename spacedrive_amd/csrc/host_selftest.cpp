@@ -100,6 +100,32 @@ void test_blake3() {
         hs.finalize(inc);
         CHECK(memcmp(one, inc, 32) == 0);
     }
+    // batches: the chunks of many messages packed across the SIMD lanes == one at a time;
+    // every length 0..2100 in steps of 3 (every block and chunk boundary class), cas
+    // message sizes, and two past the batch's 1 MiB limit, shuffled, from one buffer
+    std::vector<uint64_t> lens;
+    for (uint64_t n = 0; n <= 2100; n += 3) lens.push_back(n);
+    for (uint64_t n : {1024ull, 2048ull, 57352ull, 102408ull, 1ull << 20, (1ull << 20) + 1, 3ull << 20})
+        lens.push_back(n);
+    std::shuffle(lens.begin(), lens.end(), g);
+    uint64_t total = 0;
+    for (uint64_t n : lens) total += n;
+    const auto buf = content(99, total + 1);
+    std::vector<const uint8_t*> msgs;
+    uint64_t off = 0;
+    for (uint64_t n : lens) {
+        msgs.push_back(buf.data() + off);
+        off += n;
+    }
+    std::vector<uint8_t> got(32 * lens.size());
+    cpu_blake3_batch(msgs.data(), lens.data(), lens.size(), reinterpret_cast<uint8_t(*)[32]>(got.data()));
+    int bad = 0;
+    for (size_t i = 0; i < lens.size(); i++) {
+        uint8_t one[32];
+        cpu_blake3(msgs[i], lens[i], one);
+        bad += memcmp(one, got.data() + 32 * i, 32) != 0;
+    }
+    CHECK(bad == 0);
 }
 
 // ------------------------------------------------------------------ planners

@@ -448,12 +448,22 @@ int sd_cas_ids(sd_cas_ctx* ctx, const uint8_t* staged, uint64_t staged_bytes, co
                         a = b - std::min(COHASH_CHUNK, b - front);
                         back = a;
                     }
-                    for (size_t q = a; q < b; q++) {
-                        const sd_extent& e = extents[live[q]];  // validated above
-                        uint8_t h[32];
-                        cpu_blake3(staged + e.msg_offset, e.msg_len, h);
-                        to_hex(h, 8, out_hex17 + live[q] * 17);  // cas.rs:61 to_hex()[..16]
-                        if (status) status[live[q]] = SD_FILE_OK;
+                    // 64 files at a time, their chunks packed across the SIMD lanes together
+                    for (size_t q0 = a; q0 < b; q0 += 64) {
+                        const size_t k = std::min<size_t>(64, b - q0);
+                        const uint8_t* m[64];
+                        uint64_t l[64];
+                        uint8_t h[64][32];
+                        for (size_t q = 0; q < k; q++) {
+                            const sd_extent& e = extents[live[q0 + q]];  // validated above
+                            m[q] = staged + e.msg_offset;
+                            l[q] = e.msg_len;
+                        }
+                        cpu_blake3_batch(m, l, k, h);
+                        for (size_t q = 0; q < k; q++) {
+                            to_hex(h[q], 8, out_hex17 + live[q0 + q] * 17);  // cas.rs:61 to_hex()[..16]
+                            if (status) status[live[q0 + q]] = SD_FILE_OK;
+                        }
                     }
                     host_files.fetch_add(b - a, std::memory_order_relaxed);
                 }

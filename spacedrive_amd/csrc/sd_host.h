@@ -364,7 +364,13 @@ private:
     void finish(uint8_t out[32], bool root) const;
     // chunk CVs of the current 1 MiB block, merged level-wise (SIMD parents) when it is
     // complete; complete blocks' CVs on a stack that merges every completed subtree
-    std::unique_ptr<uint32_t[][8]> blk_{new uint32_t[BLOCK_CHUNKS][8]};
+    // (the first SMALL_CHUNKS CVs inline: a cas message never needs the heap -- a 32 KiB
+    // allocation per message cost the 16-thread CPU path a third of its rate)
+    static constexpr uint32_t SMALL_CHUNKS = 128;
+    uint32_t (*blk())[8] { return big_ ? big_.get() : small_; }
+    const uint32_t (*blk() const)[8] { return big_ ? big_.get() : small_; }
+    uint32_t small_[SMALL_CHUNKS][8];
+    std::unique_ptr<uint32_t[][8]> big_;  // BLOCK_CHUNKS entries, once a message outgrows small_
     uint32_t nblk_ = 0;
     uint32_t stack_[48][8];
     int sp_ = 0;
@@ -375,6 +381,9 @@ private:
     uint32_t buf_len_ = 0;
 };
 void cpu_blake3(const uint8_t* p, size_t n, uint8_t out[32]);
+// BLAKE3 of n messages, the chunks of all of them packed across the SIMD lanes together
+// (cas messages of a few chunks each); out[i] = the hash of msg[i][0, len[i])
+void cpu_blake3_batch(const uint8_t* const* msg, const uint64_t* len, size_t n, uint8_t (*out)[32]);
 // BLAKE3 root of a message from its nb >= 2 consecutive 1 MiB block CVs (32 B each)
 void cpu_root_from_cvs(const uint8_t* cvs, uint64_t nb, uint8_t out[32]);
 // the (non-root) chaining values of 1 MiB blocks [b0, b1) of a message of total_len >= 2

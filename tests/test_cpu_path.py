@@ -51,7 +51,17 @@ def test_cpu_simd_widths(lanes):
             "rng = np.random.default_rng(9)\n"
             "for n in [0, 1025, 4096, 16 * 1024 + 3, 40000, 57352, 300001]:\n"
             "    d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()\n"
-            "    assert cpu.blake3(d) == native.blake3(d), n\n") % ROOT
+            "    assert cpu.blake3(d) == native.blake3(d), n\n"
+            # cas batches: the chunks of many messages packed across the lanes together
+            "from spacedrive_amd.device import stage_plan\n"
+            "sizes = np.concatenate([np.arange(0, 2100, 7), [102399, 102400, 102401, 5 << 20]]).astype(np.uint64)\n"
+            "rng.shuffle(sizes)\n"
+            "cids = np.arange(len(sizes), dtype=np.uint64) + 77\n"
+            "ext, total = stage_plan(sizes)\n"
+            "buf = native.stage_synth(sizes, cids, None, ext['msg_offset'], total)\n"
+            "want = [r.tobytes().hex() for r in native.cas_ids_staged(buf, ext)]\n"
+            "for nt in (1, 3):\n"
+            "    assert cpu.cas_ids_staged(buf, ext, nthreads=nt) == want, nt\n") % ROOT
     env = dict(os.environ, SD_CPU_LANES=str(lanes))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
