@@ -108,7 +108,7 @@ def parity(files: int, mismatches: int, what: str, **kw) -> dict:
     return res
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -153,7 +153,86 @@ def parse():
     p.add_argument("--no-overlap", action="store_true",
                    help="report the serial steps (hash, then dedup, one stream) as the value instead of the "
                         "pipelined ones (batch k's dedup beside batch k+1's hashing)")
-    return p.parse_args()
+    p.add_argument("--host-cpu-budget", type=int, default=0,
+                   help="cap the library's host threads (and the oracle checks') at this many, as the tuning key "
+                        "host_cpu_budget does: 2 rehearses one rank's share of an 8-GPU node's 16-CPU quota on a "
+                        "one-GPU box; 0 = resolved from the affinity mask, quota and LOCAL_WORLD_SIZE")
+    p.add_argument("--oracle-live", action="store_true",
+                   help="recompute the multi-GiB oracle checks (configs[3] files, the mixed file, the split file) "
+                        "on this host instead of comparing with tests/golden/bench_checksums.json (the same oracle's "
+                        "output, committed)")
+    return p.parse_args(argv)
+
+
+# ------------------------------------------------------------------ launcher (--gpus N)
+def launch_mode(gpus: int, env) -> str:
+    """How this process runs the requested --gpus:
+    "rank"      -- started by torch.distributed.run (WORLD_SIZE set): one rank of `gpus`;
+    "spawn"     -- WORLD_SIZE unset and gpus > 1: start the ranks as a child launcher;
+    "inprocess" -- WORLD_SIZE unset and gpus == 1: run here, as before.
+    Raises SystemExit when WORLD_SIZE disagrees with --gpus (a silent one-GPU run labelled
+    as N would be worse than none)."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} (the launcher's rank count) but --gpus {gpus}: "
+                             f"launch with --nproc-per-node {gpus}, or pass --gpus {ws}")
+        return "rank"
+    return "spawn" if gpus > 1 else "inprocess"
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(gpus: int, argv: list, port: int) -> list:
+    """The child launch of `bench.py --gpus N` without WORLD_SIZE: torch.distributed.run with
+    N local ranks on 127.0.0.1, the same arguments (the driver's own N > 1 command line)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def spawn_ranks(gpus: int, argv: list) -> int:
+    """Runs the N ranks as a child process group (subprocess, never exec: this process has
+    made no HIP call and makes none), relays rank 0's JSON line to stdout and everything else
+    the child prints on stdout to stderr, and returns the child's exit code (1 if it exited 0
+    without a line)."""
+    import signal
+    import subprocess
+    cmd = launcher_cmd(gpus, argv, free_port())
+    log("bench.py: --gpus %d without WORLD_SIZE: launching %s" % (gpus, " ".join(cmd)))
+    env = dict(os.environ, SD_BENCH_SPAWNED="1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=None, text=True, env=env)
+
+    def forward(sig, _frame):  # a timeout's SIGTERM reaches the ranks through their launcher
+        try:
+            proc.send_signal(sig)
+        except OSError:
+            pass
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    lines = []
+    try:
+        for line in proc.stdout:
+            if line.lstrip().startswith("{"):
+                lines.append(line.strip())
+            else:
+                sys.stderr.write(line)
+                sys.stderr.flush()
+        rc = proc.wait()
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    if lines:
+        print(lines[-1], flush=True)
+    if rc == 0 and not lines:
+        log("bench.py: the ranks exited 0 without a JSON line")
+        return 1
+    return rc
 
 
 # ------------------------------------------------------------------ PMC traffic lookup
@@ -1088,7 +1167,8 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
         shutil.rmtree(d, ignore_errors=True)
 
 
-def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int, warm_ms: float):
+def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int, warm_ms: float, tm=None,
+              live: bool = False):
     """file_checksum (hash.rs:10-24) of ONE file spread over the ranks: rank r
     holds its contiguous run of 1 MiB blocks (sd_split_range), hashes them to block CVs, the
     CVs are all-gathered in place over libsdcas's RCCL communicator (32 B per MiB), and every
@@ -1155,20 +1235,114 @@ def split_leg(ctx, comm, gib: int, rank: int, world: int, dev, stream, reps: int
         res["ranks_agree"] = all(torch.equal(x, h) for x in allh)
         assert res["ranks_agree"], "the ranks' split checksums differ"
     res["hash"] = bytes(h.cpu().numpy()).hex()
+    if tm is not None:
+        tm.lap("split")
     if rank == 0:  # the file's hash against the oracle's BLAKE3 of the same content
-        from oracle import native
-        want = native.checksum_synth_mt(total, 20_000, 0, nthreads=oracle_threads()).hex()
+        want, src = synth_checksum_expected(20_000, total, live)
         res["parity"] = parity(1, int(want != res["hash"]), "the file's checksum vs the C oracle's chunk-parallel "
-                                                             "BLAKE3 of the same content (rank 0)")
+                                                             "BLAKE3 of the same content (rank 0)", expected_from=[src])
+    if tm is not None:
+        tm.lap("split_oracle_check")
     sc.close()
     del d_slice, cvs
     torch.cuda.empty_cache()
     return res
 
 
+# ------------------------------------------------------------------ wall time per leg
+class Timing(dict):
+    """Wall seconds per leg of this rank's run: lap(name) charges the
+    time since the previous lap to `name`."""
+
+    def __init__(self):
+        super().__init__()
+        self._t = time.perf_counter()
+
+    def lap(self, name: str) -> None:
+        now = time.perf_counter()
+        self[name] = round(self.get(name, 0.0) + now - self._t, 3)
+        self._t = now
+
+
+# ------------------------------------------------------------------ multi-GiB oracle checks
+GOLDEN_CHECKSUMS = os.path.join(ROOT, "tests", "golden", "bench_checksums.json")
+_golden = None
+
+
+def golden_checksums() -> dict:
+    """tests/golden/bench_checksums.json: the C oracle's checksums of the bench's multi-GiB
+    synthetic files (configs[3]'s files 0 and 15 of every rank's shard, each rank's shortest
+    mixed file, the split file), written by tests/golden/make_bench_golden.py from the same
+    deterministic generator; tests/test_bench_helpers.py re-derives some of them with the
+    oracle on every CPU run.  Empty when absent."""
+    global _golden
+    if _golden is None:
+        try:
+            with open(GOLDEN_CHECKSUMS) as f:
+                _golden = json.load(f)
+        except OSError:
+            _golden = {}
+    return _golden
+
+
+def mixed_layout(start: int, total: int):
+    """configs[3]'s mixed variant: files of 2..8 GiB (unaligned lengths) packed at 128-B
+    starts (SD_STAGE_ALIGN, profiles/r2/r2z5_ck_align.json) in the first `total` bytes of the
+    buffer that holds the rank's 16 generated files; seeded by the rank's first file index."""
+    rng = np.random.default_rng(7 + start)
+    offs, lens, pos = [], [], 0
+    while True:
+        ln = int(rng.integers(2 << 30, (8 << 30) + 1))
+        if pos + ln > total:
+            break
+        offs.append(pos)
+        lens.append(ln)
+        pos = (pos + ln + 127) // 128 * 128
+    return offs, lens
+
+
+def synth_checksum_expected(cid: int, length: int, live: bool):
+    """(hex, source) of BLAKE3 over synthetic file `cid`'s first `length` bytes: the committed
+    oracle output when it holds this file, else the C oracle on this host (this rank's share
+    of its threads)."""
+    g = golden_checksums().get("synth", {}).get(f"{cid}:{length}")
+    if g and not live:
+        return g, "golden"
+    from oracle import native
+    return native.checksum_synth_mt(length, cid, 0, nthreads=oracle_threads()).hex(), "oracle (live)"
+
+
+def mixed_expected(start: int, total: int, mi: int, off: int, ln: int, flen: int, live: bool):
+    """(hex, source) of mixed file `mi` -- bytes [off, off + ln) of the concatenation of the
+    rank's 16 generated files of flen bytes (cids 10000 + start + i)."""
+    g = golden_checksums().get("mixed", {}).get(f"{start}:{total}")
+    if g and not live and g["index"] == mi and g["offset"] == off and g["len"] == ln:
+        return g["hash"], "golden"
+    from oracle import native
+    return mixed_host_checksum(start, off, ln, flen, oracle_threads()).hex(), "oracle (live)"
+
+
+def mixed_host_checksum(start: int, off: int, ln: int, flen: int, nthreads: int) -> bytes:
+    """The oracle's checksum of a mixed file, its bytes generated on the host piece by piece
+    from the generated files it spans."""
+    from oracle import native
+    buf = np.empty(ln, np.uint8)
+    pos = off
+    while pos < off + ln:
+        i, o = divmod(pos, flen)
+        n = min(flen - o, off + ln - pos)
+        native.lib().sdo_synth_fill(10_000 + start + i, 0, o, n, buf[pos - off:].ctypes.data)
+        pos += n
+    return native.checksum_mt(buf, ln, nthreads=nthreads)
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse()
+    mode = launch_mode(args.gpus, os.environ)
+    if mode == "spawn":  # before any torch.cuda call: the ranks are children
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    t_main = time.perf_counter()
     if os.environ.get("SD_BENCH_STACKS_AFTER"):  # debugging a stuck run: dump every thread's stack
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["SD_BENCH_STACKS_AFTER"]), repeat=True)
@@ -1180,8 +1354,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    tm = Timing()
     if args.share_gpu:  # rehearsal of the N-rank path on a box with fewer GPUs
         local = local % torch.cuda.device_count()
+    elif world > 1 and local >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py: local rank {local} of {world} but {torch.cuda.device_count()} visible GPUs "
+                         f"(--share-gpu maps several ranks onto one GPU: a rehearsal)")
     torch.cuda.set_device(local)
     global DIST
     if world > 1 or args.force_dist:
@@ -1195,6 +1373,8 @@ def main():
     transport = args.dedup or ("rccl" if args.dist_backend == "nccl" else "torch")
     import spacedrive_amd as sd
     from spacedrive_amd import _native, dedup, synth
+    if args.host_cpu_budget > 0:
+        sd.set_tuning("host_cpu_budget", args.host_cpu_budget)
 
     ctx = sd.Context(local)
     n = args.files_per_gpu
@@ -1253,6 +1433,7 @@ def main():
             ev[k][3].record(stream)
         return r
 
+    tm.lap("setup")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -1337,6 +1518,7 @@ def main():
                 ded_seen[b] = True
             return r
 
+        tm.lap("steps_serial")
         pipelined_steps(args.warmup)
         torch.cuda.synchronize()
         if DIST:
@@ -1432,6 +1614,7 @@ def main():
                     "note": "the serial steps' event breakdown (steps_serial)"},
         "dedup": dedup_totals,
     }
+    tm.lap("steps_pipelined" if pipelined else "steps_serial")
     # ---- the timed steps' output, checked (outside the timed regions) --------------------
     # (1) hashes: a fixed sample of every rank's shard against the C oracle
     ps = parity_sample(sizes, cids, twins, d_hash, start)
@@ -1464,20 +1647,24 @@ def main():
     assert out["parity_sample"]["mismatches"] == 0, out["parity_sample"]
     assert out["dedup"]["parity"], out["dedup"]["parity_slice"]
 
+    tm.lap("parity_steps")
     solo = rank == 0 and not DIST and not args.no_extras
     with_h2d = {}
     if args.host_staged_files > 0 and not args.no_extras:  # every rank: one PCIe link per GPU
         k_h2d = args.host_staged_files if not DIST else min(args.host_staged_files, 150_000)
         with_h2d["cas"] = host_staged(ctx, ext, d_staged, k_h2d, dev, stream, world, lib_=(sizes, cids, twins))
+        tm.lap("with_h2d_cas")
     if solo and args.file_backed_files > 0:
         out["file_backed"] = file_backed(ctx, sizes, ext, d_staged, args.file_backed_files,
                                          with_cpu=not args.no_cpu_baseline, latency_calls=args.latency_calls,
                                          ident_files=args.identifier_files)
         if "latency" in out["file_backed"]:
             out["latency"] = out["file_backed"].pop("latency")
+        tm.lap("file_backed")
     del d_staged, recs, rep, owners
     torch.cuda.empty_cache()
 
+    tm.lap("release")
     # configs[3]: validator checksums, 16 files of (G/16) GiB per GPU
     if args.checksum_gib > 0:
         nf = 16
@@ -1512,37 +1699,30 @@ def main():
                                         "hbm": {"achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                                 "frac": gbps / HBM_PEAK_GBPS}},
                            "launch_grid": cb.blocks * 256, "traffic": tr_ck["bytes"] if tr_ck else None}
+        tm.lap("checksum")
         # the timed output against the oracle: two of the 16 files (the first and the last)
-        from oracle import native
         sums = d_sum.cpu().numpy().reshape(nf, 32)
         chk = [0, nf - 1]
-        bad = sum(native.checksum_synth_mt(flen, 10_000 + start + i, 0, nthreads=oracle_threads()) != sums[i].tobytes()
-                  for i in chk)
+        exp = [synth_checksum_expected(10_000 + start + i, flen, args.oracle_live) for i in chk]
+        bad = sum(e[0] != sums[i].tobytes().hex() for e, i in zip(exp, chk))
         out["checksum"]["parity"] = parity(len(chk), bad, "files 0 and 15 of the timed batch vs the C oracle's "
-                                                          "chunk-parallel BLAKE3 of the same content", checked=chk)
+                                                          "chunk-parallel BLAKE3 of the same content", checked=chk,
+                                           expected_from=sorted({e[1] for e in exp}))
+        tm.lap("checksum_oracle_check")
         # configs[3]'s mixed variant: files of 2..8 GiB (unaligned lengths) in the same buffer
-        rng = np.random.default_rng(7 + start)
-        m_offs, m_lens, pos = [], [], 0
-        while True:
-            ln = int(rng.integers(2 << 30, (8 << 30) + 1))
-            if pos + ln > nf * flen:
-                break
-            m_offs.append(pos)
-            m_lens.append(ln)
-            pos = (pos + ln + 127) // 128 * 128  # SD_STAGE_ALIGN starts (profiles/r2/r2z5_ck_align.json)
+        m_offs, m_lens = mixed_layout(start, nf * flen)
         if m_lens:
             cbm = ctx.checksum_batch(m_offs, m_lens)
             d_msum = torch.empty(len(m_lens) * 32, dtype=torch.uint8, device=dev)
             cbm.run(d_data, d_msum, stream)
             mx_ms = ev_ms(lambda: cbm.run(d_data, d_msum, stream), stream, reps=args.checksum_steps)
             mroof = valu_roof(cbm.compressions, mx_ms)
+            tm.lap("checksum_mixed")
             # one mixed file (the shortest: each spans parts of two generated files) against
-            # the oracle hashing the same bytes, copied to the host
+            # the oracle hashing the same bytes, generated on the host
             mi = int(np.argmin(m_lens))
-            host = d_data[m_offs[mi]:m_offs[mi] + m_lens[mi]].cpu().numpy()
-            mbad = int(native.checksum_mt(host, m_lens[mi], nthreads=oracle_threads()) !=
-                       d_msum[32 * mi:32 * mi + 32].cpu().numpy().tobytes())
-            del host
+            want_m, src_m = mixed_expected(start, nf * flen, mi, m_offs[mi], m_lens[mi], flen, args.oracle_live)
+            mbad = int(want_m != d_msum[32 * mi:32 * mi + 32].cpu().numpy().tobytes().hex())
             out["checksum"]["mixed"] = {
                 "workload": f"configs[3] mixed: {len(m_lens)} files of 2..8 GiB, unaligned lengths, "
                             f"packed at 128-B (SD_STAGE_ALIGN) starts",
@@ -1550,20 +1730,23 @@ def main():
                 "GBps": cbm.total_bytes / (mx_ms * 1e-3) / 1e9, "frac": mroof["frac"],
                 "frac_full_rate": mroof["frac_full_rate"],
                 "parity": parity(1, mbad, f"mixed file {mi} ({m_lens[mi]} B, the shortest) vs the C oracle's "
-                                          "chunk-parallel BLAKE3 of the same bytes")}
+                                          "chunk-parallel BLAKE3 of the same bytes", expected_from=[src_m])}
             del cbm, d_msum
+            tm.lap("checksum_mixed_oracle_check")
         del d_data, cb
         torch.cuda.empty_cache()
 
     if args.split_gib > 0:
         out["checksum_one_file"] = split_leg(ctx, comm, args.split_gib, rank, world, dev, stream,
-                                             args.checksum_steps, args.warm_ms)
+                                             args.checksum_steps, args.warm_ms, tm=tm, live=args.oracle_live)
 
     if solo and args.host_checksum_gib > 0:
         with_h2d["checksum"] = checksum_host(ctx, args.host_checksum_gib, dev, stream)
+        tm.lap("with_h2d_checksum")
     if solo and args.file_checksum_mib > 0:
         out["file_backed_checksum"] = file_checksums_leg(ctx, args.file_checksum_mib,
                                                          with_cpu=not args.no_cpu_baseline, dev=dev)
+        tm.lap("file_backed_checksum")
     if with_h2d:
         out["with_h2d"] = with_h2d
 
@@ -1571,6 +1754,7 @@ def main():
         out["configs"] = {k: config_leg(ctx, k, args.config_files, args.config_reps, dev, stream, valu_peak,
                                         args.warm_ms)
                           for k in ("small", "sampled")}
+        tm.lap("configs_1_2")
 
     if rank == 0 and not DIST and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sizes, cids, twins, args.cpu_seconds)
@@ -1578,8 +1762,24 @@ def main():
             out["cpu_baseline"]["file_backed"] = dict(out["file_backed"]["cpu_reference_schedule"],
                                                       files=out["file_backed"]["files"],
                                                       note="reference read schedule from files (page cache)")
+        tm.lap("cpu_baseline")
     if comm is not None:
         comm.close()
+    total_s = time.perf_counter() - t_main
+    tot = torch.tensor([total_s], dtype=torch.float64, device=cdev)
+    if DIST:
+        dist.all_reduce(tot, op=dist.ReduceOp.MAX)
+    out["timing"] = {"rank0_s": dict(tm), "rank0_total_s": round(total_s, 3),
+                     "total_s_max_over_ranks": round(float(tot.item()), 3),
+                     "host_threads_budget": _native.host_cpu_budget()["budget"],
+                     "note": "wall seconds per leg on rank 0, from main() to the line (the process's import and "
+                             "launch before main() excluded); *_oracle_check legs compare with the committed "
+                             "oracle goldens unless --oracle-live"}
+    out["launch"] = {"requested_gpus": args.gpus, "mode": mode,
+                     "spawned_by_bench": os.environ.get("SD_BENCH_SPAWNED") == "1",
+                     "share_gpu": bool(args.share_gpu),
+                     "devices_used": len({(r % torch.cuda.device_count()) if args.share_gpu else r
+                                          for r in range(world)}) if world > 1 else 1}
     if DIST:
         dist.barrier()
         dist.destroy_process_group()

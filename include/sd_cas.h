@@ -104,15 +104,17 @@ typedef struct sd_checksum_batch sd_checksum_batch;
 int sd_cas_abi_version(void);
 /* The host thread budget: the most host threads one call of this
  * process starts -- readers, CPU-path workers and co-hashing threads alike.  Resolved once
- * as min(CPUs in the affinity mask, the cgroup's CPU quota rounded up) / LOCAL_WORLD_SIZE
- * (the ranks sharing the node's host; 1 when unset), at least 1; the tuning key
+ * as min(affinity share, quota share), at least 1: the CPUs in the affinity mask, divided by
+ * LOCAL_WORLD_SIZE (the ranks sharing the node's host; 1 when unset) only when the mask holds
+ * every online CPU (a narrower mask is a per-rank binding); and the tightest cgroup CPU quota
+ * from the process's cgroup up, rounded up, divided by LOCAL_WORLD_SIZE.  The tuning key
  * "host_cpu_budget" > 0 replaces it.  out[5]: [0] the budget, [1] affinity CPUs, [2] cgroup
  * quota in milli-CPUs (0 = none), [3] LOCAL_WORLD_SIZE, [4] 1 if the tuning key set it. */
 int sd_host_cpu_budget(int out[5]);
 /* Where the library's own threads run: out[0] = 1 when they are placed on the CPUs of the
- * NUMA node of the first context's device (within the affinity mask; tuning "numa_pin",
- * default 0 = not placed), out[1] = those CPUs, out[2] = the device's node (-1 unknown).
- * Callers' threads are never moved. */
+ * NUMA node of the first context's device (within each thread's own affinity mask; tuning
+ * "numa_pin", default 0 = not placed), out[1] = those CPUs, out[2] = the device's node (-1
+ * unknown).  Callers' threads are never moved; with "numa_pin" 0 no thread is. */
 int sd_host_numa(int out[3]);
 /* last error message of the calling thread ("" if none) */
 const char* sd_cas_last_error(void);

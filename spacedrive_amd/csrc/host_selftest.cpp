@@ -399,6 +399,27 @@ void test_pool_limit() {
         pool.wait();
         CHECK(sum2.load() == 99 * 100 / 2 && (int)ids.size() <= k);
     }
+    // a pool grown by an earlier, larger call (the context's stage_pool only grows): the
+    // next call's limit still holds -- cas_files' readers and stat_files pass theirs
+    std::shared_ptr<StagePool> ctx_pool = std::make_shared<StagePool>(2);
+    ctx_pool->run(64, [](size_t) {});
+    ctx_pool = std::make_shared<StagePool>(16);  // a call asked for 16 readers
+    for (int k : {2, 3}) {
+        std::mutex mu;
+        std::vector<std::thread::id> ids;
+        auto note = [&](size_t) {
+            std::lock_guard<std::mutex> g(mu);
+            if (std::find(ids.begin(), ids.end(), std::this_thread::get_id()) == ids.end())
+                ids.push_back(std::this_thread::get_id());
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        };
+        ctx_pool->run(200, note, k);
+        CHECK((int)ids.size() <= k);
+        ids.clear();
+        ctx_pool->start(200, note, k);
+        ctx_pool->wait();
+        CHECK((int)ids.size() <= k);
+    }
 }
 
 // ------------------------------------------------------------------ pools and CPU batches
@@ -502,16 +523,22 @@ void test_cpu_checksums_fd_limit() {
 
 // ------------------------------------------------------------------ host thread budget
 void test_cpu_budget() {
-    // the rule: min(affinity, quota rounded up) / ranks on the host, at least 1
-    CpuBudget b = cpu_budget_resolve(256, 16.0, 8);  // an 8-GPU node, one 16-CPU quota
-    CHECK(b.budget == 2 && b.affinity == 256 && b.quota_milli == 16000 && b.local_world == 8);
-    CHECK(cpu_budget_resolve(256, 16.0, 1).budget == 16);  // one rank: the whole quota
-    CHECK(cpu_budget_resolve(256, 128.0, 8).budget == 16);
-    CHECK(cpu_budget_resolve(8, 0.0, 1).budget == 8);      // no quota: the affinity mask
-    CHECK(cpu_budget_resolve(8, 0.0, 1).quota_milli == 0);
-    CHECK(cpu_budget_resolve(4, 16.0, 8).budget == 1);     // never below one thread
-    CHECK(cpu_budget_resolve(64, 1.5, 1).budget == 2);     // a fractional quota rounds up
-    CHECK(cpu_budget_resolve(3, 64.0, 0).budget == 3);     // a bogus world size counts as 1
+    // the rule: min(affinity share, quota rounded up / ranks), at least 1; the affinity is
+    // split over the ranks only when it holds every online CPU
+    CpuBudget b = cpu_budget_resolve(256, 256, 16.0, 8);  // an 8-GPU node, one 16-CPU quota
+    CHECK(b.budget == 2 && b.affinity == 256 && b.online == 256 && b.quota_milli == 16000 && b.local_world == 8);
+    CHECK(cpu_budget_resolve(256, 256, 16.0, 1).budget == 16);  // one rank: the whole quota
+    CHECK(cpu_budget_resolve(256, 256, 128.0, 8).budget == 16);
+    CHECK(cpu_budget_resolve(8, 8, 0.0, 1).budget == 8);      // no quota: the affinity mask
+    CHECK(cpu_budget_resolve(8, 8, 0.0, 1).quota_milli == 0);
+    CHECK(cpu_budget_resolve(4, 4, 16.0, 8).budget == 1);     // never below one thread
+    CHECK(cpu_budget_resolve(64, 64, 1.5, 1).budget == 2);    // a fractional quota rounds up
+    CHECK(cpu_budget_resolve(3, 3, 64.0, 0).budget == 3);     // a bogus world size counts as 1
+    // ranks bound to their own CPUs (numactl, --cpu-bind): the mask is this rank's share
+    CHECK(cpu_budget_resolve(16, 256, 0.0, 8).budget == 16);
+    CHECK(cpu_budget_resolve(16, 256, 64.0, 8).budget == 8);   // the shared quota still splits
+    CHECK(cpu_budget_resolve(256, 256, 0.0, 8).budget == 32);  // unbound, no quota: the node's CPUs split
+    CHECK(cpu_budget_resolve(16, 8, 0.0, 1).online == 16);     // online never below the mask
     // the cgroup readers, on fake cgroup trees
     const std::string v2 = g_dir + "/cg2", v1 = g_dir + "/cg1", v1c = v1 + "/cpu", none = g_dir + "/cg0";
     CHECK(mkdir(v2.c_str(), 0700) == 0 && mkdir(v1.c_str(), 0700) == 0 && mkdir(v1c.c_str(), 0700) == 0 &&
@@ -532,6 +559,42 @@ void test_cpu_budget() {
     put(v1c + "/cpu.cfs_quota_us", "-1\n");
     CHECK(cgroup_cpu_quota(v1.c_str()) == 0.0);
     CHECK(cgroup_cpu_quota(none.c_str()) == 0.0);
+    // the process's own cgroup, nested below the mount root (cgroupns=host, systemd slices):
+    // the tightest limit on the path up binds; a private namespace ("0::/") reads the root
+    const std::string pc = g_dir + "/proc_cgroup", a = v2 + "/a", ab = a + "/b", abc = ab + "/c";
+    for (const std::string& d : {a, ab, abc}) CHECK(mkdir(d.c_str(), 0700) == 0);
+    put(v2 + "/cpu.max", "max 100000\n");
+    put(a + "/cpu.max", "800000 100000\n");   // 8 CPUs two levels up
+    put(ab + "/cpu.max", "max 100000\n");
+    put(abc + "/cpu.max", "2400000 100000\n");  // 24 CPUs in the process's own
+    put(pc, "0::/a/b/c\n");
+    CHECK(cgroup_cpu_quota_self(v2.c_str(), pc.c_str()) == 8.0);
+    put(abc + "/cpu.max", "400000 100000\n");  // 4 in its own: tighter
+    CHECK(cgroup_cpu_quota_self(v2.c_str(), pc.c_str()) == 4.0);
+    put(pc, "0::/\n");
+    CHECK(cgroup_cpu_quota_self(v2.c_str(), pc.c_str()) == 0.0);
+    put(v2 + "/cpu.max", "1600000 100000\n");
+    CHECK(cgroup_cpu_quota_self(v2.c_str(), pc.c_str()) == 16.0);
+    put(pc, "0::/a/b\n");
+    CHECK(cgroup_cpu_quota_self(v2.c_str(), pc.c_str()) == 8.0);
+    // v1: the cpu controller's hierarchy under <root>/cpu
+    const std::string v1d = v1c + "/slice";
+    CHECK(mkdir(v1d.c_str(), 0700) == 0);
+    put(v1d + "/cpu.cfs_quota_us", "300000\n");
+    put(v1d + "/cpu.cfs_period_us", "100000\n");
+    put(pc, "12:cpuacct,cpu:/slice\n3:memory:/other\n");
+    CHECK(cgroup_cpu_quota_self(v1.c_str(), pc.c_str()) == 3.0);
+    put(pc, "12:memory:/slice\n");  // no cpu controller line: the root only (unlimited)
+    CHECK(cgroup_cpu_quota_self(v1.c_str(), pc.c_str()) == 0.0);
+    CHECK(cgroup_cpu_quota_self(none.c_str(), (g_dir + "/no_such_file").c_str()) == 0.0);
+    for (const std::string& d : {abc, ab, a}) {
+        unlink((d + "/cpu.max").c_str());
+        rmdir(d.c_str());
+    }
+    unlink((v1d + "/cpu.cfs_quota_us").c_str());
+    unlink((v1d + "/cpu.cfs_period_us").c_str());
+    rmdir(v1d.c_str());
+    unlink(pc.c_str());
     for (const std::string& f : {v2 + "/cpu.max", v1c + "/cpu.cfs_quota_us", v1c + "/cpu.cfs_period_us"})
         unlink(f.c_str());
     rmdir(v1c.c_str());
@@ -599,6 +662,48 @@ void test_numa_placement() {
     CHECK(sd_cas_set_tuning("numa_pin", 0) == SD_OK);
     CHECK(numa_placement(nullptr, nullptr) == 0);
     CHECK(!workers_on(1));  // every thread back on the whole mask
+    // a thread's own narrower mask (a pinned runtime thread, another rank's thread) is never
+    // widened or replaced: untouched while "numa_pin" is 0, narrowed only within itself at 1,
+    // and given back its own mask -- not the process's -- at 0 again
+    int second = -1;
+    for (int c = first + 1; c < CPU_SETSIZE && second < 0; c++)
+        if (CPU_ISSET(c, &all)) second = c;
+    auto mask_is = [](std::initializer_list<int> cpus) {
+        cpu_set_t now;
+        CPU_ZERO(&now);
+        sched_getaffinity(0, sizeof now, &now);
+        bool ok = CPU_COUNT(&now) == (int)cpus.size();
+        for (int c : cpus) ok = ok && CPU_ISSET(c, &now);
+        return ok;
+    };
+    std::thread([&] {
+        cpu_set_t mine;
+        CPU_ZERO(&mine);
+        CPU_SET(second, &mine);
+        CHECK(sched_setaffinity(0, sizeof mine, &mine) == 0);
+        CHECK(sd_cas_set_tuning("numa_pin", 0) == SD_OK);  // a new generation: the thread looks again
+        library_thread_place();
+        CHECK(mask_is({second}));
+        CHECK(sd_cas_set_tuning("numa_pin", 1) == SD_OK);
+        library_thread_place();  // the preferred {first} holds none of its CPUs: left as it was
+        CHECK(mask_is({second}));
+        CHECK(sd_cas_set_tuning("numa_pin", 0) == SD_OK);
+        library_thread_place();
+        CHECK(mask_is({second}));
+    }).join();
+    std::thread([&] {
+        cpu_set_t mine;
+        CPU_ZERO(&mine);
+        CPU_SET(first, &mine);
+        CPU_SET(second, &mine);
+        CHECK(sched_setaffinity(0, sizeof mine, &mine) == 0);
+        CHECK(sd_cas_set_tuning("numa_pin", 1) == SD_OK);
+        library_thread_place();
+        CHECK(mask_is({first}));  // placed, within its own mask
+        CHECK(sd_cas_set_tuning("numa_pin", 0) == SD_OK);
+        library_thread_place();
+        CHECK(mask_is({first, second}));  // its own mask back, not the process's
+    }).join();
 }
 
 // ------------------------------------------------------------------ coalescer

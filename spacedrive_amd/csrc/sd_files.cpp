@@ -423,7 +423,7 @@ void cas_files(sd_cas_ctx* ctx, const char* const* paths, const uint64_t* sizes,
             std::lock_guard<std::mutex> g(sh.mu);
             sh.to_main.notify_one();
         }
-    });
+    }, nthreads);  // this call's readers only: the pool may hold more from an earlier call
     cleanup.staging = true;
     // SD_PROFILE_FILES=1: one stderr line per call (where this thread's time goes)
     static const bool prof = getenv("SD_PROFILE_FILES") != nullptr;
@@ -562,7 +562,7 @@ namespace {
 
 // stat every file in parallel: its length picks the route (regular files only)
 void stat_files(StagePool& pool, const char* const* paths, size_t n, std::vector<uint64_t>& hint,
-                std::vector<uint8_t>& regular) {
+                std::vector<uint8_t>& regular, int threads) {
     hint.assign(n, 0);
     regular.assign(n, 0);
     pool.run(n, [&](size_t i) {
@@ -571,7 +571,7 @@ void stat_files(StagePool& pool, const char* const* paths, size_t n, std::vector
             hint[i] = (uint64_t)st.st_size;
             regular[i] = 1;
         }
-    });
+    }, threads);  // the caller and threads - 1 workers, whatever the pool grew to before
 }
 
 // The GPU route of sd_file_checksums over the files next() yields (SIZE_MAX ends them), on
@@ -762,7 +762,7 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
     std::vector<uint8_t> regular;
     if (cpu_max != 0 && hyb > 0 && hyb < threads && n >= 2) {
         constexpr uint64_t BIG_FILE = 8ull << 20, BIG_TOTAL = 512ull << 20;
-        stat_files(*ctx->stage_pool(threads), paths, n, hint, regular);
+        stat_files(*ctx->stage_pool(threads), paths, n, hint, regular, threads);
         std::vector<size_t> big, rest;
         uint64_t big_bytes = 0;
         for (size_t i = 0; i < n; i++) {
@@ -868,7 +868,7 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
         return sd_cpu_file_checksums(paths, n, out_hex65, status, threads);
     }
     ctx->checksum_calls_gpu.fetch_add(1, std::memory_order_relaxed);
-    if (hint.size() != n) stat_files(*ctx->stage_pool(threads), paths, n, hint, regular);
+    if (hint.size() != n) stat_files(*ctx->stage_pool(threads), paths, n, hint, regular, threads);
     size_t i = 0;
     uint64_t all = 0;
     for (size_t q = 0; q < n; q++) all += hint[q];

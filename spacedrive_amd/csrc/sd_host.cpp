@@ -62,16 +62,21 @@ bool read_small(const std::string& path, char* buf, size_t cap) {
 }  // namespace
 
 // ------------------------------------------------------------------ host thread budget
-CpuBudget cpu_budget_resolve(int affinity, double quota_cpus, int local_world) {
+CpuBudget cpu_budget_resolve(int affinity, int online, double quota_cpus, int local_world) {
     CpuBudget b;
     b.affinity = std::max(1, affinity);
+    b.online = std::max(b.affinity, online);
     b.quota_milli = quota_cpus > 0 ? (int)std::min(1e9, quota_cpus * 1000.0 + 0.5) : 0;
     b.local_world = std::max(1, local_world);
-    // a fractional quota still runs that many threads' worth of time: round up, so a quota
-    // of 1.5 CPUs allows 2 threads, but never beyond the affinity mask
-    int cpus = b.affinity;
-    if (quota_cpus > 0) cpus = std::min(cpus, std::max(1, (int)(quota_cpus + 0.999)));
-    b.budget = std::max(1, cpus / b.local_world);
+    // The affinity mask is this process's own: a mask narrower than the machine is a per-rank
+    // binding (numactl, Slurm --cpu-bind, a launcher's placement) and already this rank's
+    // share; a mask of every online CPU is shared by the node's ranks and is split.
+    const int aff_share = b.affinity >= b.online ? b.affinity / b.local_world : b.affinity;
+    int cpus = std::max(1, aff_share);
+    // the cgroup quota covers every rank in the container: always split.  A fractional quota
+    // still runs that many threads' worth of time: round up (1.5 CPUs allows 2 threads)
+    if (quota_cpus > 0) cpus = std::min(cpus, std::max(1, (int)(quota_cpus + 0.999) / b.local_world));
+    b.budget = std::max(1, cpus);
     return b;
 }
 
@@ -94,15 +99,87 @@ double cgroup_cpu_quota(const char* root) {
     return 0;
 }
 
+namespace {
+// one directory's own limit: v2 cpu.max, or v1 cpu.cfs_quota_us / cpu.cfs_period_us
+double cgroup_dir_quota(const std::string& dir, bool v1) {
+    char buf[128], pb[64];
+    if (!v1) {
+        if (!read_small(dir + "/cpu.max", buf, sizeof buf)) return 0;
+        char q[32] = {0};
+        double period = 0;
+        if (sscanf(buf, "%31s %lf", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) return atof(q) / period;
+        return 0;
+    }
+    if (read_small(dir + "/cpu.cfs_quota_us", buf, sizeof buf) && read_small(dir + "/cpu.cfs_period_us", pb, sizeof pb)) {
+        const double q = atof(buf), p = atof(pb);
+        if (q > 0 && p > 0) return q / p;
+    }
+    return 0;
+}
+double min_quota(double a, double b) { return a <= 0 ? b : (b <= 0 ? a : std::min(a, b)); }
+}  // namespace
+
+double cgroup_cpu_quota_self(const char* root, const char* proc_cgroup) {
+    const std::string mnt = root ? root : "/sys/fs/cgroup";
+    // the process's own cgroup: "0::/path" (v2), or "N:...cpu...:/path" (v1)
+    std::string v2path, v1path;
+    bool have_v2 = false, have_v1 = false;
+    if (FILE* f = fopen(proc_cgroup ? proc_cgroup : "/proc/self/cgroup", "re")) {
+        char line[4096];
+        while (fgets(line, sizeof line, f)) {
+            line[strcspn(line, "\n")] = 0;
+            char* c1 = strchr(line, ':');
+            char* c2 = c1 ? strchr(c1 + 1, ':') : nullptr;
+            if (!c2) continue;
+            const std::string ctrl(c1 + 1, c2);
+            if (strncmp(line, "0:", 2) == 0 && ctrl.empty()) {
+                v2path = c2 + 1;
+                have_v2 = true;
+            } else {
+                // v1 controller lists: "cpu", "cpu,cpuacct", "cpuacct,cpu"
+                size_t s = 0;
+                while (s <= ctrl.size()) {
+                    size_t e = ctrl.find(',', s);
+                    if (e == std::string::npos) e = ctrl.size();
+                    if (ctrl.compare(s, e - s, "cpu") == 0) {
+                        v1path = c2 + 1;
+                        have_v1 = true;
+                    }
+                    s = e + 1;
+                }
+            }
+        }
+        fclose(f);
+    }
+    // the mount root's own limit (a private cgroup namespace shows "/" and lands here)
+    double q = cgroup_cpu_quota(mnt.c_str());
+    // walk from the process's cgroup up to the mount root: the tightest limit on the way
+    // binds (systemd slices, cgroupns=host containers keep it in a nested directory)
+    auto walk = [&](const std::string& base, std::string rel, bool v1) {
+        while (!rel.empty() && rel != "/") {
+            q = min_quota(q, cgroup_dir_quota(base + rel, v1));
+            const size_t slash = rel.find_last_of('/');
+            rel = slash == std::string::npos ? std::string() : rel.substr(0, slash);
+        }
+    };
+    if (have_v2) walk(mnt, v2path, false);
+    if (have_v1) {  // the cpu controller's hierarchy: <root>/cpu (often a link to cpu,cpuacct)
+        walk(mnt + "/cpu", v1path, true);
+    }
+    return q;
+}
+
 CpuBudget host_cpu_budget_detail() {
     static const CpuBudget resolved = [] {
         int affinity = 1;
         cpu_set_t set;
         CPU_ZERO(&set);
         if (sched_getaffinity(0, sizeof set, &set) == 0) affinity = CPU_COUNT(&set);
+        const long online = sysconf(_SC_NPROCESSORS_ONLN);
         int world = 1;
         if (const char* w = getenv("LOCAL_WORLD_SIZE")) world = std::max(1, atoi(w));
-        return cpu_budget_resolve(affinity, cgroup_cpu_quota(nullptr), world);
+        return cpu_budget_resolve(affinity, online > 0 ? (int)online : affinity, cgroup_cpu_quota_self(nullptr, nullptr),
+                                  world);
     }();
     CpuBudget b = resolved;
     const int o = tuning_get(SD_TUNE_HOST_CPU_BUDGET);
@@ -118,11 +195,13 @@ int host_cpu_budget() { return host_cpu_budget_detail().budget; }
 // ------------------------------------------------------------------ NUMA placement
 namespace {
 std::mutex g_numa_mu;
-cpu_set_t g_numa_set, g_numa_all;  // the preferred CPUs; the process's mask when they were set
+cpu_set_t g_numa_set;              // the preferred CPUs
 int g_numa_count = 0;             // CPUs in g_numa_set (0 = no preference)
 int g_numa_node = -1;             // the node they belong to
 std::atomic<int> g_numa_gen{0};   // bumped when the preference changes
 thread_local int t_numa_gen = 0;  // the generation this thread applied
+thread_local bool t_placed = false;  // this thread runs on a mask library_thread_place set
+thread_local cpu_set_t t_orig_mask;  // its own mask from before that
 }  // namespace
 
 int numa_prefer_cpus(const char* list) {
@@ -150,7 +229,6 @@ int numa_prefer_cpus(const char* list) {
     std::lock_guard<std::mutex> g(g_numa_mu);
     if (g_numa_count) return g_numa_count;  // the first context's node stays
     g_numa_set = want;
-    g_numa_all = allowed;
     g_numa_count = n;
     g_numa_gen.fetch_add(1);
     return n;
@@ -186,13 +264,29 @@ void library_thread_place() {
     if (gen == t_numa_gen) return;
     t_numa_gen = gen;
     cpu_set_t s;
+    bool place;
     {
         std::lock_guard<std::mutex> g(g_numa_mu);
-        if (!g_numa_count) return;
-        // "numa_pin" 0 after threads were placed: back onto every CPU the process had
-        s = tuning_get(SD_TUNE_NUMA_PIN) != 0 ? g_numa_set : g_numa_all;
+        place = g_numa_count > 0 && tuning_get(SD_TUNE_NUMA_PIN) != 0;
+        s = g_numa_set;
     }
-    (void)sched_setaffinity(0, sizeof s, &s);  // best effort: a refused mask leaves the thread as it was
+    if (!place) {
+        // "numa_pin" 0 (the default): a thread this library never placed keeps whatever mask
+        // its creator gave it; one placed earlier goes back to its own mask from before
+        if (t_placed) {
+            (void)sched_setaffinity(0, sizeof t_orig_mask, &t_orig_mask);
+            t_placed = false;
+        }
+        return;
+    }
+    if (!t_placed) {  // remember this thread's own mask, to narrow it and to restore it
+        CPU_ZERO(&t_orig_mask);
+        if (sched_getaffinity(0, sizeof t_orig_mask, &t_orig_mask) != 0) return;
+    }
+    cpu_set_t both;
+    CPU_AND(&both, &s, &t_orig_mask);  // never widen a thread beyond its own mask
+    if (CPU_COUNT(&both) == 0) return;  // none of the node's CPUs is this thread's: leave it
+    if (sched_setaffinity(0, sizeof both, &both) == 0) t_placed = true;  // best effort
 }
 
 void sd_set_err(const char* fmt, ...) {

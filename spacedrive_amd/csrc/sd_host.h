@@ -71,24 +71,35 @@ enum sd_tune_key {
 int tuning_get(int key);
 
 // ------------------------------------------------------------------ host thread budget
-// The host threads one call of this process may run at once: the
-// CPUs the process may use -- min(its affinity mask, its cgroup's CPU bandwidth quota) --
-// divided by the GPU ranks that share the node's host (LOCAL_WORLD_SIZE, which
-// torch.distributed.run sets; 1 when absent), at least 1.  "host_cpu_budget" > 0 replaces
-// the resolved value (a Rust host that knows its own share sets it).  Every pool size,
-// reader count and co-hash thread count is capped by it.
+// The host threads one call of this process may run at once, at least
+// 1: min(the affinity share, the quota share), where
+//   * the affinity share is the CPUs in the process's affinity mask -- divided by the GPU
+//     ranks sharing the node (LOCAL_WORLD_SIZE, which torch.distributed.run sets; 1 when
+//     absent) only when the mask holds every online CPU; a narrower mask is a per-rank
+//     binding and already this rank's own;
+//   * the quota share is the cgroup CPU bandwidth quota, rounded up, divided by those
+//     ranks: every rank of the container draws on the one quota.  The quota is the
+//     tightest limit on the path from the process's own cgroup (/proc/self/cgroup) up to
+//     the mount root.
+// "host_cpu_budget" > 0 replaces the resolved value (a Rust host that knows its own share
+// sets it).  Every pool size, reader count and co-hash thread count is capped by it.
 struct CpuBudget {
     int budget = 1;       // the cap
     int affinity = 1;     // CPUs in sched_getaffinity
+    int online = 1;       // CPUs online on the machine
     int quota_milli = 0;  // cgroup CPU quota in milli-CPUs (0 = no limit)
     int local_world = 1;  // ranks per node sharing the host
     int overridden = 0;   // 1 when "host_cpu_budget" set the cap
 };
-// pure arithmetic of the rule (host_selftest checks it with fake quotas and world sizes)
-CpuBudget cpu_budget_resolve(int affinity, double quota_cpus, int local_world);
-// the CPU bandwidth limit of the cgroup mounted at `root` (v2 cpu.max, else v1
+// pure arithmetic of the rule (host_selftest checks it with fake masks, quotas and world sizes)
+CpuBudget cpu_budget_resolve(int affinity, int online, double quota_cpus, int local_world);
+// the CPU bandwidth limit of the cgroup directory `root` (v2 cpu.max, else v1
 // cpu/cpu.cfs_quota_us / cpu.cfs_period_us), in CPUs; 0 when unlimited or unreadable
 double cgroup_cpu_quota(const char* root);
+// the tightest limit over the mount root and every directory from the process's own cgroup
+// (read from `proc_cgroup`, default /proc/self/cgroup) up to it; `root` defaults to
+// /sys/fs/cgroup.  0 when none is set
+double cgroup_cpu_quota_self(const char* root, const char* proc_cgroup);
 CpuBudget host_cpu_budget_detail();  // resolved once per process, then the override applied
 int host_cpu_budget();
 inline int cap_host_threads(int n) {
@@ -98,7 +109,8 @@ inline int cap_host_threads(int n) {
 
 // ------------------------------------------------------------------ NUMA placement
 // With "numa_pin" 1 (opt-in) the library's own threads (pool workers, co-hashing threads)
-// run on the CPUs of the GPU's NUMA node, within the process's affinity mask.  When the
+// run on the CPUs of the GPU's NUMA node, within each thread's own affinity mask; with 0 a
+// thread is never touched, and one placed earlier gets its own mask back.  When the
 // files' page cache was written on that node too, it pays (scripts/numa_probe.sh: the CPU
 // path 90 vs 77 GB/s, the split checksum 106 vs 100 GB/s); with the page cache where an
 // unplaced writer left it -- the usual case -- it measured neutral (0.93-1.04x,

@@ -298,7 +298,9 @@ def test_host_cpu_budget_caps_and_override():
 
 def test_host_cpu_budget_divides_by_local_world_size():
     """Each of the node's ranks gets its share: a process started as one of 4 local ranks
-    (LOCAL_WORLD_SIZE=4, as torch.distributed.run sets it) resolves min(affinity, quota) / 4."""
+    (LOCAL_WORLD_SIZE=4, as torch.distributed.run sets it) resolves min(affinity share,
+    quota / 4), the affinity split only when the mask holds every online CPU (a narrower
+    mask is a per-rank binding)."""
     import math
     import sys
     code = ("import os, json, spacedrive_amd as sd; "
@@ -308,10 +310,35 @@ def test_host_cpu_budget_divides_by_local_world_size():
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__)))).stdout
     import json
     b = json.loads(out.strip().splitlines()[-1])
-    cpus = b["affinity"]
+    aff = b["affinity"]
+    cpus = aff // 4 if aff >= os.cpu_count() else aff
     if b["cgroup_quota_cpus"]:
-        cpus = min(cpus, max(1, math.ceil(b["cgroup_quota_cpus"] - 1e-9)))
-    assert b["local_world_size"] == 4 and b["budget"] == max(1, cpus // 4)
+        cpus = min(cpus, max(1, math.ceil(b["cgroup_quota_cpus"] - 1e-9)) // 4)
+    assert b["local_world_size"] == 4 and b["budget"] == max(1, cpus)
+
+
+def test_host_cpu_budget_keeps_a_bound_ranks_mask():
+    """A rank bound to its own CPUs (taskset / numactl / --cpu-bind: a mask narrower than
+    the machine) keeps that mask as its share; it is not divided by LOCAL_WORLD_SIZE a second
+    time."""
+    import json
+    import sys
+    cpus = sorted(os.sched_getaffinity(0))
+    if len(cpus) < 2 or len(cpus) < os.cpu_count():
+        pytest.skip("needs an unbound process on a machine of >= 2 CPUs")
+    mine = cpus[:2]
+    code = ("import os, json; os.sched_setaffinity(0, %r); import spacedrive_amd as sd; "
+            "print(json.dumps(sd.host_cpu_budget()))" % (mine,))
+    env = dict(os.environ, LOCAL_WORLD_SIZE="8")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__)))).stdout
+    b = json.loads(out.strip().splitlines()[-1])
+    assert b["affinity"] == 2
+    want = 2
+    if b["cgroup_quota_cpus"]:
+        import math
+        want = min(want, max(1, math.ceil(b["cgroup_quota_cpus"] - 1e-9) // 8))
+    assert b["budget"] == max(1, want)
 
 
 def test_host_numa_without_a_context_places_nothing():

@@ -60,3 +60,115 @@ def test_effective_cpus_within_the_affinity_mask_and_quota():
     q = bench.host_cpu()["cgroup_cpu_quota"]
     if q:
         assert n <= int(np.ceil(q))
+
+
+# ------------------------------------------------------------------ --gpus N launcher
+def test_launch_mode_rules():
+    """--gpus N without WORLD_SIZE starts N ranks; under a launcher the
+    rank count must equal --gpus; --gpus 1 stays in-process."""
+    assert bench.launch_mode(1, {}) == "inprocess"
+    assert bench.launch_mode(2, {}) == "spawn"
+    assert bench.launch_mode(8, {}) == "spawn"
+    assert bench.launch_mode(8, {"WORLD_SIZE": "8"}) == "rank"
+    assert bench.launch_mode(1, {"WORLD_SIZE": "1"}) == "rank"
+    for gpus, ws in ((8, "1"), (1, "8"), (2, "4")):
+        with pytest.raises(SystemExit) as e:
+            bench.launch_mode(gpus, {"WORLD_SIZE": ws})
+        assert "WORLD_SIZE" in str(e.value) and f"--gpus {gpus}" in str(e.value)
+    with pytest.raises(SystemExit):
+        bench.launch_mode(0, {})
+
+
+def test_launcher_cmd_is_the_drivers_command():
+    cmd = bench.launcher_cmd(4, ["--gpus", "4", "--steps", "5"], 29555)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    i = cmd.index("--nproc-per-node")
+    assert cmd[i + 1] == "4"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[cmd.index("--master-port") + 1] == "29555"
+    assert cmd[cmd.index("--nnodes") + 1] == "1"
+    assert cmd[-5] == os.path.join(ROOT, "bench.py") and cmd[-4:] == ["--gpus", "4", "--steps", "5"]
+
+
+def test_bench_refuses_a_world_size_mismatch():
+    """The real entry point: WORLD_SIZE=2 with --gpus 8 exits non-zero before any GPU work."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr and r.stdout == ""
+
+
+def test_spawn_relays_rank0_line_and_exit_code(tmp_path):
+    """spawn_ranks runs the launcher as a child, relays its JSON line to stdout (other stdout
+    to stderr) and returns its exit code; a child that exits 0 without a line is a failure.
+    A stand-in launcher prints what rank 0 would."""
+    import subprocess
+    script = tmp_path / "fake_launcher.py"
+    script.write_text("import sys\nprint('banner')\nprint('{\"metric\": \"m\", \"n_gpus\": 2}')\n"
+                      "sys.exit(int(sys.argv[1]))\n")
+    for rc in (0, 3):
+        r = subprocess.run([sys.executable, "-c",
+                            "import sys; sys.path.insert(0, %r); import bench\n"
+                            "bench.launcher_cmd = lambda g, a, p: [sys.executable, %r, a[0]]\n"
+                            "sys.exit(bench.spawn_ranks(2, [%r]))" % (ROOT, str(script), str(rc))],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == rc
+        assert r.stdout.strip() == '{"metric": "m", "n_gpus": 2}'
+        assert "banner" in r.stderr and "banner" not in r.stdout
+    script.write_text("print('no line')\n")
+    r = subprocess.run([sys.executable, "-c",
+                        "import sys; sys.path.insert(0, %r); import bench\n"
+                        "bench.launcher_cmd = lambda g, a, p: [sys.executable, %r]\n"
+                        "sys.exit(bench.spawn_ranks(2, []))" % (ROOT, str(script))],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and r.stdout == ""
+
+
+# ------------------------------------------------------------------ multi-GiB goldens
+def test_bench_goldens_cover_every_rank_of_the_default_run():
+    g = bench.golden_checksums()
+    flen = (64 << 30) // 16
+    for r in range(8):
+        start = r * 1_250_000
+        for i in (0, 15):
+            assert f"{10_000 + start + i}:{flen}" in g["synth"]
+        m = g["mixed"][f"{start}:{16 * flen}"]
+        offs, lens = bench.mixed_layout(start, 16 * flen)
+        mi = min(range(len(lens)), key=lambda k: lens[k])
+        assert (m["index"], m["offset"], m["len"]) == (mi, offs[mi], lens[mi])
+    assert f"20000:{(32 << 30) + 12345}" in g["synth"]
+
+
+@pytest.mark.parametrize("which", ["configs3", "mixed"])
+def test_bench_goldens_equal_the_oracle(oracle_native, which):
+    """Re-derives goldens with the oracle: rank 1's configs[3] file 15 (4 GiB), and rank 0's
+    shortest mixed file (2.2 GiB spanning two generated files).  The rest were made by the
+    same code (make_bench_golden.py); the split file's 32 GiB hash equals round 4's GPU run
+    (profiles/r4/r4y_bench.json checksum_one_file.hash)."""
+    g = bench.golden_checksums()
+    flen = (64 << 30) // 16
+    nt = min(8, os.cpu_count() or 1)
+    if which == "configs3":
+        cid = 10_000 + 1_250_000 + 15
+        assert oracle_native.checksum_synth_mt(flen, cid, 0, nthreads=nt).hex() == g["synth"][f"{cid}:{flen}"]
+        want, src = bench.synth_checksum_expected(cid, flen, live=False)
+        assert src == "golden" and want == g["synth"][f"{cid}:{flen}"]
+    else:
+        m = g["mixed"][f"0:{16 * flen}"]
+        assert bench.mixed_host_checksum(0, m["offset"], m["len"], flen, nt).hex() == m["hash"]
+
+
+def test_bench_golden_lookup_falls_back_to_the_oracle(oracle_native):
+    """A file the goldens do not hold (a non-default size) is hashed by the oracle live."""
+    want, src = bench.synth_checksum_expected(10_000, 3 << 20, live=False)
+    assert src == "oracle (live)"
+    assert want == oracle_native.checksum_synth_mt(3 << 20, 10_000, 0, nthreads=2).hex()
+
+
+def test_timing_laps_add_up():
+    tm = bench.Timing()
+    tm.lap("a")
+    tm.lap("b")
+    tm.lap("a")
+    assert set(tm) == {"a", "b"} and all(v >= 0 for v in tm.values())
