@@ -24,9 +24,16 @@
 // Build (on the CPU container; runs on the GPU box):
 //   hipcc -O2 -std=c++17 -mavx2 -o scripts/ck_host_cost scripts/ck_host_cost.cpp \
 //         -Lspacedrive_amd -lsdcas -Wl,-rpath,'$ORIGIN/../spacedrive_amd' -lpthread
-// Run: scripts/ck_host_cost [NF=32] [FL_MiB=256] [ghz=2.4] [quick]  -> JSON lines on stdout
+// Run: scripts/ck_host_cost [NF=32] [FL_MiB=256] [ghz=2.4] [quick|bound]  -> JSON lines on stdout
 // ("quick": read_hash, read_hot_nt_dma and the hot_nt split at 16 threads only, for A/Bs
-// such as scripts/numa_probe.sh's thread placements)
+// such as scripts/numa_probe.sh's thread placements; "bound", VERDICT r4 item 3: what bounds
+// the split -- STREAM-like host DRAM legs on 16 threads (read, non-temporal write, copy), the
+// split's own memory traffic with the CPU half's hashing removed (hybrid_nohash: g threads
+// of the GPU route's read_hot_nt + DMA, 16 - g of read_hot), the split itself (hybrid_hot_nt)
+// and its CPU half alone on 16 - g threads, each line with its DRAM passes per byte moved:
+// read_hot / read_hash 1 (the page-cache read; the per-thread buffer stays in cache),
+// read_hot_nt + DMA 3 (page-cache read, streaming write to pinned memory, the device's DMA
+// read), stream_read 1, stream_nt_write 1, stream_copy_nt 2)
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
@@ -118,9 +125,48 @@ void make_files() {
 struct Res {
     double wall = 0, cpu = 0;
     uint64_t bytes = 0;
+    uint64_t bytes_dma = 0;  // of which the threads that DMA'd them to the device moved
 };
 
 enum Kind { READ_PINNED, READ_HOT_NT, READ_HASH, READ_HOT, HASH_HOT, ZERO_COPY };
+
+// STREAM-like legs over an anonymous buffer, T threads, each its contiguous slice (first
+// touched by that thread): kind 0 = read (AVX2 loads, summed), 1 = non-temporal write,
+// 2 = copy with non-temporal stores (a read + a write per byte).  Returns bytes moved per
+// second counting each byte once (a copy of n bytes = n).
+double stream_leg(int kind, int T, uint8_t* a, uint8_t* b, uint64_t len, int reps) {
+    std::vector<std::thread> th;
+    std::atomic<uint64_t> sink{0};
+    const uint64_t per = len / (uint64_t)T / 4096 * 4096;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+            uint8_t* x = a + per * (uint64_t)t;
+            uint8_t* y = b + per * (uint64_t)t;
+            __m256i acc = _mm256_setzero_si256();
+            for (int r = 0; r < reps; r++) {
+                if (kind == 0) {
+                    for (uint64_t o = 0; o < per; o += 64) {
+                        acc = _mm256_add_epi64(acc, _mm256_load_si256(reinterpret_cast<const __m256i*>(x + o)));
+                        acc = _mm256_add_epi64(acc, _mm256_load_si256(reinterpret_cast<const __m256i*>(x + o + 32)));
+                    }
+                } else if (kind == 1) {
+                    const __m256i v = _mm256_set1_epi64x(r + 1);
+                    for (uint64_t o = 0; o < per; o += 64) {
+                        _mm256_stream_si256(reinterpret_cast<__m256i*>(x + o), v);
+                        _mm256_stream_si256(reinterpret_cast<__m256i*>(x + o + 32), v);
+                    }
+                    _mm_sfence();
+                } else {
+                    nt_copy(y, x, per);
+                }
+            }
+            sink += (uint64_t)_mm256_extract_epi64(acc, 0);
+        });
+    for (auto& x : th) x.join();
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return (double)per * T * reps / wall / 1e9 + (sink.load() == 42 ? 1e-12 : 0.0);
+}
 const char* NAMES[] = {"read_pinned", "read_hot_nt", "read_hash", "read_hot", "hash_hot", "zero_copy"};
 
 struct ThreadBufs {
@@ -149,7 +195,7 @@ Res run(const std::vector<int>& kinds, const std::vector<int>& dma, std::vector<
     const uint64_t per_file = FL / UNIT, units = per_file * (uint64_t)NF;
     std::atomic<uint64_t> cursor{0};
     std::vector<double> cpu(T, 0);
-    std::atomic<uint64_t> total{0};
+    std::atomic<uint64_t> total{0}, total_dma{0};
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < T; t++)
@@ -226,6 +272,7 @@ Res run(const std::vector<int>& kinds, const std::vector<int>& dma, std::vector<
                     HIPOK(hipEventRecord(B.ev[b], B.s));
                     B.pending[b] = true;
                     b ^= 1;
+                    total_dma += UNIT;
                 }
                 total += UNIT;
             }
@@ -243,14 +290,21 @@ Res run(const std::vector<int>& kinds, const std::vector<int>& dma, std::vector<
     r.wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     for (double c : cpu) r.cpu += c;
     r.bytes = total.load();
+    r.bytes_dma = total_dma.load();
     return r;
 }
 
 void report(const char* name, int T, int g, const Res& r) {
     const double ns_b = r.cpu * 1e9 / (double)r.bytes;
+    // DRAM passes: a byte DMA'd after read_hot_nt 3 (page-cache read, streaming write, DMA
+    // read); any other byte 1 (the page-cache read) -- read_pinned's DMA'd bytes are not
+    // counted this way (its pread writes the pinned window through the cache)
+    const double dram = ((double)r.bytes_dma * 3 + (double)(r.bytes - r.bytes_dma)) / r.wall / 1e9;
     printf("{\"mode\": \"%s\", \"threads\": %d, \"gpu_route_threads\": %d, \"GBps\": %.2f, \"cpu_ns_per_byte\": %.4f, "
-           "\"cycles_per_byte\": %.3f, \"cpu_s\": %.3f, \"wall_s\": %.3f, \"bytes\": %llu}\n",
-           name, T, g, (double)r.bytes / r.wall / 1e9, ns_b, ns_b * GHZ, r.cpu, r.wall, (unsigned long long)r.bytes);
+           "\"cycles_per_byte\": %.3f, \"cpu_s\": %.3f, \"wall_s\": %.3f, \"bytes\": %llu, \"gpu_share\": %.3f, "
+           "\"dram_GBps\": %.2f}\n",
+           name, T, g, (double)r.bytes / r.wall / 1e9, ns_b, ns_b * GHZ, r.cpu, r.wall, (unsigned long long)r.bytes,
+           r.bytes ? (double)r.bytes_dma / (double)r.bytes : 0.0, dram);
     fflush(stdout);
 }
 }  // namespace
@@ -277,6 +331,43 @@ int main(int argc, char** argv) {
     }
     // page cache warm (the files were just written) -- one untimed pass anyway
     run(std::vector<int>(TMAX, READ_HOT), std::vector<int>(TMAX, 0), bufs);
+    const bool bound = argc > 4 && strcmp(argv[4], "bound") == 0;
+    if (bound) {
+        const uint64_t SLEN = 4ull << 30;  // two 4 GiB anonymous buffers: far past the caches
+        uint8_t* sa = static_cast<uint8_t*>(aligned_alloc(4096, SLEN));
+        uint8_t* sb = static_cast<uint8_t*>(aligned_alloc(4096, SLEN));
+        stream_leg(1, TMAX, sa, sb, SLEN, 1);  // first touch by the threads that use the slices
+        stream_leg(1, TMAX, sb, sa, SLEN, 1);
+        for (int rep = 0; rep < 3; rep++) {
+            for (int T : {8, 16}) {
+                const char* names[3] = {"stream_read", "stream_nt_write", "stream_copy_nt"};
+                const int passes[3] = {1, 1, 2};
+                for (int k = 0; k < 3; k++) {
+                    const double g = stream_leg(k, T, sa, sb, SLEN, 3);
+                    printf("{\"mode\": \"%s\", \"threads\": %d, \"GBps\": %.2f, \"dram_passes\": %d, "
+                           "\"dram_GBps\": %.2f, \"rep\": %d}\n", names[k], T, g, passes[k], g * passes[k], rep);
+                    fflush(stdout);
+                }
+            }
+            for (int g : {3, 4, 6}) {
+                std::vector<int> kinds(TMAX, READ_HOT), dma(TMAX, 0);
+                for (int t = 0; t < g; t++) kinds[t] = READ_HOT_NT, dma[t] = 1;
+                report("hybrid_nohash", TMAX, g, run(kinds, dma, bufs));
+                std::vector<int> kinds2(TMAX, READ_HASH), dma2(TMAX, 0);
+                for (int t = 0; t < g; t++) kinds2[t] = READ_HOT_NT, dma2[t] = 1;
+                report("hybrid_hot_nt", TMAX, g, run(kinds2, dma2, bufs));
+                report("read_hash", TMAX - g, 0, run(std::vector<int>(TMAX - g, READ_HASH), std::vector<int>(TMAX - g, 0), bufs));
+                report("read_hot_nt_dma", g, g, run(std::vector<int>(g, READ_HOT_NT), std::vector<int>(g, 1), bufs));
+            }
+            report("read_hot", TMAX, 0, run(std::vector<int>(TMAX, READ_HOT), std::vector<int>(TMAX, 0), bufs));
+            report("read_hash", TMAX, 0, run(std::vector<int>(TMAX, READ_HASH), std::vector<int>(TMAX, 0), bufs));
+        }
+        free(sa);
+        free(sb);
+        for (int f = 0; f < NF; f++) unlink(path_of(f).c_str());
+        rmdir(DIR.c_str());
+        return 0;
+    }
     if (quick) {
         for (int rep = 0; rep < 3; rep++) {
             report("read_hash", TMAX, 0, run(std::vector<int>(TMAX, READ_HASH), std::vector<int>(TMAX, 0), bufs));

@@ -39,8 +39,9 @@ constexpr int sigma(int r, int i) { return r == 0 ? i : sigma(r - 1, PERM[i]); }
 
 // rotr(d ^ a, 16) as two VOP2-SDWA xors that write the two 16-bit halves crosswise:
 // both are 2-source ops, where xor + v_alignbit pays one 3-source op (half issue rate on
-// gfx950).  scripts/valu_probe4.hip: 39.4 vs 38.5 T baseline lane-ops/s on four
-// independent G columns (profiles/r2/r2z4_valu_probe4.txt).  Not volatile: the compiler
+// gfx950).  scripts/valu_probe7.hip at 8 waves/SIMD: 39.51 vs 38.49 T lane-ops/s for the G
+// mix (profiles/r3/r3c_valu_probe7.txt; first seen with archive/scripts/valu_probe4.hip,
+// profiles/r2/r2z4_valu_probe4.txt).  Not volatile: the compiler
 // still schedules it; the early-clobber output keeps d and a readable by the second xor.
 #ifndef SD_ROTR16_SDWA
 #define SD_ROTR16_SDWA 1
@@ -58,11 +59,28 @@ __device__ __forceinline__ uint32_t xor_rotr16(uint32_t d, uint32_t a) {
 #endif
 }
 
-#define SD_G(a, b, c, d, x, y)            \
-    a = a + b + (x); d = xor_rotr16(d, a); \
-    c = c + d;       b = rotr(b ^ c, 12); \
-    a = a + b + (y); d = rotr(d ^ a, 8);  \
-    c = c + d;       b = rotr(b ^ c, 7);
+// a + b + m.  Default: one v_add3_u32 (3 sources, half issue rate).  SD_ADD3_SPLIT=1: two
+// 2-source v_add_u32 (full rate each; the first held in asm so the compiler cannot fuse
+// them back) -- the one op-level lever the issue probes found (scripts/valu_probe7.hip,
+// profiles/r3/r3c_valu_probe7.txt: 39.88 vs 39.51 T for the G mix at 8 waves/SIMD).
+#ifndef SD_ADD3_SPLIT
+#define SD_ADD3_SPLIT 0
+#endif
+__device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t m) {
+#if SD_ADD3_SPLIT
+    uint32_t t;
+    asm("v_add_u32 %0, %1, %2" : "=v"(t) : "v"(a), "v"(b));
+    return t + m;
+#else
+    return a + b + m;
+#endif
+}
+
+#define SD_G(a, b, c, d, x, y)              \
+    a = add3(a, b, (x)); d = xor_rotr16(d, a); \
+    c = c + d;           b = rotr(b ^ c, 12); \
+    a = add3(a, b, (y)); d = rotr(d ^ a, 8);  \
+    c = c + d;           b = rotr(b ^ c, 7);
 
 template <int R>
 __device__ __forceinline__ void round_r(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
