@@ -1540,6 +1540,112 @@ def test_split_checksum_mgpu_in_process_ranks(ctx, oracle_native):
                 c.close()
 
 
+def _need_devices(k):
+    if torch.cuda.device_count() < k:
+        pytest.skip(f"needs {k} visible GPUs (the pool's boxes have one): the in-process communicator's "
+                    "cross-device copies are untested there")
+
+
+@pytest.mark.parametrize("R", [2, 4])
+def test_dedup_mgpu_in_process_ranks_across_devices(R):
+    """The in-process communicator with its ranks on DIFFERENT devices of one process
+    (README: several GPUs from one process): each rank's shard, context,
+    stream and output on device r % ndev, the exchange's peer copies (hipMemcpyDefault)
+    crossing devices.  Each rank's groups, representatives and Object owners == the host
+    grouping.  Skipped where fewer than two GPUs are visible."""
+    _need_devices(2)
+    from spacedrive_amd import dedup
+    from spacedrive_amd.dedup import dest_of
+    from spacedrive_amd.device import Comm, CommGroup, Context
+    from spacedrive_amd.identifier import object_owners
+    ndev = torch.cuda.device_count()
+    n = 60000
+    sizes, cids, twins = synth.library(0, n, n, dup_frac=0.3)
+    c0 = Context(0)
+    try:
+        h = gpu_cas(c0, sizes, cids, twins)
+    finally:
+        c0.close()
+    valid = sizes != 0
+    keys = keys_from_hashes(h)
+    cuts = [0] + [int(c) for c in np.cumsum(np.random.default_rng(R).dirichlet(np.ones(R)) * n)[:-1]] + [n]
+    group = CommGroup(R)
+    ctxs = [Context(r % ndev) for r in range(R)]
+    comms = [Comm(ctxs[r], None, R, r, group=group) for r in range(R)]
+    all_recs = np.stack([keys[valid].view(np.int64), np.arange(n)[valid]], axis=1)
+    dst = dest_of(all_recs[:, 0].view(np.uint64), R)
+
+    def rank_call(r):
+        lo, hi = cuts[r], cuts[r + 1]
+        dev = torch.device("cuda", r % ndev)
+        with torch.cuda.device(dev):
+            d_hash = torch.from_numpy(h[lo:hi].reshape(-1).copy()).to(dev)
+            d_valid = torch.from_numpy(valid[lo:hi].astype(np.uint8)).to(dev)
+            st = torch.cuda.Stream(device=dev)
+            runner = dedup.RcclDedup(ctxs[r], comms[r], dev, capacity=n)
+            recs, rep, ng, own = runner(d_hash, d_valid, hi - lo, lo, stream=st)
+            st.synchronize()
+            assert recs.device == dev
+            return recs.cpu().numpy(), rep.cpu().numpy(), ng, own.cpu().numpy()
+
+    try:
+        got = _run_ranks(R, rank_call)
+        assert sum(len(g[0]) for g in got) == int(valid.sum())
+        for r in range(R):
+            gr, grep, gng = group_host(all_recs[dst == r])
+            want_owner = object_owners(torch.from_numpy(gr[:, 1].copy()), torch.from_numpy(grep), 100).numpy()
+            recs, rep, ng, own = got[r]
+            assert ng == gng and np.array_equal(recs, gr) and np.array_equal(rep, grep)
+            assert np.array_equal(own, want_owner)
+    finally:
+        for c in comms:
+            c.close()
+        group.close()
+        for c in ctxs:
+            c.close()
+
+
+def test_split_checksum_mgpu_in_process_ranks_across_devices(oracle_native):
+    """sd_split_checksum_mgpu over in-process ranks on different devices: each rank's slice
+    and CV buffer on its own device, the in-place all-gather copying CV slots across
+    devices; every rank's root == the oracle.  Skipped where fewer than two GPUs are
+    visible."""
+    _need_devices(2)
+    from spacedrive_amd.device import Comm, CommGroup, Context, SplitChecksum
+    ndev = torch.cuda.device_count()
+    R = max(2, min(4, ndev))
+    total = (37 << 20) + 501
+    want = oracle_native.checksum_synth_mt(total, 903, 0, nthreads=NT).hex()
+    group = CommGroup(R)
+    ctxs = [Context(r % ndev) for r in range(R)]
+    comms = [Comm(ctxs[r], None, R, r, group=group) for r in range(R)]
+
+    def rank(r):
+        dev = torch.device("cuda", r % ndev)
+        with torch.cuda.device(dev):
+            sc = SplitChecksum(ctxs[r], total, R, r)
+            d = torch.zeros(sc.len + 128, dtype=torch.uint8, device=dev)
+            if sc.len:
+                ctxs[r].synth_fill(903, 0, sc.len, d, offset=sc.offset)
+            cvs = torch.zeros(sc.cv_bytes, dtype=torch.uint8, device=dev)
+            out = torch.zeros(32, dtype=torch.uint8, device=dev)
+            st = torch.cuda.Stream(device=dev)
+            torch.cuda.synchronize(dev)
+            sc.mgpu(comms[r], d, cvs, out, stream=st)
+            st.synchronize()
+            sc.close()
+            return bytes(out.cpu().numpy()).hex()
+
+    try:
+        assert _run_ranks(R, rank) == [want] * R
+    finally:
+        for c in comms:
+            c.close()
+        group.close()
+        for c in ctxs:
+            c.close()
+
+
 @pytest.mark.parametrize("route", ["batch", "single-gpu"])
 def test_pipe_whole_kind_reads_every_byte(ctx, tmp_path, oracle_native, route):
     """generate_cas_id on a pipe (a metadata length of 0, as non_indexed passes for one):
