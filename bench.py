@@ -677,10 +677,13 @@ def checksum_host(ctx, gib: int, dev, stream):
     out = ctypes.create_string_buffer(65 * nf)
     keep = sd.get_tuning("host_cohash_threads")
     e2e = {}
+    st0, st1 = np.zeros(2, np.uint64), np.zeros(2, np.uint64)
     for mode, h in (("gpu_only", 0), ("default", keep)):
         sd.set_tuning("host_cohash_threads", h)
         try:
             runs = []
+            if mode == "default":
+                check(lib().sd_checksums_stats(ctx.handle, st0.ctypes.data))
             for _ in range(3):  # the first call allocates the context's windows
                 ctypes.memset(out, 0, 65 * nf)
                 t0 = time.perf_counter()
@@ -688,10 +691,14 @@ def checksum_host(ctx, gib: int, dev, stream):
                 runs.append(time.perf_counter() - t0)
         finally:
             sd.set_tuning("host_cohash_threads", keep)
+        if mode == "default":
+            check(lib().sd_checksums_stats(ctx.handle, st1.ctypes.data))
         raw = out.raw
         got = [raw[65 * i:65 * i + 64].decode() for i in range(nf)]
         assert got == want, f"sd_checksums ({mode}) differs from the device-resident batch"
         e2e[mode] = min(runs)
+    d_gpu, d_host = (int(x) for x in (st1 - st0))
+    host_share = d_host / (d_gpu + d_host) if d_gpu + d_host else None
     e2e_s = e2e["default"]
     from oracle import native
     bad = sum(native.checksum_synth_mt(flen, 20_000 + i, 0, nthreads=oracle_threads()).hex() != got[i]
@@ -727,6 +734,7 @@ def checksum_host(ctx, gib: int, dev, stream):
     return {"files": nf, "bytes": total, "h2d_ms": h2d_ms, "h2d_GBps": total / (h2d_ms * 1e-3) / 1e9, "parity": par,
             "kernel_ms": kernel_ms, "kernel_GBps": total / (kernel_ms * 1e-3) / 1e9,
             "end_to_end_ms": e2e_s * 1e3, "end_to_end_GBps": total / e2e_s / 1e9, "host_cohash_threads": keep,
+            "host_share": host_share,
             "gpu_only": {"end_to_end_ms": e2e["gpu_only"] * 1e3, "end_to_end_GBps": total / e2e["gpu_only"] / 1e9},
             "library_cpu_path": {"threads": cpu_t, "GBps": total / min(cpu_runs) / 1e9,
                                  "parity": parity(nf, cpu_bad, "sd_cpu_checksums of each range vs sd_checksums' "
@@ -742,7 +750,8 @@ def checksum_host(ctx, gib: int, dev, stream):
             "note": f"sd_checksums over {nf} x 1 GiB of pinned host memory (best of 3): 256 MiB windows, H2D on one "
                     "copy queue overlapping the kernels on two slot streams, with the library default of "
                     "host_cohash_threads host threads hashing ranges from the end meanwhile, one range shared "
-                    "block by block where the two sides meet (gpu_only: 0); "
+                    "block by block where the two sides meet (gpu_only: 0; host_share = the bytes those threads "
+                    "hashed over the 3 default calls, sd_checksums_stats); "
                     "h2d_ms = one raw copy; kernel_ms = device-resident"}
 
 
@@ -1336,6 +1345,43 @@ def mixed_host_checksum(start: int, off: int, ln: int, flen: int, nthreads: int)
     return native.checksum_mt(buf, ln, nthreads=nthreads)
 
 
+def end_to_end_summary(out: dict) -> dict:
+    """The end-to-end rows beside the library's own CPU path on the same host threads, with
+    the share of the work host threads did in each, copied into
+    cpu_baseline so the driver's record keeps them."""
+    s = {}
+    h = out.get("with_h2d", {})
+    if "cas" in h and "library_cpu_path" in h["cas"]:
+        c = h["cas"]
+        s["with_h2d_cas"] = {"unit": "files/s", "default": c["end_to_end_files_per_s"],
+                             "gpu_only": c["gpu_only"]["end_to_end_files_per_s"],
+                             "library_cpu_path": c["library_cpu_path"]["files_per_s"],
+                             "ratio": c["library_cpu_path"]["default_over_cpu_path"],
+                             "host_share": c.get("host_share"), "host_threads": c.get("host_cohash_threads")}
+    if "checksum" in h and "library_cpu_path" in h["checksum"]:
+        c = h["checksum"]
+        s["with_h2d_checksum"] = {"unit": "GB/s", "default": c["end_to_end_GBps"],
+                                  "gpu_only": c["gpu_only"]["end_to_end_GBps"],
+                                  "library_cpu_path": c["library_cpu_path"]["GBps"],
+                                  "ratio": c["default_over_cpu_path"], "host_share": c.get("host_share"),
+                                  "host_threads": c.get("host_cohash_threads")}
+    fb = out.get("file_backed", {})
+    if "gpu" in fb and "library_cpu_path" in fb:
+        s["file_backed_cas"] = {"unit": "files/s", "gpu_route": fb["gpu"]["files_per_s"],
+                                "library_cpu_path": fb["library_cpu_path"]["files_per_s"],
+                                "ratio": fb.get("gpu_over_cpu_path_16_threads"), "host_share_of_hashing": 0.0,
+                                "note": "the GPU route hashes every file on the device; its host threads read"}
+    fc = out.get("file_backed_checksum", {})
+    if "policy_default" in fc and "library_cpu_path" in fc:
+        s["file_backed_checksum"] = {"unit": "GB/s", "default": fc["policy_default"]["GBps"],
+                                     "gpu_route": fc.get("gpu", {}).get("GBps"),
+                                     "library_cpu_path": fc["library_cpu_path"]["GBps"],
+                                     "ratio": fc.get("policy_default_over_cpu_path"),
+                                     "host_share": (1.0 - fc["policy_default"]["gpu_share"])
+                                     if fc["policy_default"].get("gpu_share") is not None else None}
+    return s
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse()
@@ -1763,6 +1809,7 @@ def main():
                                                       files=out["file_backed"]["files"],
                                                       note="reference read schedule from files (page cache)")
         tm.lap("cpu_baseline")
+        out["cpu_baseline"]["end_to_end_vs_library_cpu_path"] = end_to_end_summary(out)
     if comm is not None:
         comm.close()
     total_s = time.perf_counter() - t_main

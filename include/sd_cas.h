@@ -234,6 +234,9 @@ int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
  * predicted meeting point, is shared 1 MiB block by block. */
 int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
                  char* out_hex65);
+/* bytes sd_checksums hashed so far on this context: [0] by the GPU, [1] by the co-hashing
+ * host threads (their share of a call: the host_share of the bench's with-H2D rows) */
+int sd_checksums_stats(sd_cas_ctx* ctx, uint64_t out[2]);
 /* Drop-in: checksums of n files on disk -> 65-byte lowercase hex each (hash.rs:21-23);
  * status[n] required.  Each file is read as hash.rs reads it: 1 MiB read calls until a
  * short one -- for a regular file its bytes up to EOF, read with parallel preads

@@ -134,6 +134,14 @@ def cas_ids_host_stats(device: Optional[int] = None) -> dict:
     return {"gpu_files": int(v[0]), "host_files": int(v[1])}
 
 
+def checksums_host_stats(device: Optional[int] = None) -> dict:
+    """Bytes hashed by sd_checksums (ranges in host memory) on the GPU and by the host threads
+    that co-hash beside it ("host_cohash_threads"), since the context was created."""
+    v = np.zeros(2, np.uint64)
+    check(lib().sd_checksums_stats(default_context(device).handle, _ptr(v)))
+    return {"gpu_bytes": int(v[0]), "host_bytes": int(v[1])}
+
+
 def coalescer_stats(device: Optional[int] = None) -> dict:
     """Latency-path counters of the device's default context: single-file requests, the
     GPU batches they were coalesced into, the largest batch, and requests hashed on the

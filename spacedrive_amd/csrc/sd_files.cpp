@@ -976,6 +976,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     } sh;
     int host_rc = SD_OK;
     std::string host_err;
+    std::atomic<uint64_t> host_bytes{0};  // bytes the host threads hashed (sd_checksums_stats)
     std::thread host;
     struct JoinHost {
         std::thread& t;
@@ -1029,6 +1030,8 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
                             }
                         } done{sh, claim_mu};
                         cpu_block_cvs(data + offsets[sh.idx], lens[sh.idx], u0, u1, sh.cvs.data(), cohash);
+                        host_bytes.fetch_add(std::min(u1 * SD_CK_BLOCK, lens[sh.idx]) - u0 * SD_CK_BLOCK,
+                                             std::memory_order_relaxed);
                         continue;
                     }
                     {
@@ -1059,7 +1062,10 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
                     } else {
                         check_rc(sd_cpu_checksums(data, offsets + b0, lens + b0, b1 - b0, h32.data(), cohash));
                     }
-                    for (size_t q = b0; q < b1; q++) to_hex(h32.data() + 32 * (q - b0), 32, out_hex65 + 65 * q);
+                    for (size_t q = b0; q < b1; q++) {
+                        to_hex(h32.data() + 32 * (q - b0), 32, out_hex65 + 65 * q);
+                        host_bytes.fetch_add(lens[q], std::memory_order_relaxed);
+                    }
                 }
             } catch (const sd_failure& e) {
                 host_rc = e.rc;
@@ -1223,6 +1229,17 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     harvest(1);
     if (host.joinable()) host.join();
     if (host_rc != SD_OK) throw sd_failure(host_rc, host_err);
+    ctx->checksums_host_bytes.fetch_add(host_bytes.load(), std::memory_order_relaxed);
+    ctx->checksums_gpu_bytes.fetch_add(all_bytes - std::min(all_bytes, host_bytes.load()), std::memory_order_relaxed);
+    return SD_OK;
+    SD_GUARD_END
+}
+
+int sd_checksums_stats(sd_cas_ctx* ctx, uint64_t out[2]) {
+    SD_GUARD_BEGIN
+    if (!ctx || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    out[0] = ctx->checksums_gpu_bytes.load(std::memory_order_relaxed);
+    out[1] = ctx->checksums_host_bytes.load(std::memory_order_relaxed);
     return SD_OK;
     SD_GUARD_END
 }
