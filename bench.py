@@ -766,7 +766,8 @@ def warm(fn, stream, ms_target: float) -> float:
     return first
 
 
-def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: float, warm_ms: float):
+def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: float, warm_ms: float,
+               live: bool = False):
     """configs[1] (1 M files <= 100 KiB, whole-content cas_id) or configs[2] (1 M files
     > 100 KiB, sampled cas_id) on this GPU: kernel-only files/s over device-resident
     staged messages, timed with HIP events on the launch stream, plus determinism of the
@@ -798,6 +799,7 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
         kernels, grid = ["k_whole_items", "k_whole_merge8"], whole_grid(b)
         tr = pmc_traffic(kernels[0], grid)
     ps = parity_sample(sizes, cids, twins, h1, 0)
+    pf = full_parity(h1, nfiles, config_digest_key(which, nfiles), lambda: (sizes, cids, twins), live)
     res = {"workload": ("configs[1]: 1M files <= 100 KiB, whole-content cas_id (log-uniform sizes 1..102400)"
                         if which == "small" else
                         "configs[2]: 1M files > 100 KiB, sampled cas_id (log-uniform sizes 102401..4 GiB)"),
@@ -813,7 +815,8 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
            "kernels": kernels, "launch_grid": grid,
            "traffic": tr["bytes"] if tr else None, "deterministic": deterministic,
            "parity": parity(ps["files"], ps["mismatches"], "full 32-byte hashes of an even-stride sample (+ the first "
-                            "32) vs the C oracle (oracle/sd_oracle.c) on the same generator")}
+                            "32) vs the C oracle (oracle/sd_oracle.c) on the same generator"),
+           "parity_full": parity(pf["files"], pf["mismatches"], pf["oracle"], expected_from=pf["expected_from"])}
     del d_staged, h0, h1, b
     torch.cuda.empty_cache()
     assert deterministic, which
@@ -1310,6 +1313,45 @@ def mixed_layout(start: int, total: int):
     return offs, lens
 
 
+def cas_digest(ids8: np.ndarray) -> str:
+    """SHA-256 of n cas_ids (the first 8 hash bytes of each file, in file order): one value
+    that equals the oracle's only if every one of the n cas_ids does."""
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(ids8, np.uint8).tobytes()).hexdigest()
+
+
+def library_digest_key(start: int, n: int, n_total: int) -> str:
+    return f"library:{start}:{n}:{n_total}"
+
+
+def config_digest_key(which: str, n: int) -> str:
+    return f"configs:{which}:{n}"
+
+
+def full_parity(d_hash: torch.Tensor, n: int, key: str, gen, live: bool) -> dict:
+    """ALL n cas_ids of a timed output against the oracle (a 4 096-file sample
+    is 0.4 % of a leg): their SHA-256 against the committed digest of the oracle's cas_ids
+    (tests/golden/bench_checksums.json, make_bench_golden.py), or -- for a workload the
+    goldens do not hold, with --oracle-live, or to locate a mismatch -- the oracle's own
+    cas_ids computed here from gen() = (sizes, cids, twins)."""
+    got = d_hash.view(-1, 32)[:n, :8].cpu().numpy()
+    want_digest = golden_checksums().get("cas_digest", {}).get(key)
+    if want_digest and not live:
+        ok = cas_digest(got) == want_digest
+        if ok:
+            return {"files": n, "mismatches": 0, "oracle": "SHA-256 of all n cas_ids == the committed digest of "
+                                                             "the C oracle's (oracle/sd_oracle_simd.c)",
+                    "expected_from": "golden", "key": key}
+    from oracle import native
+    s, c, t = gen()
+    want = native.cas_ids_synth_simd(s, c, t, nthreads=oracle_threads())
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    return {"files": n, "mismatches": int(len(bad)), "first_bad_index": int(bad[0]) if len(bad) else None,
+            "oracle": "all n cas_ids vs the C oracle's (oracle/sd_oracle_simd.c) on the same generator",
+            "expected_from": "oracle (live)", "key": key,
+            "digest_mismatch": bool(want_digest) and not live}
+
+
 def synth_checksum_expected(cid: int, length: int, live: bool):
     """(hex, source) of BLAKE3 over synthetic file `cid`'s first `length` bytes: the committed
     oracle output when it holds this file, else the C oracle on this host (this rank's share
@@ -1670,6 +1712,15 @@ def main():
     out["parity_sample"] = dict(ps, files=int(bad[1]), mismatches=int(bad[0]), ranks=world,
                                 rank0_first_bad_global_index=ps["first_bad_global_index"])
     out["parity_sample"].pop("first_bad_global_index")
+    # (1b) all of every rank's cas_ids: one digest per shard against the oracle's
+    pf = full_parity(d_hash, n, library_digest_key(start, n, n_total), lambda: (sizes, cids, twins), args.oracle_live)
+    bad = torch.tensor([pf["mismatches"], pf["files"], int(pf["expected_from"] == "golden")], dtype=torch.int64,
+                       device=cdev)
+    if DIST:
+        dist.all_reduce(bad)
+    out["parity_full"] = dict(pf, files=int(bad[1]), mismatches=int(bad[0]), ranks=world,
+                              ranks_from_golden=int(bad[2]))
+    assert out["parity_full"]["mismatches"] == 0, out["parity_full"]
     # (2) the exchange, grouping and Object owners: a key slice from every rank, on rank 0
     out["dedup"]["parity_slice"] = dedup_parity(d_hash, d_valid, n, start, recs, rep, owners, world, dev, transport)
     out["dedup"]["parity"] = out["dedup"]["parity_slice"]["parity"]
@@ -1798,7 +1849,7 @@ def main():
 
     if not DIST and args.config_files > 0:
         out["configs"] = {k: config_leg(ctx, k, args.config_files, args.config_reps, dev, stream, valu_peak,
-                                        args.warm_ms)
+                                        args.warm_ms, live=args.oracle_live)
                           for k in ("small", "sampled")}
         tm.lap("configs_1_2")
 

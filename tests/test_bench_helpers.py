@@ -172,3 +172,44 @@ def test_timing_laps_add_up():
     tm.lap("b")
     tm.lap("a")
     assert set(tm) == {"a", "b"} and all(v >= 0 for v in tm.values())
+
+
+# ------------------------------------------------------------------ full-output parity
+def test_full_parity_digest_and_live(oracle_native, monkeypatch):
+    """full_parity checks every cas_id: against the committed digest when it holds the
+    workload, else (or to locate a mismatch) against the oracle's cas_ids computed live."""
+    import torch
+    n = 3000
+    sizes, cids, twins = synth.library(0, n, 10 * n)
+    ids = oracle_native.cas_ids_synth_simd(sizes, cids, twins, nthreads=4)
+    h = np.zeros((n, 32), np.uint8)
+    h[:, :8] = ids
+    h[:, 8:] = 7  # bytes past the cas_id are not part of it
+    d = torch.from_numpy(h.reshape(-1).copy())
+    gen = lambda: (sizes, cids, twins)  # noqa: E731
+    live = bench.full_parity(d, n, "test:none", gen, live=False)
+    assert live["mismatches"] == 0 and live["expected_from"] == "oracle (live)" and not live["digest_mismatch"]
+    g = dict(bench.golden_checksums())
+    g["cas_digest"] = dict(g.get("cas_digest", {}), **{"test:key": bench.cas_digest(ids)})
+    monkeypatch.setattr(bench, "_golden", g)
+    ok = bench.full_parity(d, n, "test:key", gen, live=False)
+    assert ok["mismatches"] == 0 and ok["expected_from"] == "golden"
+    h[1234, 3] ^= 1
+    bad = bench.full_parity(torch.from_numpy(h.reshape(-1).copy()), n, "test:key", gen, live=False)
+    assert bad["mismatches"] == 1 and bad["first_bad_index"] == 1234 and bad["digest_mismatch"]
+
+
+def test_library_digests_cover_every_rank_of_1_2_4_8():
+    g = bench.golden_checksums()["cas_digest"]
+    for world in (1, 2, 4, 8):
+        for r in range(world):
+            assert bench.library_digest_key(r * 1_250_000, 1_250_000, world * 1_250_000) in g
+    assert bench.config_digest_key("small", 1_000_000) in g and bench.config_digest_key("sampled", 1_000_000) in g
+
+
+def test_library_digest_equals_the_oracle_for_one_shard(oracle_native):
+    """Re-derives one committed shard digest (rank 1 of 2) with the oracle."""
+    s, c, t = synth.library(1_250_000, 1_250_000, 2_500_000)
+    ids = oracle_native.cas_ids_synth_simd(s, c, t, nthreads=min(8, os.cpu_count() or 1))
+    assert bench.cas_digest(ids) == bench.golden_checksums()["cas_digest"][
+        bench.library_digest_key(1_250_000, 1_250_000, 2_500_000)]
