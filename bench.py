@@ -1867,7 +1867,12 @@ def main():
     tot = torch.tensor([total_s], dtype=torch.float64, device=cdev)
     if DIST:
         dist.all_reduce(tot, op=dist.ReduceOp.MAX)
-    out["timing"] = {"rank0_s": dict(tm), "rank0_total_s": round(total_s, 3),
+    try:  # the process's whole life so far: interpreter start, imports, launch included
+        import psutil
+        proc_s = round(time.time() - psutil.Process().create_time(), 3)
+    except Exception:  # noqa: BLE001 -- a diagnostic
+        proc_s = None
+    out["timing"] = {"rank0_s": dict(tm), "rank0_total_s": round(total_s, 3), "rank0_process_s": proc_s,
                      "total_s_max_over_ranks": round(float(tot.item()), 3),
                      "host_threads_budget": _native.host_cpu_budget()["budget"],
                      "note": "wall seconds per leg on rank 0, from main() to the line (the process's import and "
