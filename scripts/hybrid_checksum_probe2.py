@@ -7,6 +7,8 @@ rounds on two tmpfs file sets (the bench's 32 x 256 MiB, and 48 files of 8..320 
   cpu_16                 sd_cpu_file_checksums on 16 threads (the library's CPU path)
   gpu_16[_hot0]          the GPU route alone ("checksum_cpu_max" 0), pread_stream on / off
   hybrid_g[_hot0]        the policy's split, "checksum_hybrid_threads" g
+  *_pK                   the same with "cpu_read_piece_kib" K (round 5: the CPU path reads and
+                         hashes each 1 MiB block K KiB at a time)
 Every call's output is asserted equal to the CPU path's.
 python scripts/hybrid_checksum_probe2.py [rounds] [legs,...] -> one JSON line (per-round rows on stderr)"""
 import ctypes
@@ -24,7 +26,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import spacedrive_amd as sd  # noqa: E402
 from spacedrive_amd._native import check, lib, path_array  # noqa: E402
 
-KNOBS = ("checksum_cpu_max", "checksum_hybrid_threads", "checksum_stage_hot", "read_threads")
+KNOBS = ("checksum_cpu_max", "checksum_hybrid_threads", "checksum_stage_hot", "read_threads", "cpu_read_piece_kib")
 
 
 def write_set(ctx, d, lens, cid0):
@@ -57,6 +59,9 @@ def main():
             st = np.zeros(n, np.int32)
             check(L.sd_cpu_file_checksums(arr, n, out, st.ctypes.data, 16))
             want = out.raw
+            from oracle import native  # the reference answer for the probe's own check
+            ref, _ = native.file_checksums(paths, nthreads=16)
+            assert [want[65 * i:65 * i + 64].decode() for i in range(n)] == [r.tobytes().hex() for r in ref]
 
             def timed(fn, reps=3):
                 best = None
@@ -69,14 +74,21 @@ def main():
                     best = dt if best is None else min(best, dt)
                 return total / best / 1e9
 
-            def cpu16():
-                check(L.sd_cpu_file_checksums(arr, n, out, st.ctypes.data, 16))
+            def cpu16(piece=0):
+                def f():
+                    sd.set_tuning("cpu_read_piece_kib", piece)
+                    try:
+                        check(L.sd_cpu_file_checksums(arr, n, out, st.ctypes.data, 16))
+                    finally:
+                        sd.set_tuning("cpu_read_piece_kib", keep["cpu_read_piece_kib"])
+                return f
 
-            def policy(cpu_max, g, hot):
+            def policy(cpu_max, g, hot, piece=0):
                 def f():
                     sd.set_tuning("checksum_cpu_max", cpu_max)
                     sd.set_tuning("checksum_hybrid_threads", g)
                     sd.set_tuning("checksum_stage_hot", hot)
+                    sd.set_tuning("cpu_read_piece_kib", piece)
                     try:
                         check(L.sd_file_checksums(ctx.handle, arr, n, out, st.ctypes.data))
                     finally:
@@ -84,8 +96,10 @@ def main():
                             sd.set_tuning(k, v)
                 return f
 
-            legs = [("cpu_16", cpu16), ("gpu_16", policy(0, 0, 1)), ("gpu_16_hot0", policy(0, 0, 0))]
+            legs = [("cpu_16", cpu16()), ("gpu_16", policy(0, 0, 1)), ("gpu_16_hot0", policy(0, 0, 0))]
+            legs += [(f"cpu_16_p{k}", cpu16(k)) for k in (64, 128, 256, 512)]
             legs += [(f"hybrid_{g}", policy(2147483647, g, 1)) for g in (2, 3, 4, 5, 6, 8)]
+            legs += [(f"hybrid_{g}_p{k}", policy(2147483647, g, 1, k)) for g in (4, 5, 6) for k in (128, 256)]
             legs += [("hybrid_3_hot0", policy(2147483647, 3, 0))]
             if len(sys.argv) > 2:
                 legs = [lg for lg in legs if lg[0] in sys.argv[2].split(",")]

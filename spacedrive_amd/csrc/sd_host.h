@@ -66,7 +66,8 @@ enum sd_tune_key {
     SD_TUNE_HOST_CPU_BUDGET = 14,          // cap on the host threads one call starts (0 = resolve it)
     SD_TUNE_CHECKSUM_STAGE_HOT = 15,       // sd_file_checksums' GPU route: pread_stream into the windows
     SD_TUNE_NUMA_PIN = 16,                 // library threads on the GPU's NUMA node (0 = float)
-    SD_TUNE_NKEYS = 17
+    SD_TUNE_CPU_READ_PIECE_KIB = 17,       // CPU path: a 1 MiB block read and hashed in pieces of this size
+    SD_TUNE_NKEYS = 18
 };
 int tuning_get(int key);
 

@@ -172,6 +172,25 @@ def test_cpu_file_checksums_vs_oracle(tmp_path, oracle_native):
             assert cpu.file_checksum(paths[i]) == got[i]
 
 
+@pytest.mark.parametrize("piece_kib", [0, 64, 100, 256, 1024, 4096])
+def test_cpu_file_checksums_read_pieces(tmp_path, oracle_native, piece_kib):
+    """"cpu_read_piece_kib": the CPU path reads and hashes each 1 MiB block of a large file
+    in pieces (round 5); every piece size -- a divisor of the block, one that is not (100),
+    the whole block, more than it -- gives the oracle's checksums."""
+    import spacedrive_amd as sd
+    MiB = 1 << 20
+    sizes = [8 * MiB, 9 * MiB + 123, 17 * MiB - 1]
+    paths = [_write(tmp_path, f"p{i}", oracle_native.synth_bytes(70 + i, 0, 0, s)) for i, s in enumerate(sizes)]
+    want, wst = oracle_native.file_checksums(paths, nthreads=2)
+    keep = sd.get_tuning("cpu_read_piece_kib")
+    try:
+        sd.set_tuning("cpu_read_piece_kib", piece_kib)
+        got = cpu.file_checksums(paths, nthreads=4)
+    finally:
+        sd.set_tuning("cpu_read_piece_kib", keep)
+    assert (wst == 0).all() and got == [w.tobytes().hex() for w in want]
+
+
 def test_cpu_file_checksum_of_a_pipe(tmp_path):
     """hash.rs stops at the first short read: a FIFO (st_size 0) hashes what one read returns."""
     fifo = str(tmp_path / "fifo")
