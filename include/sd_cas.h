@@ -465,8 +465,12 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * sd_file_checksums splits a large call with the CPU path (0 = never split);
  * "checksum_stage_hot" (1): sd_file_checksums' GPU-route readers deliver through a
  * cache-resident buffer and streaming stores (0 = pread straight into the pinned window);
- * "cpu_read_piece_kib" (0): the CPU path reads and hashes each 1 MiB block of a large file
- * in pieces of this many KiB (0 = one 1 MiB read, then the hash);
+ * "cpu_read_piece_kib" (256): the CPU path reads and hashes each 1 MiB block of a large file
+ * in pieces of this many KiB, each hashed while still in the core's L2 (0 = one 1 MiB read,
+ * then the hash; 256 measured 1.04-1.07x, profiles/r5/r5d_hybrid.json);
+ * "checksum_split_blocks" (1): sd_file_checksums' split claims work by 1 MiB blocks (the
+ * GPU's "checksum_hybrid_threads" slots take runs of blocks while free, the host threads
+ * single blocks); 0 = by whole files (round 4);
  * "host_cohash_threads" (15): host threads hashing beside the GPU in sd_cas_ids calls of
  * >= 8192 files and sd_checksums calls of >= 1 GiB (0 = the GPU alone; never more than the
  * host budget less one); "host_cpu_budget" (0 = resolved, see sd_host_cpu_budget): the cap

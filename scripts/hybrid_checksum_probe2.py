@@ -8,7 +8,9 @@ rounds on two tmpfs file sets (the bench's 32 x 256 MiB, and 48 files of 8..320 
   gpu_16[_hot0]          the GPU route alone ("checksum_cpu_max" 0), pread_stream on / off
   hybrid_g[_hot0]        the policy's split, "checksum_hybrid_threads" g
   *_pK                   the same with "cpu_read_piece_kib" K (round 5: the CPU path reads and
-                         hashes each 1 MiB block K KiB at a time)
+                         hashes each 1 MiB block K KiB at a time; 256 the default since)
+  hybrid_g / _files      round 5: the split claimed by blocks with g GPU slots (the default) /
+                         by whole files (round 4, "checksum_split_blocks" 0)
 Every call's output is asserted equal to the CPU path's.
 python scripts/hybrid_checksum_probe2.py [rounds] [legs,...] -> one JSON line (per-round rows on stderr)"""
 import ctypes
@@ -26,7 +28,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import spacedrive_amd as sd  # noqa: E402
 from spacedrive_amd._native import check, lib, path_array  # noqa: E402
 
-KNOBS = ("checksum_cpu_max", "checksum_hybrid_threads", "checksum_stage_hot", "read_threads", "cpu_read_piece_kib")
+KNOBS = ("checksum_cpu_max", "checksum_hybrid_threads", "checksum_stage_hot", "read_threads", "cpu_read_piece_kib",
+         "checksum_split_blocks")
 
 
 def write_set(ctx, d, lens, cid0):
@@ -74,7 +77,7 @@ def main():
                     best = dt if best is None else min(best, dt)
                 return total / best / 1e9
 
-            def cpu16(piece=0):
+            def cpu16(piece=256):
                 def f():
                     sd.set_tuning("cpu_read_piece_kib", piece)
                     try:
@@ -83,8 +86,9 @@ def main():
                         sd.set_tuning("cpu_read_piece_kib", keep["cpu_read_piece_kib"])
                 return f
 
-            def policy(cpu_max, g, hot, piece=0):
+            def policy(cpu_max, g, hot, piece=256, blocks=1):
                 def f():
+                    sd.set_tuning("checksum_split_blocks", blocks)
                     sd.set_tuning("checksum_cpu_max", cpu_max)
                     sd.set_tuning("checksum_hybrid_threads", g)
                     sd.set_tuning("checksum_stage_hot", hot)
@@ -96,11 +100,9 @@ def main():
                             sd.set_tuning(k, v)
                 return f
 
-            legs = [("cpu_16", cpu16()), ("gpu_16", policy(0, 0, 1)), ("gpu_16_hot0", policy(0, 0, 0))]
-            legs += [(f"cpu_16_p{k}", cpu16(k)) for k in (64, 128, 256, 512)]
-            legs += [(f"hybrid_{g}", policy(2147483647, g, 1)) for g in (2, 3, 4, 5, 6, 8)]
-            legs += [(f"hybrid_{g}_p{k}", policy(2147483647, g, 1, k)) for g in (4, 5, 6) for k in (128, 256)]
-            legs += [("hybrid_3_hot0", policy(2147483647, 3, 0))]
+            legs = [("cpu_16", cpu16()), ("cpu_16_p0", cpu16(0)), ("gpu_16", policy(0, 0, 1))]
+            legs += [(f"hybrid_{g}", policy(2147483647, g, 1)) for g in (3, 4, 5, 6, 8)]
+            legs += [(f"hybrid_{g}_files", policy(2147483647, g, 1, blocks=0)) for g in (4, 6)]
             if len(sys.argv) > 2:
                 legs = [lg for lg in legs if lg[0] in sys.argv[2].split(",")]
             rounds = []

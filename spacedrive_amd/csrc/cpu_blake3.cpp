@@ -424,6 +424,25 @@ int32_t cpu_cas_id_file(const char* path, uint64_t size, char out_hex17[17]) {
     return SD_FILE_OK;
 }
 
+bool cpu_block_cv_fd(int fd, uint64_t file_len, uint64_t block, uint8_t cv[32]) {
+    const uint64_t off = block * SD_CK_BLOCK;
+    if (off >= file_len) return false;
+    const uint64_t want = std::min<uint64_t>(SD_CK_BLOCK, file_len - off);
+    // "cpu_read_piece_kib" p > 0: the block is read and hashed p KiB at a time, so each
+    // piece is hashed while it is still in this core's L2 (0: one 1 MiB read, then the hash)
+    const int pk = tuning_get(SD_TUNE_CPU_READ_PIECE_KIB);
+    const uint64_t piece = pk > 0 ? std::min<uint64_t>(SD_CK_BLOCK, (uint64_t)pk << 10) : SD_CK_BLOCK;
+    uint8_t* buf = scratch(piece);
+    CpuHasher h(block * (SD_CK_BLOCK / 1024));
+    for (uint64_t o = 0; o < want; o += piece) {
+        const uint64_t n = std::min(piece, want - o);
+        if (pread_full(fd, buf, n, off + o) != (int64_t)n) return false;
+        h.update(buf, n);
+    }
+    h.finalize_cv(cv);
+    return true;
+}
+
 int32_t cpu_checksum_file(const char* path, char out_hex65[65]) {
     Fd f{open(path, O_RDONLY | O_CLOEXEC)};  // hash.rs:11
     if (f.fd < 0) return io_status(errno);
@@ -618,28 +637,12 @@ int sd_cpu_file_checksums(const char* const* paths, size_t n, char* out_hex65, i
         }
         Big& b = *big[task.file];
         if (b.failed.load(std::memory_order_relaxed)) return;
-        const uint64_t off = task.block * SD_CK_BLOCK;
-        const uint64_t want = std::min<uint64_t>(SD_CK_BLOCK, b.len - off);
-        // "cpu_read_piece_kib" p > 0: the block is read and hashed p KiB at a time, so each
-        // piece is hashed while it is still in this core's L2 (0: one 1 MiB read, then the hash)
-        const int pk = tuning_get(SD_TUNE_CPU_READ_PIECE_KIB);
-        const uint64_t piece = pk > 0 ? std::min<uint64_t>(SD_CK_BLOCK, (uint64_t)pk << 10) : SD_CK_BLOCK;
-        uint8_t* buf = scratch(piece);
-        CpuHasher h(task.block * (SD_CK_BLOCK / 1024));
         // the task's own descriptor: pool workers have private fd tables (stage_pool.h)
         const int fd = open(paths[b.file], O_RDONLY | O_CLOEXEC);
-        bool ok = fd >= 0;
-        for (uint64_t o = 0; ok && o < want; o += piece) {
-            const uint64_t n = std::min(piece, want - o);
-            ok = pread_full(fd, buf, n, off + o) == (int64_t)n;
-            if (ok) h.update(buf, n);
-        }
+        const bool ok = fd >= 0 && cpu_block_cv_fd(fd, b.len, task.block, b.cvs.data() + 32 * task.block);
         if (fd >= 0) close(fd);
-        if (!ok) {  // shrank, replaced, unopenable: the read loop below reports it
+        if (!ok)  // shrank, replaced, unopenable: the read loop below reports it
             b.failed.store(true, std::memory_order_relaxed);
-            return;
-        }
-        h.finalize_cv(b.cvs.data() + 32 * task.block);
     });
     for (auto& bp : big) {
         Big& b = *bp;

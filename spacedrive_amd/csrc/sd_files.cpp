@@ -727,6 +727,223 @@ void gpu_file_checksums(sd_cas_ctx* ctx, const char* const* paths, char* out_hex
     streamer.finish(slots);
 }
 
+
+// sd_file_checksums' split, claimed block by block (round 5).  Every
+// large regular file's 1 MiB blocks form one queue, in file order (largest file first); the
+// call's `threads` pool threads all take from it.  A thread first looks for a free GPU slot
+// (at most `gpu_slots`): if one is free it claims a run of up to 32 blocks of one file,
+// reads them into the slot's pinned window (pread_stream), queues the H2D on the call's one
+// copy queue and k_ck_leaf + the blocks' CVs back to the host table on the slot's stream,
+// and moves on; otherwise it hashes the small files (whole-file tasks, CPU path) and then
+// ONE block at a time on the CPU (cpu_block_cv_fd).  So the GPU takes as much as its slots
+// keep moving -- PCIe fills with the fewest reader threads -- and the rest is hashed on the
+// host with 1 MiB granularity: no route waits on the other's last whole file (round 4's
+// split claimed whole files and lost up to one file's time at the end; the GPU's claims
+// shrink towards the end as well).  Each file's root is merged on the host from its block
+// CVs (cpu_root_from_cvs); a file that turns out shorter or longer than its stat length is
+// hashed again with hash.rs's sequential loop, as the CPU path does.
+void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out_hex65, int32_t* status,
+                            int threads, int gpu_slots, const std::vector<size_t>& big,
+                            const std::vector<size_t>& rest, const std::vector<uint64_t>& hint) {
+    ctx->bind();
+    constexpr uint64_t GPU_RUN = 32;  // blocks per GPU claim while plenty is left
+    const size_t nf = big.size();
+    // one plan over every large file: file q's blocks are CV slots [fb[q], fb[q+1]) and its
+    // message bytes sit at the virtual offset fb[q] MiB, so a window holding its blocks
+    // [b0, b1) is shifted by (fb[q] + b0) MiB
+    std::vector<ck_file> files(nf);
+    std::vector<uint64_t> fb(nf + 1, 0);
+    for (size_t q = 0; q < nf; q++) {
+        const uint64_t len = hint[big[q]];
+        files[q] = ck_file{fb[q] * SD_CK_BLOCK, len, fb[q]};
+        fb[q + 1] = fb[q] + (len + SD_CK_BLOCK - 1) / SD_CK_BLOCK;
+    }
+    const uint64_t nb_total = fb[nf];
+    if (nb_total >= (1ull << 31)) throw sd_failure(SD_ERR_INVALID, "split call too large");
+    std::vector<sd_u32x2> map(nb_total);
+    for (size_t q = 0; q < nf; q++)
+        for (uint64_t b = fb[q]; b < fb[q + 1]; b++) map[b] = sd_u32x2{(uint32_t)q, (uint32_t)(b - fb[q])};
+    Tables tab;
+    tab.begin();
+    const size_t o_files = tab.add(files), o_map = tab.add(map);
+    tab.upload(nullptr);
+    DevBuf d_cv;
+    d_cv.ensure(nb_total * 32);
+    PinnedBuf h_cv;  // every block's CV, from either side
+    h_cv.ensure(nb_total * 32);
+
+    struct GpuSlot {
+        std::unique_ptr<Slot> s;
+        hipEvent_t copied = nullptr, done = nullptr;
+        bool filling = false, used = false;
+    };
+    struct Slots {
+        sd_cas_ctx* c;
+        std::vector<GpuSlot> g;
+        std::unique_ptr<Slot> cp;  // the call's one H2D queue (SlotPair::copy_stream)
+        ~Slots() {
+            for (auto& x : g) {
+                if (x.s) {
+                    (void)hipStreamSynchronize(x.s->stream);
+                    c->release(std::move(x.s));
+                }
+                if (x.copied) (void)hipEventDestroy(x.copied);
+                if (x.done) (void)hipEventDestroy(x.done);
+            }
+            if (cp) {
+                (void)hipStreamSynchronize(cp->stream);
+                c->release(std::move(cp));
+            }
+        }
+    } sl{ctx, std::vector<GpuSlot>(std::max(1, gpu_slots)), nullptr};
+    sl.cp = ctx->acquire();
+    for (auto& x : sl.g) {
+        x.s = ctx->acquire();
+        x.s->window.ensure(GPU_RUN * SD_CK_BLOCK + 128);
+        x.s->staged.ensure(GPU_RUN * SD_CK_BLOCK + 128);
+        HIP_CHECK(hipEventCreateWithFlags(&x.copied, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
+    }
+
+    std::mutex mu, copy_mu;
+    size_t cf = 0;     // claim cursor: file cf, its block cb
+    uint64_t cb = 0, left = nb_total;
+    std::atomic<size_t> small_next{0};
+    std::vector<uint8_t> failed(nf, 0);  // a short read: hashed again with the read loop
+    std::atomic<uint64_t> gpu_bytes{0}, cpu_bytes{0};
+    std::atomic<bool> stop{false};
+    int err_rc = SD_OK;
+    std::string err_msg;
+    // [b0, b1) of file q, at most `want` blocks (under mu)
+    auto claim = [&](uint64_t want, size_t& q, uint64_t& b0, uint64_t& b1) -> bool {
+        while (cf < nf && cb >= fb[cf + 1] - fb[cf]) {
+            cf++;
+            cb = 0;
+        }
+        if (cf >= nf) return false;
+        q = cf;
+        b0 = cb;
+        b1 = std::min(fb[cf + 1] - fb[cf], cb + want);
+        cb = b1;
+        left -= b1 - b0;
+        return true;
+    };
+    auto feed = [&](int k, size_t q, uint64_t b0, uint64_t b1) {
+        GpuSlot& x = sl.g[k];
+        Slot& s = *x.s;
+        const uint64_t off = b0 * SD_CK_BLOCK, bytes = std::min(b1 * SD_CK_BLOCK, files[q].len) - off;
+        const int fd = open(paths[big[q]], O_RDONLY | O_CLOEXEC);  // hash.rs:11
+        const int64_t got = fd < 0 ? -1 : pread_stream(fd, s.window.u8(), bytes, off);
+        if (fd >= 0) close(fd);
+        if (got != (int64_t)bytes) {
+            std::lock_guard<std::mutex> g(mu);
+            failed[q] = 1;
+            x.filling = false;
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(copy_mu);  // the copy and its event, back to back on the queue
+            HIP_CHECK(hipMemcpyAsync(s.staged.p, s.window.p, bytes, hipMemcpyHostToDevice, sl.cp->stream));
+            HIP_CHECK(hipEventRecord(x.copied, sl.cp->stream));
+        }
+        HIP_CHECK(hipStreamWaitEvent(s.stream, x.copied, 0));
+        HIP_CHECK(sdk::launch_ck_leaf(s.staged.as<uint8_t>(), files[q].offset + off, 0, tab.at<ck_file>(o_files),
+                                      tab.at<uint2>(o_map) + fb[q] + b0, (uint32_t)(b1 - b0), d_cv.as<uint32_t>(),
+                                      d_cv.as<uint32_t>(), s.stream));
+        HIP_CHECK(hipMemcpyAsync(h_cv.u8() + 32 * (fb[q] + b0), d_cv.as<uint8_t>() + 32 * (fb[q] + b0), 32 * (b1 - b0),
+                                 hipMemcpyDeviceToHost, s.stream));
+        HIP_CHECK(hipEventRecord(x.done, s.stream));
+        gpu_bytes.fetch_add(bytes, std::memory_order_relaxed);
+        std::lock_guard<std::mutex> g(mu);
+        x.filling = false;
+        x.used = true;
+    };
+    auto worker = [&](size_t) {
+        try {
+            while (!stop.load(std::memory_order_relaxed)) {
+                int k = -1;
+                size_t q = 0;
+                uint64_t b0 = 0, b1 = 0;
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    if (left > 0)
+                        for (int j = 0; j < (int)sl.g.size() && k < 0; j++)
+                            if (!sl.g[j].filling && (!sl.g[j].used || hipEventQuery(sl.g[j].done) == hipSuccess)) k = j;
+                    // the GPU's runs shrink towards the end, so its last ones finish with the host's
+                    if (k >= 0 && claim(std::max<uint64_t>(4, std::min<uint64_t>(GPU_RUN, left / (2 * (uint64_t)threads))),
+                                        q, b0, b1))
+                        sl.g[k].filling = true;
+                    else
+                        k = -1;
+                }
+                if (k >= 0) {
+                    feed(k, q, b0, b1);
+                    continue;
+                }
+                const size_t i = small_next.fetch_add(1, std::memory_order_relaxed);
+                if (i < rest.size()) {  // the small and non-regular files: whole-file tasks, CPU path
+                    status[rest[i]] = cpu_checksum_file(paths[rest[i]], out_hex65 + 65 * rest[i]);
+                    cpu_bytes.fetch_add(hint[rest[i]], std::memory_order_relaxed);
+                    continue;
+                }
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    if (!claim(1, q, b0, b1)) return;
+                    if (failed[q]) continue;
+                }
+                const int fd = open(paths[big[q]], O_RDONLY | O_CLOEXEC);
+                const bool ok = fd >= 0 && cpu_block_cv_fd(fd, files[q].len, b0, h_cv.u8() + 32 * (fb[q] + b0));
+                if (fd >= 0) close(fd);
+                if (!ok) {
+                    std::lock_guard<std::mutex> g(mu);
+                    failed[q] = 1;
+                }
+                cpu_bytes.fetch_add(std::min(SD_CK_BLOCK, files[q].len - b0 * SD_CK_BLOCK), std::memory_order_relaxed);
+            }
+        } catch (const sd_failure& e) {
+            std::lock_guard<std::mutex> g(mu);
+            if (err_rc == SD_OK) {
+                err_rc = e.rc;
+                err_msg = e.what();
+            }
+            stop.store(true);
+        } catch (...) {
+            std::lock_guard<std::mutex> g(mu);
+            if (err_rc == SD_OK) {
+                err_rc = SD_ERR_NOMEM;
+                err_msg = "host allocation failed in a split sd_file_checksums call";
+            }
+            stop.store(true);
+        }
+    };
+    std::shared_ptr<StagePool> pool = ctx->stage_pool(threads);  // private fd tables
+    pool->run((size_t)threads, worker, threads);
+    for (auto& x : sl.g) HIP_CHECK(hipStreamSynchronize(x.s->stream));  // every CV is in h_cv
+    if (err_rc != SD_OK) throw sd_failure(err_rc, err_msg);
+    ctx->checksum_bytes_gpu.fetch_add(gpu_bytes.load(), std::memory_order_relaxed);
+    ctx->checksum_bytes_cpu_split.fetch_add(cpu_bytes.load(), std::memory_order_relaxed);
+    // each file's root from its block CVs -- unless a read came back short, or a byte lies
+    // past the stat length (it grew): then hash.rs's sequential loop, to EOF
+    for (size_t q = 0; q < nf; q++) {
+        const size_t i = big[q];
+        bool at_end = false;
+        if (!failed[q]) {
+            const int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+            uint8_t probe;
+            at_end = fd >= 0 && pread_full(fd, &probe, 1, files[q].len) == 0;
+            if (fd >= 0) close(fd);
+        }
+        if (at_end) {
+            uint8_t h[32];
+            cpu_root_from_cvs(h_cv.u8() + 32 * fb[q], fb[q + 1] - fb[q], h);
+            to_hex(h, 32, out_hex65 + 65 * i);  // hash.rs:21-23
+            status[i] = SD_FILE_OK;
+        } else {
+            status[i] = cpu_checksum_file(paths[i], out_hex65 + 65 * i);
+        }
+    }
+}
+
 }  // namespace
 
 // file_checksum (hash.rs:10-24) for n paths: the batch policy picks the CPU path, the GPU
@@ -776,6 +993,10 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
         if (big.size() >= 2 && big_bytes >= BIG_TOTAL) {
             ctx->checksum_calls_hybrid.fetch_add(1, std::memory_order_relaxed);
             std::stable_sort(big.begin(), big.end(), [&](size_t a, size_t b) { return hint[a] > hint[b]; });
+            if (tuning_get(SD_TUNE_CHECKSUM_SPLIT_BLOCKS) != 0) {
+                split_checksums_blocks(ctx, paths, out_hex65, status, threads, hyb, big, rest, hint);
+                return SD_OK;
+            }
             std::atomic<size_t> cursor{0};
             auto next_big = [&]() -> size_t {
                 const size_t k = cursor.fetch_add(1, std::memory_order_relaxed);

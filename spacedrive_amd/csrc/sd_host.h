@@ -67,7 +67,8 @@ enum sd_tune_key {
     SD_TUNE_CHECKSUM_STAGE_HOT = 15,       // sd_file_checksums' GPU route: pread_stream into the windows
     SD_TUNE_NUMA_PIN = 16,                 // library threads on the GPU's NUMA node (0 = float)
     SD_TUNE_CPU_READ_PIECE_KIB = 17,       // CPU path: a 1 MiB block read and hashed in pieces of this size
-    SD_TUNE_NKEYS = 18
+    SD_TUNE_CHECKSUM_SPLIT_BLOCKS = 18,    // sd_file_checksums' split: 1 = claims by blocks, 0 = by files
+    SD_TUNE_NKEYS = 19
 };
 int tuning_get(int key);
 
@@ -413,4 +414,7 @@ int cpu_lanes();
 // generate_cas_id / file_checksum of one file on the calling thread -> sd_file_status
 int32_t cpu_cas_id_file(const char* path, uint64_t size, char out_hex17[17]);
 int32_t cpu_checksum_file(const char* path, char out_hex65[65]);
+// the (non-root) chaining value of 1 MiB block `block` of a regular file of file_len >= 2
+// blocks, read from fd at its offset ("cpu_read_piece_kib" pieces); false on a short read
+bool cpu_block_cv_fd(int fd, uint64_t file_len, uint64_t block, uint8_t cv[32]);
 void hex_lower(const uint8_t* h, int nbytes, char* out);

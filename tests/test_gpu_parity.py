@@ -494,12 +494,16 @@ def test_file_checksums_packing_and_streaming(ctx, tmp_path):
         assert got[i] == want[i], (i, sizes[i])
 
 
-def test_file_checksums_hybrid_split(ctx, tmp_path):
+@pytest.mark.parametrize("mode,budget", [("blocks", 0), ("blocks", 3), ("files", 0)])
+def test_file_checksums_hybrid_split(ctx, tmp_path, mode, budget):
     """sd_file_checksums' split policy ("checksum_hybrid_threads", default 4): a call whose regular
-    files of >= 8 MiB total >= 512 MiB runs the GPU route and the CPU path at once, the large
-    files going to whichever is free, the small ones and a FIFO to the CPU path.  Every
-    result equals the oracle's read schedule (hash.rs:10-24), an unreadable path keeps its
-    error, and the call is counted as split; below the threshold the CPU path alone runs."""
+    files of >= 8 MiB total >= 512 MiB runs the GPU route and the CPU path at once -- by
+    blocks (round 5's default: the GPU's slots take runs of 1 MiB blocks while free, the host
+    threads single blocks, roots merged from both sides' CVs) or by whole files (round 4,
+    "checksum_split_blocks" 0) -- the small ones and a FIFO to the CPU path.  Every result
+    equals the oracle's read schedule (hash.rs:10-24), an unreadable path keeps its error,
+    the call is counted as split and both sides hashed bytes, also under a 3-thread host
+    budget; below the threshold the CPU path alone runs."""
     import threading
     import spacedrive_amd as sd
     from oracle import native
@@ -527,9 +531,15 @@ def test_file_checksums_hybrid_split(ctx, tmp_path):
     paths.insert(9, str(tmp_path / "missing"))
     want_h, want_st = native.file_checksums([p for p in paths if p != fifo], nthreads=NT)
     want = dict(zip([p for p in paths if p != fifo], zip(want_h, want_st)))
-    keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads")}
+    from spacedrive_amd._native import check, lib
+    keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads", "checksum_split_blocks",
+                                          "host_cpu_budget")}
     sd.set_tuning("checksum_cpu_max", 2147483647)  # the library default (the module sets 0)
     sd.set_tuning("checksum_hybrid_threads", 4)  # the library default
+    sd.set_tuning("checksum_split_blocks", 1 if mode == "blocks" else 0)
+    sd.set_tuning("host_cpu_budget", budget)
+    by0 = np.zeros(2, np.uint64)
+    check(lib().sd_file_checksums_bytes(sd.default_context().handle, by0.ctypes.data))
     try:
         before = sd.file_checksums_stats()
         t = threading.Thread(target=feed)
@@ -538,6 +548,9 @@ def test_file_checksums_hybrid_split(ctx, tmp_path):
         t.join()
         after = sd.file_checksums_stats()
         assert after["hybrid"] == before["hybrid"] + 1 and after["cpu"] == before["cpu"]
+        by1 = np.zeros(2, np.uint64)
+        check(lib().sd_file_checksums_bytes(sd.default_context().handle, by1.ctypes.data))
+        assert by1[0] > by0[0] and by1[1] > by0[1], (by0, by1)  # both sides hashed
         assert got[5] == native.blake3(fifo_data).hex()
         for p, g in zip(paths, got):
             if p == fifo:
