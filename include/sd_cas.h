@@ -245,11 +245,13 @@ int sd_checksums_stats(sd_cas_ctx* ctx, uint64_t out[2]);
  * whatever their final length; two windows alternate so host reads overlap the H2D
  * copies and the kernels (the readers stream each piece through a cache-resident buffer into
  * the pinned window, "checksum_stage_hot" 1).  Batch policy: with "checksum_hybrid_threads"
- * g > 0 (default 4), a call whose regular files of >= 8 MiB add up to >= 512 MiB is split
- * between that GPU route (on g of the 16 "read_threads"; fewer under a smaller host budget)
- * and sd_cpu_file_checksums (the rest of the threads), running at once: the large files go
- * to whichever route is free next, the small ones to the CPU path -- from the page cache
- * 1.04-1.21x the CPU path alone, by box.  Any other call of at most "checksum_cpu_max" files is
+ * g > 0 (default 6), a call whose regular files of >= 8 MiB add up to >= 512 MiB is split
+ * between the GPU and the CPU path on the 16 "read_threads" at once, claimed by 1 MiB blocks
+ * ("checksum_split_blocks" 1): a thread that finds one of g GPU slots free reads a run of up
+ * to 32 blocks of a file into it (fewer slots under a smaller host budget); otherwise it
+ * hashes the small files, then single blocks, on the CPU path; each file's root is merged
+ * from both sides' block CVs -- from the page cache 1.13-1.43x the CPU path alone
+ * (round 4's whole-file claims, "checksum_split_blocks" 0: 0.9-1.24x).  Any other call of at most "checksum_cpu_max" files is
  * hashed by sd_cpu_file_checksums on "read_threads" threads -- by default every such call,
  * because from the page cache the host's threads hash faster than PCIe can carry the bytes
  * to the GPU; "checksum_cpu_max" 0 = the GPU route alone for every call. */
@@ -461,8 +463,8 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * copies; "files_stage_hot" (1): its readers read each file into a per-thread buffer and
  * stream-copy it into the window (0 = read straight into the window); "checksum_cpu_max" (2147483647): sd_file_checksums calls of at most that many
  * files take the CPU path (sd_cpu_file_checksums on "read_threads" threads; 0 = the GPU
- * route always); "checksum_hybrid_threads" (4): reader threads of the GPU route when
- * sd_file_checksums splits a large call with the CPU path (0 = never split);
+ * route always); "checksum_hybrid_threads" (6): GPU slots -- threads feeding the GPU at once
+ * -- when sd_file_checksums splits a large call with the CPU path (0 = never split);
  * "checksum_stage_hot" (1): sd_file_checksums' GPU-route readers deliver through a
  * cache-resident buffer and streaming stores (0 = pread straight into the pinned window);
  * "cpu_read_piece_kib" (256): the CPU path reads and hashes each 1 MiB block of a large file

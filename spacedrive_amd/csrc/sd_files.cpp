@@ -949,21 +949,19 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
 // file_checksum (hash.rs:10-24) for n paths: the batch policy picks the CPU path, the GPU
 // route (gpu_file_checksums) or both at once.
 //   * "checksum_cpu_max" = 0: the GPU route for every call.
-//   * Hybrid ("checksum_hybrid_threads" = g, default 4): a call whose regular files of
+//   * Hybrid ("checksum_hybrid_threads" = g, default 6): a call whose regular files of
 //     >= 8 MiB add up to >= 512 MiB is split.  Handing a byte to the GPU costs the host
-//     0.068 ns (pread into a cache-resident buffer, streaming stores into the pinned window:
-//     pread_stream), hashing it on the CPU path 0.172 ns (the pread plus 0.110 ns of
-//     AVX-512 BLAKE3) -- scripts/ck_host_cost.cpp, profiles/r4/r4b_ck_host_cost.jsonl -- so a
-//     few reader threads fill PCIe while the rest hash: the GPU route gets g of the
-//     "read_threads" (g of 16, fewer under a smaller host budget) and the CPU path the rest,
-//     on a second host thread.  The large files go to whichever route is free next (one
-//     shared cursor, largest first; the CPU half takes ~16 MiB per thread at a time), so
-//     neither waits on a static split; the small and non-regular files go to the CPU path.
-//     From the page cache: 1.13-1.21x the CPU path alone at g = 4
-//     (scripts/hybrid_checksum_probe2.py,
-//     profiles/r4/r4c_hybrid_checksum_probe.json).  (Round 3's split ran its GPU half
-//     on pools grown to 16 threads by earlier calls and read straight into pinned memory:
-//     78-90 against 81-87 GB/s, profiles/r3/r3z_hybrid_checksum_probe.json.)
+//     0.07-0.10 ns (pread into a cache-resident buffer, streaming stores into the pinned
+//     window: pread_stream), hashing it on the CPU path 0.17-0.18 ns (the pread plus 0.11 ns
+//     of AVX-512 BLAKE3) -- scripts/ck_host_cost.cpp, profiles/r4/r4b_ck_host_cost.jsonl,
+//     profiles/r5/r5c_ck_host_bound.jsonl -- and both are bound by host CPU time, not DRAM
+//     (the split moves 150-230 GB/s of DRAM traffic against the 16 threads' measured 450-650
+//     GB/s).  So the threads feed the GPU while it has room (g slots) and hash the rest:
+//     split_checksums_blocks above, claimed by 1 MiB blocks ("checksum_split_blocks" 1,
+//     profiles/r5/r5e_hybrid_blocks.json: 1.13-1.43x the CPU path alone from the page cache).
+//     With "checksum_split_blocks" 0, round 4's split: the GPU route on g reader threads and
+//     the CPU path on the rest on a second host thread, whole large files to whichever is
+//     free next (one shared cursor, largest first; 0.9-1.24x, the last whole file the tail).
 //   * Otherwise calls of at most "checksum_cpu_max" files (default: all) take the CPU path:
 //     from the page cache the host's threads hash faster than PCIe carries the bytes.
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65, int32_t* status) {

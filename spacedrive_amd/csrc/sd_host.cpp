@@ -35,15 +35,16 @@ thread_local std::string g_err;
 // sd_file_checksums call on the CPU path unless it is large enough to split (DESIGN.md §4:
 // from the page cache the host hashes faster than PCIe carries the bytes), the stager's
 // readers through their cache-resident buffers (profiles/r3/r3n_files_ab_private_fds.json:
-// 1.04 vs 0.84 M files/s), large sd_file_checksums calls split between the GPU route on 4
-// of the 16 readers and the CPU path on the rest, the GPU route's readers through
-// pread_stream (profiles/r4/r4c_hybrid_checksum_probe.json: 1.13-1.21x the CPU path alone
-// from the page cache); no host thread budget override; library threads left unplaced
+// 1.04 vs 0.84 M files/s), large sd_file_checksums calls split between the GPU route (at most
+// 6 of the 16 threads feeding it at once) and the CPU path, claimed by 1 MiB blocks, the GPU
+// route's readers through pread_stream (profiles/r5/r5e_hybrid_blocks.json: 1.20-1.43x the
+// CPU path alone from the page cache), the CPU path's block reads in 256 KiB pieces
+// (profiles/r5/r5d_hybrid.json: 1.04-1.07x); no host thread budget override; library threads left unplaced
 // ("numa_pin" 0: placing them on the GPU's node measured neutral with the page cache where
 // the writer left it, profiles/r4/r4h_numa_lib_probe.json); 15 host threads hashing beside the GPU in
 // large sd_cas_ids calls (profiles/r3/r3ad_cohash_probe.json: 300 000 files from pinned memory,
 // GPU alone 1.89-1.94 M files/s, CPU path alone 2.24-2.36 M, both at once 3.87-4.08 M)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {4}, {15}, {0}, {1}, {0}, {256}, {1}};
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {6}, {15}, {0}, {1}, {0}, {256}, {1}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
                                                "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",
