@@ -1,5 +1,5 @@
 """sd_cas_ids from pinned host memory with h host threads co-hashing ("host_cohash_threads"),
-h in {0, 4, 8, 12, 15}, against the library's CPU path alone on 16 threads (sd_cpu_cas_ids):
+h in {0, 8, 11..15}, against the library's CPU path alone on 16 threads (sd_cpu_cas_ids):
 the bench's with-H2D leg (300 000 files of the library mixture, 8.55 GB of messages),
 interleaved rounds, outputs asserted equal.
 python scripts/cohash_probe.py [files] [rounds] -> one JSON line"""
@@ -39,7 +39,7 @@ def main():
     try:
         for _ in range(rounds):
             row = {}
-            for h in ((0, 4, 8, 12, 15) if k >= 100_000 else (0, 15)):
+            for h in ((0, 8, 11, 12, 13, 14, 15) if k >= 100_000 else (0, 15)):
                 sd.set_tuning("host_cohash_threads", h)
                 check(L.sd_cas_ids(ctx.handle, host.data_ptr(), total + 64, ext.ctypes.data, k, out, None))  # warm
                 s0 = np.zeros(2, np.uint64)
