@@ -652,6 +652,7 @@ def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1, lib_=None):
 def checksum_host(ctx, gib: int, dev, stream):
     """with-H2D checksums: `gib` GiB of pinned host memory (files of 1 GiB) through the
     drop-in sd_checksums, beside the raw H2D copy and the device-resident kernels."""
+    from spacedrive_amd import _native
     from spacedrive_amd._native import check, lib
     nf, flen = gib, 1 << 30
     total = nf * flen
@@ -733,7 +734,8 @@ def checksum_host(ctx, gib: int, dev, stream):
     par = parity(nf, bad, "every file's 64-hex checksum vs the C oracle's chunk-parallel BLAKE3 of the same content")
     return {"files": nf, "bytes": total, "h2d_ms": h2d_ms, "h2d_GBps": total / (h2d_ms * 1e-3) / 1e9, "parity": par,
             "kernel_ms": kernel_ms, "kernel_GBps": total / (kernel_ms * 1e-3) / 1e9,
-            "end_to_end_ms": e2e_s * 1e3, "end_to_end_GBps": total / e2e_s / 1e9, "host_cohash_threads": keep,
+            "end_to_end_ms": e2e_s * 1e3, "end_to_end_GBps": total / e2e_s / 1e9,
+            "host_cohash_threads": max(0, min(keep, _native.host_cpu_budget()["budget"] - 3)),
             "host_share": host_share,
             "gpu_only": {"end_to_end_ms": e2e["gpu_only"] * 1e3, "end_to_end_GBps": total / e2e["gpu_only"] / 1e9},
             "library_cpu_path": {"threads": cpu_t, "GBps": total / min(cpu_runs) / 1e9,

@@ -475,7 +475,8 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * single blocks); 0 = by whole files (round 4);
  * "host_cohash_threads" (15): host threads hashing beside the GPU in sd_cas_ids calls of
  * >= 8192 files and sd_checksums calls of >= 1 GiB (0 = the GPU alone; never more than the
- * host budget less one); "host_cpu_budget" (0 = resolved, see sd_host_cpu_budget): the cap
+ * host budget less one in sd_cas_ids, less three in sd_checksums -- 13 of 16 measured best
+ * there); "host_cpu_budget" (0 = resolved, see sd_host_cpu_budget): the cap
  * on every call's host threads -- thread counts callers pass (nthreads) and the knobs above
  * are clamped to it.  Unknown keys fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);

@@ -1175,8 +1175,14 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     // there the GPU loop claims its 1 MiB blocks a window at a time from the front, the
     // host thread 64 blocks at a time from the back into a host CV table; when none is
     // left, the GPU loop uploads the host's CVs next to its own and runs the reduce passes.
-    // (never more host threads than the process's host budget, less one for this thread)
-    const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS), host_cpu_budget() - 1}));
+    // Never more host threads than the process's host budget less three: this thread, and
+    // two CPUs of headroom.  Measured on the box (16-CPU quota, 4 x 1 GiB, interleaved
+    // rounds; scripts/cohash_checksum_probe.py, profiles/r5/r5g_cohash_checksum.json and
+    // r5h_cohash_ck.json): 13 co-hashing threads 138-151 GB/s, 14: 136-148, 15: 123-129 --
+    // at 15 the process burns 16.5 CPUs of time per call for fewer bytes (no throttled
+    // periods: the contention is the cores', not the quota's).  sd_cas_ids keeps budget - 1:
+    // there 15 measured best (4.86 vs 4.51 M files/s at 13, r5h_cohash_cas.json).
+    const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS), host_cpu_budget() - 3}));
     uint64_t all_bytes = 0;
     for (size_t q = 0; q < n; q++) all_bytes += lens[q];
     std::mutex claim_mu;
