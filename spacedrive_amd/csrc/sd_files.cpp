@@ -860,6 +860,7 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
     };
     auto worker = [&](size_t) {
         try {
+            ctx->bind();  // pool threads queue copies and kernels on this context's device
             while (!stop.load(std::memory_order_relaxed)) {
                 int k = -1;
                 size_t q = 0;
