@@ -1155,14 +1155,21 @@ def test_checksums_from_host_memory_cohashed(ctx, oracle_native, cohash):
     out = ctypes.create_string_buffer(65 * len(lens))
     keep = sd.get_tuning("host_cohash_threads")
     sd.set_tuning("host_cohash_threads", cohash)
+    st0, st1 = np.zeros(2, np.uint64), np.zeros(2, np.uint64)
     try:
+        check(lib().sd_checksums_stats(ctx.handle, st0.ctypes.data))
         check(lib().sd_checksums(ctx.handle, host.data_ptr(), arr_o.ctypes.data, arr_l.ctypes.data, len(lens), out))
+        check(lib().sd_checksums_stats(ctx.handle, st1.ctypes.data))
     finally:
         sd.set_tuning("host_cohash_threads", keep)
     want = oracle_native.checksums_simd(host.numpy(), arr_o, arr_l, nthreads=NT)
     raw = out.raw
     for i in range(len(lens)):
         assert raw[65 * i:65 * i + 64].decode() == want[i].tobytes().hex(), (i, lens[i])
+    # sd_checksums_stats: every byte counted once, on the side that hashed it
+    d_gpu, d_host = (int(x) for x in (st1 - st0))
+    assert d_gpu + d_host == sum(lens)
+    assert (d_host > 0 and d_gpu > 0) if cohash else d_host == 0
 
 
 @pytest.mark.parametrize("cohash", [0, 15])
