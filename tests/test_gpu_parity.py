@@ -602,6 +602,54 @@ def test_concurrent_callers_share_a_context(ctx, tmp_path):
     assert not errors, errors
 
 
+def test_concurrent_split_checksum_calls(ctx, tmp_path, oracle_native):
+    """Two host threads, one context, each a split sd_file_checksums call (>= 512 MiB of
+    files >= 8 MiB: the block split, round 5) at once, three times over: the calls share the
+    context's pools and slots, and every checksum equals the oracle's."""
+    import threading
+    import spacedrive_amd as sd
+    MiB = 1 << 20
+    sets = [[40 * MiB + 7 * i for i in range(12)] + [3000, 77 * MiB], [64 * MiB + 11 * i for i in range(9)]]
+    paths = []
+    for s, lens in enumerate(sets):
+        ps = []
+        for i, L in enumerate(lens):
+            p = tmp_path / f"s{s}_{i}"
+            with open(p, "wb") as f:
+                pos = 0
+                while pos < L:
+                    k = min(32 * MiB, L - pos)
+                    f.write(oracle_native.synth_bytes(7000 + 100 * s + i, 0, pos, k))
+                    pos += k
+            ps.append(str(p))
+        paths.append(ps)
+    want = [[w.tobytes().hex() for w in oracle_native.file_checksums(ps, nthreads=NT)[0]] for ps in paths]
+    keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads")}
+    sd.set_tuning("checksum_cpu_max", 2147483647)  # the library default (the module sets 0)
+    sd.set_tuning("checksum_hybrid_threads", 6)
+    errors = []
+    before = sd.file_checksums_stats()["hybrid"]
+
+    def worker(s):
+        try:
+            for _ in range(3):
+                assert sd.file_checksums(paths[s]) == want[s]
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+    try:
+        th = [threading.Thread(target=worker, args=(s,)) for s in range(2)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=300)
+        assert not any(x.is_alive() for x in th)
+    finally:
+        for k, v in keep.items():
+            sd.set_tuning(k, v)
+    assert not errors, errors
+    assert sd.file_checksums_stats()["hybrid"] == before + 6
+
+
 @pytest.mark.parametrize("ring,hot", [(4, 0), (2, 0), (16, 1)])
 def test_cas_ids_files_pipelined_windows(ctx, tmp_path, oracle_native, ring, hot):
     """sd_cas_ids_files over many 1 MiB windows (the readers run ahead through a ring of
