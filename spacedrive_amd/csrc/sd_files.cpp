@@ -730,21 +730,22 @@ void gpu_file_checksums(sd_cas_ctx* ctx, const char* const* paths, char* out_hex
 
 // sd_file_checksums' split, claimed block by block (round 5).  Every
 // large regular file's 1 MiB blocks form one queue, in file order (largest file first); the
-// call's pool threads take from it.  A thread first looks for a free GPU slot (at most
-// `gpu_slots`): if one is free it claims a run of up to 32 blocks of one file, reads them
-// into the slot's pinned window (pread_stream) and hands the slot to the calling thread;
-// otherwise it hashes the small files (whole-file tasks, CPU path) and then ONE block at a
-// time on the CPU (cpu_block_cv_fd).  The calling thread does every HIP call: it queues each
-// filled window's H2D on the call's one copy queue and k_ck_leaf + the blocks' CVs back to
-// the host table on the slot's stream, and frees a slot when its event has completed.  (The
-// pool threads run on private fd tables -- stage_pool.h -- whose copies of the runtime's
-// device descriptors are closed, so they make no HIP call at all.)  So the GPU takes as much
+// call's `threads` threads (the caller included) all take from it.  A thread first looks for
+// a free GPU slot (at most `gpu_slots`): if one is free it claims a run of up to 32 blocks
+// of one file, reads them into the slot's pinned window (pread_stream), queues the H2D on
+// the call's one copy queue and k_ck_leaf + the blocks' CVs back to the host table on the
+// slot's stream, and moves on; otherwise it hashes the small files (whole-file tasks, CPU
+// path) and then ONE block at a time on the CPU (cpu_block_cv_fd).  So the GPU takes as much
 // as its slots keep moving -- PCIe fills with the fewest reader threads -- and the rest is
 // hashed on the host with 1 MiB granularity: no route waits on the other's last whole file
 // (round 4's split claimed whole files and lost up to one file's time at the end; the GPU's
-// claims shrink towards the end as well).  Each file's root is merged on the host from its
-// block CVs (cpu_root_from_cvs); a file that turns out shorter or longer than its stat
-// length is hashed again with hash.rs's sequential loop, as the CPU path does.
+// claims shrink towards the end as well).  The threads make HIP calls, so they run on the
+// context's shared-fd-table pool (io_pool: a private table's copies of the runtime's device
+// descriptors are closed); a thread keeps its descriptor while its claims stay in one file,
+// so the shared table's lock sees about one open per file and thread.  Each file's root is
+// merged on the host from its block CVs (cpu_root_from_cvs); a file that turns out shorter
+// or longer than its stat length is hashed again with hash.rs's sequential loop, as the CPU
+// path does.
 void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out_hex65, int32_t* status,
                             int threads, int gpu_slots, const std::vector<size_t>& big,
                             const std::vector<size_t>& rest, const std::vector<uint64_t>& hint) {
@@ -775,13 +776,10 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
     PinnedBuf h_cv;  // every block's CV, from either side
     h_cv.ensure(nb_total * 32);
 
-    enum SlotState { FREE, FILLING, READY, INFLIGHT };
     struct GpuSlot {
         std::unique_ptr<Slot> s;
         hipEvent_t copied = nullptr, done = nullptr;
-        SlotState state = FREE;
-        size_t q = 0;  // the run it holds: file q's blocks [b0, b1), `bytes` of them
-        uint64_t b0 = 0, b1 = 0, bytes = 0;
+        bool filling = false, used = false;
     };
     struct Slots {
         sd_cas_ctx* c;
@@ -811,25 +809,15 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
         HIP_CHECK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
     }
 
-    std::mutex mu;
-    std::condition_variable filled;  // a slot turned READY, or a worker finished
-    size_t cf = 0;                   // claim cursor: file cf, its block cb
+    std::mutex mu, copy_mu;
+    size_t cf = 0;  // claim cursor: file cf, its block cb
     uint64_t cb = 0, left = nb_total;
     std::atomic<size_t> small_next{0};
     std::vector<uint8_t> failed(nf, 0);  // a short read: hashed again with the read loop
     std::atomic<uint64_t> gpu_bytes{0}, cpu_bytes{0};
     std::atomic<bool> stop{false};
-    const int workers = std::max(1, threads - 1);  // the calling thread drives the GPU
-    int workers_left = workers;
     int err_rc = SD_OK;
     std::string err_msg;
-    auto fail = [&](int rc, const std::string& msg) {  // under mu
-        if (err_rc == SD_OK) {
-            err_rc = rc;
-            err_msg = msg;
-        }
-        stop.store(true);
-    };
     // [b0, b1) of file q, at most `want` blocks (under mu)
     auto claim = [&](uint64_t want, size_t& q, uint64_t& b0, uint64_t& b1) -> bool {
         while (cf < nf && cb >= fb[cf + 1] - fb[cf]) {
@@ -844,9 +832,19 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
         left -= b1 - b0;
         return true;
     };
-    // a pool thread: fill a free GPU slot, else hash on the CPU path; no HIP call here
     auto worker = [&](size_t) {
+        int fd = -1;               // this thread's descriptor of file fd_q, kept across its claims
+        size_t fd_q = SIZE_MAX;
+        auto file = [&](size_t q) {
+            if (q != fd_q) {
+                if (fd >= 0) close(fd);
+                fd = open(paths[big[q]], O_RDONLY | O_CLOEXEC);  // hash.rs:11
+                fd_q = q;
+            }
+            return fd;
+        };
         try {
+            ctx->bind();  // (the caller's device is already current; a pool thread's may not be)
             while (!stop.load(std::memory_order_relaxed)) {
                 int k = -1;
                 size_t q = 0;
@@ -855,32 +853,43 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
                     std::lock_guard<std::mutex> g(mu);
                     if (left > 0)
                         for (int j = 0; j < (int)sl.g.size() && k < 0; j++)
-                            if (sl.g[j].state == FREE) k = j;
+                            if (!sl.g[j].filling && (!sl.g[j].used || hipEventQuery(sl.g[j].done) == hipSuccess)) k = j;
                     // the GPU's runs shrink towards the end, so its last ones finish with the host's
                     if (k >= 0 && claim(std::max<uint64_t>(4, std::min<uint64_t>(GPU_RUN, left / (2 * (uint64_t)threads))),
                                         q, b0, b1))
-                        sl.g[k].state = FILLING;
+                        sl.g[k].filling = true;
                     else
                         k = -1;
                 }
                 if (k >= 0) {
                     GpuSlot& x = sl.g[k];
+                    Slot& s = *x.s;
                     const uint64_t off = b0 * SD_CK_BLOCK, bytes = std::min(b1 * SD_CK_BLOCK, files[q].len) - off;
-                    const int fd = open(paths[big[q]], O_RDONLY | O_CLOEXEC);  // hash.rs:11
-                    const int64_t got = fd < 0 ? -1 : pread_stream(fd, x.s->window.u8(), bytes, off);
-                    if (fd >= 0) close(fd);
-                    std::lock_guard<std::mutex> g(mu);
-                    if (got == (int64_t)bytes) {
-                        x.q = q;
-                        x.b0 = b0;
-                        x.b1 = b1;
-                        x.bytes = bytes;
-                        x.state = READY;
-                        filled.notify_one();
-                    } else {
+                    const int f = file(q);
+                    const int64_t got = f < 0 ? -1 : pread_stream(f, s.window.u8(), bytes, off);
+                    if (got != (int64_t)bytes) {
+                        std::lock_guard<std::mutex> g(mu);
                         failed[q] = 1;
-                        x.state = FREE;
+                        x.filling = false;
+                        continue;
                     }
+                    {
+                        std::lock_guard<std::mutex> g(copy_mu);  // the copy and its event, back to back on the queue
+                        HIP_CHECK(hipMemcpyAsync(s.staged.p, s.window.p, bytes, hipMemcpyHostToDevice, sl.cp->stream));
+                        HIP_CHECK(hipEventRecord(x.copied, sl.cp->stream));
+                    }
+                    HIP_CHECK(hipStreamWaitEvent(s.stream, x.copied, 0));
+                    HIP_CHECK(sdk::launch_ck_leaf(s.staged.as<uint8_t>(), files[q].offset + off, 0,
+                                                  tab.at<ck_file>(o_files), tab.at<uint2>(o_map) + fb[q] + b0,
+                                                  (uint32_t)(b1 - b0), d_cv.as<uint32_t>(), d_cv.as<uint32_t>(),
+                                                  s.stream));
+                    HIP_CHECK(hipMemcpyAsync(h_cv.u8() + 32 * (fb[q] + b0), d_cv.as<uint8_t>() + 32 * (fb[q] + b0),
+                                             32 * (b1 - b0), hipMemcpyDeviceToHost, s.stream));
+                    HIP_CHECK(hipEventRecord(x.done, s.stream));
+                    gpu_bytes.fetch_add(bytes, std::memory_order_relaxed);
+                    std::lock_guard<std::mutex> g(mu);
+                    x.filling = false;
+                    x.used = true;
                     continue;
                 }
                 const size_t i = small_next.fetch_add(1, std::memory_order_relaxed);
@@ -894,9 +903,8 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
                     if (!claim(1, q, b0, b1)) break;
                     if (failed[q]) continue;
                 }
-                const int fd = open(paths[big[q]], O_RDONLY | O_CLOEXEC);
-                const bool ok = fd >= 0 && cpu_block_cv_fd(fd, files[q].len, b0, h_cv.u8() + 32 * (fb[q] + b0));
-                if (fd >= 0) close(fd);
+                const int f = file(q);
+                const bool ok = f >= 0 && cpu_block_cv_fd(f, files[q].len, b0, h_cv.u8() + 32 * (fb[q] + b0));
                 if (!ok) {
                     std::lock_guard<std::mutex> g(mu);
                     failed[q] = 1;
@@ -905,75 +913,24 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
             }
         } catch (const sd_failure& e) {
             std::lock_guard<std::mutex> g(mu);
-            fail(e.rc, e.what());
+            if (err_rc == SD_OK) {
+                err_rc = e.rc;
+                err_msg = e.what();
+            }
+            stop.store(true);
         } catch (...) {
             std::lock_guard<std::mutex> g(mu);
-            fail(SD_ERR_NOMEM, "host allocation failed in a split sd_file_checksums call");
+            if (err_rc == SD_OK) {
+                err_rc = SD_ERR_NOMEM;
+                err_msg = "host allocation failed in a split sd_file_checksums call";
+            }
+            stop.store(true);
         }
-        std::lock_guard<std::mutex> g(mu);
-        workers_left--;
-        filled.notify_one();
+        if (fd >= 0) close(fd);
     };
-    std::shared_ptr<StagePool> pool = ctx->stage_pool(threads);  // private fd tables
-    pool->start((size_t)workers, worker, workers);
-    // the calling thread: queue every filled window on the GPU, free the slots it is done with
-    try {
-        for (;;) {
-            std::vector<int> ready;
-            bool inflight = false, done = false;
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                for (auto& x : sl.g) inflight |= x.state == INFLIGHT;
-                auto any_ready = [&] {
-                    for (auto& x : sl.g)
-                        if (x.state == READY) return true;
-                    return false;
-                };
-                // while runs are in flight, look at their events every 50 us
-                if (inflight) filled.wait_for(lk, std::chrono::microseconds(50), [&] { return any_ready() || stop.load(); });
-                else filled.wait(lk, [&] { return any_ready() || workers_left == 0 || stop.load(); });
-                for (int k = 0; k < (int)sl.g.size(); k++)
-                    if (sl.g[k].state == READY) ready.push_back(k);
-                done = workers_left == 0 && ready.empty() && !inflight;
-            }
-            if (done || stop.load()) break;
-            for (int k : ready) {
-                GpuSlot& x = sl.g[k];
-                Slot& s = *x.s;
-                const size_t q = x.q;
-                HIP_CHECK(hipMemcpyAsync(s.staged.p, s.window.p, x.bytes, hipMemcpyHostToDevice, sl.cp->stream));
-                HIP_CHECK(hipEventRecord(x.copied, sl.cp->stream));
-                HIP_CHECK(hipStreamWaitEvent(s.stream, x.copied, 0));
-                HIP_CHECK(sdk::launch_ck_leaf(s.staged.as<uint8_t>(), files[q].offset + x.b0 * SD_CK_BLOCK, 0,
-                                              tab.at<ck_file>(o_files), tab.at<uint2>(o_map) + fb[q] + x.b0,
-                                              (uint32_t)(x.b1 - x.b0), d_cv.as<uint32_t>(), d_cv.as<uint32_t>(),
-                                              s.stream));
-                HIP_CHECK(hipMemcpyAsync(h_cv.u8() + 32 * (fb[q] + x.b0), d_cv.as<uint8_t>() + 32 * (fb[q] + x.b0),
-                                         32 * (x.b1 - x.b0), hipMemcpyDeviceToHost, s.stream));
-                HIP_CHECK(hipEventRecord(x.done, s.stream));
-                gpu_bytes.fetch_add(x.bytes, std::memory_order_relaxed);
-                std::lock_guard<std::mutex> g(mu);
-                x.state = INFLIGHT;
-            }
-            for (auto& x : sl.g) {  // a slot whose run is hashed and its CVs home is free again
-                bool fl;
-                {
-                    std::lock_guard<std::mutex> g(mu);
-                    fl = x.state == INFLIGHT;
-                }
-                if (!fl) continue;
-                const hipError_t e = hipEventQuery(x.done);
-                if (e == hipErrorNotReady) continue;
-                HIP_CHECK(e);
-                std::lock_guard<std::mutex> g(mu);
-                x.state = FREE;
-            }
-        }
-    } catch (const sd_failure& e) {
-        std::lock_guard<std::mutex> g(mu);
-        fail(e.rc, e.what());
-    }
-    pool->wait();  // every worker has returned (they stop at their next claim after a failure)
+    // the shared-fd-table pool: these threads make HIP calls (see above)
+    std::shared_ptr<StagePool> pool = ctx->io_pool(threads);
+    pool->run((size_t)threads, worker, threads);
     for (auto& x : sl.g) HIP_CHECK(hipStreamSynchronize(x.s->stream));  // every CV is in h_cv
     if (err_rc != SD_OK) throw sd_failure(err_rc, err_msg);
     ctx->checksum_bytes_gpu.fetch_add(gpu_bytes.load(), std::memory_order_relaxed);
