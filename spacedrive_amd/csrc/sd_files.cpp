@@ -778,8 +778,9 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
 
     struct GpuSlot {
         std::unique_ptr<Slot> s;
-        hipEvent_t copied = nullptr, done = nullptr;
-        bool filling = false, used = false;
+        hipEvent_t copied = nullptr;
+        bool filling = false;          // a thread is reading into it (under mu)
+        std::atomic<uint32_t> busy{0};  // 1 from its claim until its run's CVs are home
     };
     struct Slots {
         sd_cas_ctx* c;
@@ -792,7 +793,6 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
                     c->release(std::move(x.s));
                 }
                 if (x.copied) (void)hipEventDestroy(x.copied);
-                if (x.done) (void)hipEventDestroy(x.done);
             }
             if (cp) {
                 (void)hipStreamSynchronize(cp->stream);
@@ -806,8 +806,11 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
         x.s->window.ensure(GPU_RUN * SD_CK_BLOCK + 128);
         x.s->staged.ensure(GPU_RUN * SD_CK_BLOCK + 128);
         HIP_CHECK(hipEventCreateWithFlags(&x.copied, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
     }
+    // a slot's run is done when the stream reaches this host function: it clears `busy`,
+    // so the threads look for free slots without a HIP call (an hipEventQuery per claim,
+    // made under the claim lock, stalled every thread whenever it was slow)
+    const hipHostFn_t slot_done = [](void* p) { static_cast<std::atomic<uint32_t>*>(p)->store(0, std::memory_order_release); };
 
     std::mutex mu, copy_mu;
     size_t cf = 0;  // claim cursor: file cf, its block cb
@@ -853,13 +856,15 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
                     std::lock_guard<std::mutex> g(mu);
                     if (left > 0)
                         for (int j = 0; j < (int)sl.g.size() && k < 0; j++)
-                            if (!sl.g[j].filling && (!sl.g[j].used || hipEventQuery(sl.g[j].done) == hipSuccess)) k = j;
+                            if (!sl.g[j].filling && sl.g[j].busy.load(std::memory_order_acquire) == 0) k = j;
                     // the GPU's runs shrink towards the end, so its last ones finish with the host's
                     if (k >= 0 && claim(std::max<uint64_t>(4, std::min<uint64_t>(GPU_RUN, left / (2 * (uint64_t)threads))),
-                                        q, b0, b1))
+                                        q, b0, b1)) {
                         sl.g[k].filling = true;
-                    else
+                        sl.g[k].busy.store(1, std::memory_order_relaxed);
+                    } else {
                         k = -1;
+                    }
                 }
                 if (k >= 0) {
                     GpuSlot& x = sl.g[k];
@@ -870,6 +875,7 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
                     if (got != (int64_t)bytes) {
                         std::lock_guard<std::mutex> g(mu);
                         failed[q] = 1;
+                        x.busy.store(0, std::memory_order_relaxed);
                         x.filling = false;
                         continue;
                     }
@@ -885,11 +891,10 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
                                                   s.stream));
                     HIP_CHECK(hipMemcpyAsync(h_cv.u8() + 32 * (fb[q] + b0), d_cv.as<uint8_t>() + 32 * (fb[q] + b0),
                                              32 * (b1 - b0), hipMemcpyDeviceToHost, s.stream));
-                    HIP_CHECK(hipEventRecord(x.done, s.stream));
+                    HIP_CHECK(hipLaunchHostFunc(s.stream, slot_done, &x.busy));
                     gpu_bytes.fetch_add(bytes, std::memory_order_relaxed);
                     std::lock_guard<std::mutex> g(mu);
                     x.filling = false;
-                    x.used = true;
                     continue;
                 }
                 const size_t i = small_next.fetch_add(1, std::memory_order_relaxed);
