@@ -128,14 +128,30 @@ __device__ __forceinline__ void parent(uint32_t (&out)[8], const uint32_t (&l)[8
     compress(out, m, 0u, 0u, BLOCK_LEN, PARENT | extra_flags);
 }
 
+// Message loads.  SD_MSG_NT=1 marks them non-temporal (every message byte is read once);
+// default 0, plain loads (the A/B: DESIGN.md section 3).
+#ifndef SD_MSG_NT
+#define SD_MSG_NT 0
+#endif
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
 // 64 message bytes -> 16 little-endian words (4x 16-byte loads; ptr 16-B aligned)
 __device__ __forceinline__ void load_block(uint32_t (&m)[16], const uint8_t* __restrict__ p) {
+#if SD_MSG_NT
+    const u32x4_t* q = reinterpret_cast<const u32x4_t*>(p);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        u32x4_t v = __builtin_nontemporal_load(q + k);
+        m[4 * k + 0] = v.x; m[4 * k + 1] = v.y; m[4 * k + 2] = v.z; m[4 * k + 3] = v.w;
+    }
+#else
     const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         uint4 v = q[k];
         m[4 * k + 0] = v.x; m[4 * k + 1] = v.y; m[4 * k + 2] = v.z; m[4 * k + 3] = v.w;
     }
+#endif
 }
 
 // Partial final block: len in [0, 64). Bytes past len are zero (BLAKE3 padding).  Reads
