@@ -314,6 +314,9 @@ __global__ __launch_bounds__(256) void k_whole_items(const uint8_t* __restrict__
 // merges into the stack as it arrives (the next node's load in flight meanwhile), then the
 // stack folds from the top.  ROOT on the final parent when the group is the whole file.
 // Two passes (<= 8 pair nodes, then <= 8 of those) cover messages of up to 128 chunks.
+#ifndef SD_MERGE8_PRELOAD
+#define SD_MERGE8_PRELOAD 1
+#endif
 __global__ __launch_bounds__(256) void k_whole_merge8(const uint4* __restrict__ items, uint32_t n,
                                                       const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                                       uint32_t* __restrict__ out) {
@@ -322,6 +325,36 @@ __global__ __launch_bounds__(256) void k_whole_merge8(const uint4* __restrict__ 
     const uint4 it = items[g];
     const uint32_t m = it.y & 0xFu;
     const bool root = (it.y >> 31) != 0u;
+#if SD_MERGE8_PRELOAD
+    // All m node CVs are loaded at once (they were written by another XCD's workgroups, so
+    // each load is a trip past this XCD's L2: one round trip per lane instead of m), then
+    // merged level-wise with static register indices -- pairs (2k, 2k+1), the odd node
+    // carried up -- the BLAKE3 tree of an aligned group.  The lanes of a wave hold items
+    // sorted by node count, so the guarded parents rarely diverge.
+    uint32_t nd[8][8];
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if ((uint32_t)k < m) load_cv(nd[k], src + (size_t)(it.x + k) * 8);
+    uint32_t cnt = m;
+#pragma unroll
+    for (int lvl = 0; lvl < 3; lvl++) {
+        const uint32_t flags = (root && cnt == 2u) ? ROOT : 0u;
+#pragma unroll
+        for (int k = 0; k < 4 >> lvl; k++) {
+            if ((uint32_t)(2 * k + 1) < cnt) {
+                uint32_t r[8];
+                parent(r, nd[2 * k], nd[2 * k + 1], flags);
+#pragma unroll
+                for (int i = 0; i < 8; i++) nd[k][i] = r[i];
+            } else if ((uint32_t)(2 * k) < cnt) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) nd[k][i] = nd[2 * k][i];
+            }
+        }
+        cnt = (cnt + 1u) >> 1;
+    }
+    store_cv((root ? out : dst) + (size_t)it.z * 8, nd[0]);
+#else
     const bool pow2 = (m & (m - 1u)) == 0u;
     CvStack<3> st;  // after node i it holds popcount(i + 1) <= 3 subtrees
     uint32_t cur[8], nxt[8];
@@ -343,6 +376,7 @@ __global__ __launch_bounds__(256) void k_whole_merge8(const uint4* __restrict__ 
 #pragma unroll 1
     for (; depth > 0; depth--) st.merge_top(cur, (root && depth == 1) ? ROOT : 0u);
     store_cv((root ? out : dst) + (size_t)it.z * 8, cur);
+#endif
 }
 
 // 32-byte hash rows src[i] -> out[idx[i]] (whole-file cas messages hashed by the checksum
