@@ -76,10 +76,24 @@ __device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t m) {
 #endif
 }
 
+// rotr(d ^ a, 8).  Default: v_alignbit.  SD_ROTR8_PERM=1: a byte permute (v_perm_b32), the
+// same issue class; measured for its power under the board's cap.
+#ifndef SD_ROTR8_PERM
+#define SD_ROTR8_PERM 0
+#endif
+__device__ __forceinline__ uint32_t xor_rotr8(uint32_t d, uint32_t a) {
+#if SD_ROTR8_PERM
+    const uint32_t x = d ^ a;
+    return __builtin_amdgcn_perm(x, x, 0x00030201u);
+#else
+    return rotr(d ^ a, 8);
+#endif
+}
+
 #define SD_G(a, b, c, d, x, y)              \
     a = add3(a, b, (x)); d = xor_rotr16(d, a); \
     c = c + d;           b = rotr(b ^ c, 12); \
-    a = add3(a, b, (y)); d = rotr(d ^ a, 8);  \
+    a = add3(a, b, (y)); d = xor_rotr8(d, a); \
     c = c + d;           b = rotr(b ^ c, 7);
 
 template <int R>
