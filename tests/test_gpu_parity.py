@@ -569,6 +569,44 @@ def test_file_checksums_hybrid_split(ctx, tmp_path, mode, budget):
             sd.set_tuning(k, v)
 
 
+@pytest.mark.parametrize("slots", [1, 15])
+def test_file_checksums_split_block_edges(ctx, tmp_path, oracle_native, slots):
+    """The block split (round 5) around its own boundaries: files of k MiB and k MiB +- 1 /
+    1023 / 1024 / 1025 bytes (a last block of 1 byte up to a full one, and one-byte-short
+    blocks), a file of 32 MiB (one GPU run exactly) and 33 MiB + 1, with the GPU given 1 slot
+    (the host threads take most blocks, edge blocks included) or 15 (the GPU takes most):
+    every root merged from the two sides' CVs equals the oracle's file_checksum."""
+    import spacedrive_amd as sd
+    MiB = 1 << 20
+    sizes = [8 * MiB - 1, 8 * MiB, 8 * MiB + 1, 9 * MiB + 1023, 9 * MiB + 1024, 9 * MiB + 1025, 10 * MiB - 1024,
+             32 * MiB, 33 * MiB + 1, 47 * MiB + 77, 64 * MiB - 1, 64 * MiB + 1, 100 * MiB + 3, 128 * MiB + 513,
+             130 * MiB - 1]
+    assert sum(sizes) >= 512 * MiB
+    paths = []
+    for i, L in enumerate(sizes):
+        p = tmp_path / f"e{i}"
+        with open(p, "wb") as f:
+            pos = 0
+            while pos < L:
+                k = min(32 * MiB, L - pos)
+                f.write(oracle_native.synth_bytes(9000 + i, 0, pos, k))
+                pos += k
+        paths.append(str(p))
+    want = [w.tobytes().hex() for w in oracle_native.file_checksums(paths, nthreads=NT)[0]]
+    keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads", "checksum_split_blocks")}
+    sd.set_tuning("checksum_cpu_max", 2147483647)  # the library default (the module sets 0)
+    sd.set_tuning("checksum_hybrid_threads", slots)
+    sd.set_tuning("checksum_split_blocks", 1)
+    try:
+        before = sd.file_checksums_stats()["hybrid"]
+        for _ in range(2):  # the sides' shares differ run to run
+            assert sd.file_checksums(paths) == want
+        assert sd.file_checksums_stats()["hybrid"] == before + 2
+    finally:
+        for k, v in keep.items():
+            sd.set_tuning(k, v)
+
+
 def test_concurrent_callers_share_a_context(ctx, tmp_path):
     # the C ABI is thread-safe and re-entrant: 6 host threads, one context
     import threading
