@@ -593,6 +593,13 @@ def test_file_checksums_split_block_edges(ctx, tmp_path, oracle_native, slots):
                 pos += k
         paths.append(str(p))
     want = [w.tobytes().hex() for w in oracle_native.file_checksums(paths, nthreads=NT)[0]]
+    locked = None
+    if os.geteuid() != 0:  # a large file the call stats but cannot open: its error, the rest hashed
+        locked = tmp_path / "locked"
+        with open(locked, "wb") as f:
+            f.truncate(24 * MiB)
+        os.chmod(locked, 0)
+        paths.insert(4, str(locked))
     keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads", "checksum_split_blocks")}
     sd.set_tuning("checksum_cpu_max", 2147483647)  # the library default (the module sets 0)
     sd.set_tuning("checksum_hybrid_threads", slots)
@@ -600,7 +607,10 @@ def test_file_checksums_split_block_edges(ctx, tmp_path, oracle_native, slots):
     try:
         before = sd.file_checksums_stats()["hybrid"]
         for _ in range(2):  # the sides' shares differ run to run
-            assert sd.file_checksums(paths) == want
+            got = sd.file_checksums(paths)
+            if locked is not None:
+                assert isinstance(got.pop(4), PermissionError)
+            assert got == want
         assert sd.file_checksums_stats()["hybrid"] == before + 2
     finally:
         for k, v in keep.items():
