@@ -1,6 +1,5 @@
-"""Why the co-hashed checksum call over pinned memory tops out at 125-150 GB/s on every box
-(round 5): the host's hashing against the device's DMA from host
-memory.  4 GiB of pinned memory A (the bench's with-H2D checksum input: 4 x 1 GiB), a second
+"""What bounds the co-hashed checksum call over pinned memory (round 5; DESIGN.md section
+4.2): the host's hashing against the device's DMA from host memory.  4 GiB of pinned memory A (the bench's with-H2D checksum input: 4 x 1 GiB), a second
 pinned buffer B of 4 GiB and a device buffer; legs, in interleaved rounds:
   cpu_T          sd_cpu_checksums over A on T threads (T = 13, 16), nothing else running
   dma            one 4 GiB H2D copy B -> device, alone
