@@ -59,36 +59,13 @@ __device__ __forceinline__ uint32_t xor_rotr16(uint32_t d, uint32_t a) {
 #endif
 }
 
-// a + b + m.  Default: one v_add3_u32 (3 sources, half issue rate).  SD_ADD3_SPLIT=1: two
-// 2-source v_add_u32 (full rate each; the first held in asm so the compiler cannot fuse
-// them back) -- the one op-level lever the issue probes found (scripts/valu_probe7.hip,
-// profiles/r3/r3c_valu_probe7.txt: 39.88 vs 39.51 T for the G mix at 8 waves/SIMD).
-#ifndef SD_ADD3_SPLIT
-#define SD_ADD3_SPLIT 0
-#endif
-__device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t m) {
-#if SD_ADD3_SPLIT
-    uint32_t t;
-    asm("v_add_u32 %0, %1, %2" : "=v"(t) : "v"(a), "v"(b));
-    return t + m;
-#else
-    return a + b + m;
-#endif
-}
+// a + b + m: one v_add3_u32 (3 sources, half issue rate).  Two 2-source adds issue faster
+// in registers (scripts/valu_probe7.hip) but measured 8-9 % slower in the kernels (more
+// VGPRs, fewer waves; DESIGN.md section 3, profiles/r5/r5b_add3_ab/, variant in 9bfbbfb).
+__device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t m) { return a + b + m; }
 
-// rotr(d ^ a, 8).  Default: v_alignbit.  SD_ROTR8_PERM=1: a byte permute (v_perm_b32), the
-// same issue class; measured for its power under the board's cap.
-#ifndef SD_ROTR8_PERM
-#define SD_ROTR8_PERM 0
-#endif
-__device__ __forceinline__ uint32_t xor_rotr8(uint32_t d, uint32_t a) {
-#if SD_ROTR8_PERM
-    const uint32_t x = d ^ a;
-    return __builtin_amdgcn_perm(x, x, 0x00030201u);
-#else
-    return rotr(d ^ a, 8);
-#endif
-}
+// rotr(d ^ a, 8) with v_alignbit (a v_perm_b32 byte permute measured the same, r5x; c6256dd)
+__device__ __forceinline__ uint32_t xor_rotr8(uint32_t d, uint32_t a) { return rotr(d ^ a, 8); }
 
 #define SD_G(a, b, c, d, x, y)              \
     a = add3(a, b, (x)); d = xor_rotr16(d, a); \
@@ -142,30 +119,15 @@ __device__ __forceinline__ void parent(uint32_t (&out)[8], const uint32_t (&l)[8
     compress(out, m, 0u, 0u, BLOCK_LEN, PARENT | extra_flags);
 }
 
-// Message loads.  SD_MSG_NT=1 marks them non-temporal (every message byte is read once);
-// default 0, plain loads (the A/B: DESIGN.md section 3).
-#ifndef SD_MSG_NT
-#define SD_MSG_NT 0
-#endif
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-
 // 64 message bytes -> 16 little-endian words (4x 16-byte loads; ptr 16-B aligned)
+// (plain loads: non-temporal ones measured 50 % slower, r5u; de4d437)
 __device__ __forceinline__ void load_block(uint32_t (&m)[16], const uint8_t* __restrict__ p) {
-#if SD_MSG_NT
-    const u32x4_t* q = reinterpret_cast<const u32x4_t*>(p);
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        u32x4_t v = __builtin_nontemporal_load(q + k);
-        m[4 * k + 0] = v.x; m[4 * k + 1] = v.y; m[4 * k + 2] = v.z; m[4 * k + 3] = v.w;
-    }
-#else
     const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         uint4 v = q[k];
         m[4 * k + 0] = v.x; m[4 * k + 1] = v.y; m[4 * k + 2] = v.z; m[4 * k + 3] = v.w;
     }
-#endif
 }
 
 // Partial final block: len in [0, 64). Bytes past len are zero (BLAKE3 padding).  Reads

@@ -310,13 +310,11 @@ __global__ __launch_bounds__(256) void k_whole_items(const uint8_t* __restrict__
 
 // Item = (first node slot in src, m | root << 31, dst slot or file): merges nodes
 // src[first .. first + m), m in 1..8, an aligned group of one file's node list (every node
-// but the last a full subtree of one size), into one CV with BLAKE3's CV stack: each node
-// merges into the stack as it arrives (the next node's load in flight meanwhile), then the
-// stack folds from the top.  ROOT on the final parent when the group is the whole file.
-// Two passes (<= 8 pair nodes, then <= 8 of those) cover messages of up to 128 chunks.
-#ifndef SD_MERGE8_PRELOAD
-#define SD_MERGE8_PRELOAD 1
-#endif
+// but the last a full subtree of one size), into one CV, level-wise (below).  ROOT on the
+// final parent when the group is the whole file.  Two passes (<= 8 pair nodes, then <= 8 of
+// those) cover messages of up to 128 chunks.  (Round 5: every node loaded up front, 4 %
+// faster than merging each into a CV stack as it arrived, profiles/r5/r5w_merge8_trace.md;
+// the stack version is in e9a97a5.)
 __global__ __launch_bounds__(256) void k_whole_merge8(const uint4* __restrict__ items, uint32_t n,
                                                       const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                                       uint32_t* __restrict__ out) {
@@ -325,7 +323,6 @@ __global__ __launch_bounds__(256) void k_whole_merge8(const uint4* __restrict__ 
     const uint4 it = items[g];
     const uint32_t m = it.y & 0xFu;
     const bool root = (it.y >> 31) != 0u;
-#if SD_MERGE8_PRELOAD
     // All m node CVs are loaded at once (they were written by another XCD's workgroups, so
     // each load is a trip past this XCD's L2: one round trip per lane instead of m), then
     // merged level-wise with static register indices -- pairs (2k, 2k+1), the odd node
@@ -354,29 +351,6 @@ __global__ __launch_bounds__(256) void k_whole_merge8(const uint4* __restrict__ 
         cnt = (cnt + 1u) >> 1;
     }
     store_cv((root ? out : dst) + (size_t)it.z * 8, nd[0]);
-#else
-    const bool pow2 = (m & (m - 1u)) == 0u;
-    CvStack<3> st;  // after node i it holds popcount(i + 1) <= 3 subtrees
-    uint32_t cur[8], nxt[8];
-    load_cv(nxt, src + (size_t)it.x * 8);
-    uint32_t depth = 0;
-#pragma unroll 1
-    for (uint32_t i = 0; i < m; i++) {
-#pragma unroll
-        for (int k = 0; k < 8; k++) cur[k] = nxt[k];
-        if (i + 1 < m) load_cv(nxt, src + (size_t)(it.x + i + 1) * 8);
-#pragma unroll 1
-        for (uint32_t t = i + 1; (t & 1u) == 0; t >>= 1, depth--)  // a power-of-two group ends here
-            st.merge_top(cur, (root && pow2 && i + 1 == m && t == 2) ? ROOT : 0u);
-        if (i + 1 < m) {
-            st.push(cur);
-            depth++;
-        }
-    }
-#pragma unroll 1
-    for (; depth > 0; depth--) st.merge_top(cur, (root && depth == 1) ? ROOT : 0u);
-    store_cv((root ? out : dst) + (size_t)it.z * 8, cur);
-#endif
 }
 
 // 32-byte hash rows src[i] -> out[idx[i]] (whole-file cas messages hashed by the checksum
