@@ -24,7 +24,7 @@
 // Build (on the CPU container; runs on the GPU box):
 //   hipcc -O2 -std=c++17 -mavx2 -o scripts/ck_host_cost scripts/ck_host_cost.cpp \
 //         -Lspacedrive_amd -lsdcas -Wl,-rpath,'$ORIGIN/../spacedrive_amd' -lpthread
-// Run: scripts/ck_host_cost [NF=32] [FL_MiB=256] [ghz=2.4] [quick|bound]  -> JSON lines on stdout
+// Run: scripts/ck_host_cost [NF=32] [FL_MiB=256] [ghz=2.4] [quick|bound|wc]  -> JSON lines on stdout
 // ("quick": read_hash, read_hot_nt_dma and the hot_nt split at 16 threads only, for A/Bs
 // such as scripts/numa_probe.sh's thread placements; "bound", VERDICT r4 item 3: what bounds
 // the split -- STREAM-like host DRAM legs on 16 threads (read, non-temporal write, copy), the
@@ -128,7 +128,7 @@ struct Res {
     uint64_t bytes_dma = 0;  // of which the threads that DMA'd them to the device moved
 };
 
-enum Kind { READ_PINNED, READ_HOT_NT, READ_HASH, READ_HOT, HASH_HOT, ZERO_COPY };
+enum Kind { READ_PINNED, READ_HOT_NT, READ_HASH, READ_HOT, HASH_HOT, ZERO_COPY, READ_PINNED_WC };
 
 // STREAM-like legs over an anonymous buffer, T threads, each its contiguous slice (first
 // touched by that thread): kind 0 = read (AVX2 loads, summed), 1 = non-temporal write,
@@ -167,10 +167,11 @@ double stream_leg(int kind, int T, uint8_t* a, uint8_t* b, uint64_t len, int rep
     const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return (double)per * T * reps / wall / 1e9 + (sink.load() == 42 ? 1e-12 : 0.0);
 }
-const char* NAMES[] = {"read_pinned", "read_hot_nt", "read_hash", "read_hot", "hash_hot", "zero_copy"};
+const char* NAMES[] = {"read_pinned", "read_hot_nt", "read_hash", "read_hot", "hash_hot", "zero_copy", "read_pinned_wc"};
 
 struct ThreadBufs {
     uint8_t* pinned[2] = {nullptr, nullptr};  // two UNIT windows (double buffer for the DMA)
+    uint8_t* wc[2] = {nullptr, nullptr};      // the same, write-combined ("wc" mode)
     uint8_t* hot = nullptr;                   // 1 MiB, cache-resident working buffer
     void* dev = nullptr;
     hipStream_t s = nullptr;
@@ -241,10 +242,11 @@ Res run(const std::vector<int>& kinds, const std::vector<int>& dma, std::vector<
                     HIPOK(hipEventSynchronize(B.ev[b]));
                     B.pending[b] = false;
                 }
-                uint8_t* win = B.pinned[b];
+                uint8_t* win = kind == READ_PINNED_WC ? B.wc[b] : B.pinned[b];
                 for (uint64_t o = 0; o < UNIT;) {
                     switch (kind) {
                         case READ_PINNED:
+                        case READ_PINNED_WC:
                             if (pread_all(fd, win + o, MiB, base + o) != (int64_t)MiB) exit(6);
                             o += MiB;
                             break;
@@ -332,6 +334,33 @@ int main(int argc, char** argv) {
     // page cache warm (the files were just written) -- one untimed pass anyway
     run(std::vector<int>(TMAX, READ_HOT), std::vector<int>(TMAX, 0), bufs);
     const bool bound = argc > 4 && strcmp(argv[4], "bound") == 0;
+    if (argc > 4 && strcmp(argv[4], "wc") == 0) {
+        // (round 5) preads straight into write-combined pinned windows: one pass, no
+        // read-for-ownership of the destination, against read_pinned (write-back windows)
+        // and read_hot_nt (a cache-resident bounce buffer + streaming stores)
+        for (auto& B : bufs)
+            for (int k = 0; k < 2; k++) {
+                HIPOK(hipHostMalloc(reinterpret_cast<void**>(&B.wc[k]), UNIT, hipHostMallocWriteCombined));
+                memset(B.wc[k], 0, UNIT);
+            }
+        for (int rep = 0; rep < 3; rep++) {
+            for (int kind : {READ_PINNED, READ_HOT_NT, READ_PINNED_WC})
+                report(NAMES[kind], 1, 0, run(std::vector<int>(1, kind), std::vector<int>(1, 0), bufs));
+            for (int kind : {READ_PINNED, READ_HOT_NT, READ_PINNED_WC}) {
+                const std::string name = std::string(NAMES[kind]) + "_dma";
+                for (int T : {4, 6})
+                    report(name.c_str(), T, T, run(std::vector<int>(T, kind), std::vector<int>(T, 1), bufs));
+            }
+            for (int gk : {READ_HOT_NT, READ_PINNED_WC}) {
+                std::vector<int> kinds(TMAX, READ_HASH), dma(TMAX, 0);
+                for (int t = 0; t < 6; t++) kinds[t] = gk, dma[t] = 1;
+                report(gk == READ_HOT_NT ? "hybrid_hot_nt" : "hybrid_pinned_wc", TMAX, 6, run(kinds, dma, bufs));
+            }
+        }
+        for (int f = 0; f < NF; f++) unlink(path_of(f).c_str());
+        rmdir(DIR.c_str());
+        return 0;
+    }
     if (bound) {
         const uint64_t SLEN = 4ull << 30;  // two 4 GiB anonymous buffers: far past the caches
         uint8_t* sa = static_cast<uint8_t*>(aligned_alloc(4096, SLEN));
