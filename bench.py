@@ -265,6 +265,26 @@ def pmc_traffic_sum(kernels, grids):
             "fetch_factor": parts[0]["fetch_factor"], "per_kernel": {k: p["bytes"] for k, p in zip(kernels, parts)}}
 
 
+def pmc_issue_rate(kernel: str, grid: int):
+    """VALU lane-ops per clock per CU of `kernel` at launch shape `grid` from the committed
+    PMC summary: SQ_INSTS_VALU x 64 lanes / (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs), against the
+    G mix's measured ceiling of G_MIX_LANE_OPS_PER_CLK -- a per-clock figure, so the board's
+    clock drops out.  GRBM_GUI_ACTIVE also counts busy cycles around the launch, so the rate
+    is a slight underestimate.  None when no pass measured that shape."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
+        for e in d["kernels"].get(kernel, []):
+            c = e.get("counters", {})
+            if int(e["grid"]) == int(grid) and c.get("SQ_INSTS_VALU") and c.get("GRBM_GUI_ACTIVE"):
+                r = c["SQ_INSTS_VALU"] * 64 / (c["GRBM_GUI_ACTIVE"] / 8 * N_CUS)
+                return {"lane_ops_per_clk_cu": r, "ceiling": G_MIX_LANE_OPS_PER_CLK,
+                        "frac": r / G_MIX_LANE_OPS_PER_CLK, "kernel": kernel, "grid": grid, "tag": d.get("tag"),
+                        "source": "profiles/pmc_summary.json (rocprofv3 --pmc SQ_INSTS_VALU ... GRBM_GUI_ACTIVE)"}
+    except (OSError, KeyError, ValueError, TypeError, AttributeError, ZeroDivisionError):
+        pass
+    return None
+
+
 def whole_grid(batch) -> int:
     return ((batch.full_items + 255) // 256 + (batch.tail_items + 255) // 256) * 256
 
@@ -815,6 +835,7 @@ def config_leg(ctx, which: str, nfiles: int, reps: int, dev, stream, valu_peak: 
                                   / (G_MIX_LANE_OPS_PER_CLK * N_CUS * clock_res["sclk_mhz_median"] * 1e6)
                                   if clock_res else None),
            "kernels": kernels, "launch_grid": grid,
+           "issue_rate_pmc": pmc_issue_rate(kernels[0], grid[0] if isinstance(grid, list) else grid),
            "traffic": tr["bytes"] if tr else None, "deterministic": deterministic,
            "parity": parity(ps["files"], ps["mismatches"], "full 32-byte hashes of an even-stride sample (+ the first "
                             "32) vs the C oracle (oracle/sd_oracle.c) on the same generator"),
@@ -1679,6 +1700,7 @@ def main():
                          if clock_res else None),
                      "measured_valu_peak": valu_peak / 1e12,
                      "frac_of_measured_peak": dom["achieved"] * 1e12 / valu_peak if valu_peak else None,
+                     "issue_rate_pmc": pmc_issue_rate(SAMPLED_KERNELS[0], s_grid[0]),
                      "hbm": {"achieved": dom_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                              "frac": dom_gbps / HBM_PEAK_GBPS},
                      "phase": {"kernels": SAMPLED_KERNELS + ["k_whole_items", "k_whole_merge8"], "ms": hash_ms,
@@ -1795,6 +1817,7 @@ def main():
                                             roof["achieved"] * 1e12
                                             / (G_MIX_LANE_OPS_PER_CLK * N_CUS * ck_clock["sclk_mhz_median"] * 1e6)
                                             if ck_clock else None),
+                                        "issue_rate_pmc": pmc_issue_rate("k_ck_leaf", cb.blocks * 256),
                                         "hbm": {"achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                                 "frac": gbps / HBM_PEAK_GBPS}},
                            "launch_grid": cb.blocks * 256, "traffic": tr_ck["bytes"] if tr_ck else None}

@@ -213,3 +213,21 @@ def test_library_digest_equals_the_oracle_for_one_shard(oracle_native):
     ids = oracle_native.cas_ids_synth_simd(s, c, t, nthreads=min(8, os.cpu_count() or 1))
     assert bench.cas_digest(ids) == bench.golden_checksums()["cas_digest"][
         bench.library_digest_key(1_250_000, 1_250_000, 2_500_000)]
+
+
+def test_pmc_lookups_cover_the_default_launch_shapes():
+    """The committed PMC summary holds the default run's dominant launch shapes: the sampled
+    pair of a 1.25 M-file shard and configs[3]'s 16 x 4 GiB leaf launch -- HBM bytes per launch
+    (`traffic`) and the per-clock issue rate (`issue_rate_pmc`), the latter at the G mix's
+    ceiling within 5 %."""
+    from spacedrive_amd import synth
+    sizes, _, _ = synth.library(0, 1_250_000, 1_250_000)  # the default shard (--files-per-gpu)
+    n_sampled = int((sizes > 102400).sum())
+    grids = bench.sampled_grids(n_sampled)
+    tr = bench.pmc_traffic_sum(bench.SAMPLED_KERNELS, grids)
+    assert tr is not None and 0.99 < tr["bytes"] / (n_sampled * (57352 + 32)) < 1.02
+    r = bench.pmc_issue_rate(bench.SAMPLED_KERNELS[0], grids[0])
+    assert r is not None and 0.95 < r["frac"] <= 1.02, r
+    ck = bench.pmc_issue_rate("k_ck_leaf", 16 * 4096 * 256)
+    assert ck is not None and 0.95 < ck["frac"] <= 1.02, ck
+    assert bench.pmc_issue_rate("k_cas_sampled_lanes", 12345) is None
