@@ -24,7 +24,8 @@
 // Build (on the CPU container; runs on the GPU box):
 //   hipcc -O2 -std=c++17 -mavx2 -o scripts/ck_host_cost scripts/ck_host_cost.cpp \
 //         -Lspacedrive_amd -lsdcas -Wl,-rpath,'$ORIGIN/../spacedrive_amd' -lpthread
-// Run: scripts/ck_host_cost [NF=32] [FL_MiB=256] [ghz=2.4] [quick|bound|wc]  -> JSON lines on stdout
+// Run: scripts/ck_host_cost [NF=32] [FL_MiB=256] [ghz=2.4] [quick|bound|wc|cold]  -> JSON lines on stdout
+// (cold: SD_CK_DIR=<dir on a real filesystem>; every leg evicts the files first)
 // ("quick": read_hash, read_hot_nt_dma and the hot_nt split at 16 threads only, for A/Bs
 // such as scripts/numa_probe.sh's thread placements; "bound", VERDICT r4 item 3: what bounds
 // the split -- STREAM-like host DRAM legs on 16 threads (read, non-temporal write, copy), the
@@ -59,7 +60,7 @@ constexpr uint64_t UNIT = 64ull << 20, MiB = 1ull << 20, HOT = 256ull << 10;
 int NF = 32;
 uint64_t FL = 256 * MiB;
 double GHZ = 2.4;
-std::string DIR = "/dev/shm/sd_ckcost";
+std::string DIR = getenv("SD_CK_DIR") ? getenv("SD_CK_DIR") : "/dev/shm/sd_ckcost";
 
 #define HIPOK(x)                                                                  \
     do {                                                                          \
@@ -122,13 +123,26 @@ void make_files() {
     for (auto& x : th) x.join();
 }
 
+// drop every file's pages from the page cache (written files are fsync'ed first): the
+// next reads go to the storage ("cold" mode)
+void evict_all() {
+    for (int f = 0; f < NF; f++) {
+        const int fd = open(path_of(f).c_str(), O_RDONLY);
+        if (fd < 0) exit(8);
+        fsync(fd);
+        posix_fadvise(fd, 0, 0, POSIX_FADV_DONTNEED);
+        close(fd);
+    }
+}
+
 struct Res {
     double wall = 0, cpu = 0;
     uint64_t bytes = 0;
     uint64_t bytes_dma = 0;  // of which the threads that DMA'd them to the device moved
 };
 
-enum Kind { READ_PINNED, READ_HOT_NT, READ_HASH, READ_HOT, HASH_HOT, ZERO_COPY, READ_PINNED_WC };
+enum Kind { READ_PINNED, READ_HOT_NT, READ_HASH, READ_HOT, HASH_HOT, ZERO_COPY, READ_PINNED_WC, READ_HASH_DIRECT,
+            READ_PINNED_DIRECT };
 
 // STREAM-like legs over an anonymous buffer, T threads, each its contiguous slice (first
 // touched by that thread): kind 0 = read (AVX2 loads, summed), 1 = non-temporal write,
@@ -167,7 +181,8 @@ double stream_leg(int kind, int T, uint8_t* a, uint8_t* b, uint64_t len, int rep
     const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return (double)per * T * reps / wall / 1e9 + (sink.load() == 42 ? 1e-12 : 0.0);
 }
-const char* NAMES[] = {"read_pinned", "read_hot_nt", "read_hash", "read_hot", "hash_hot", "zero_copy", "read_pinned_wc"};
+const char* NAMES[] = {"read_pinned", "read_hot_nt", "read_hash", "read_hot", "hash_hot", "zero_copy", "read_pinned_wc",
+                       "read_hash_direct", "read_pinned_direct"};
 
 struct ThreadBufs {
     uint8_t* pinned[2] = {nullptr, nullptr};  // two UNIT windows (double buffer for the DMA)
@@ -222,7 +237,8 @@ Res run(const std::vector<int>& kinds, const std::vector<int>& dma, std::vector<
                 if (u >= units) break;
                 const int f = (int)(u / per_file);
                 const uint64_t base = (u % per_file) * UNIT;
-                const int fd = open(path_of(f).c_str(), O_RDONLY);
+                const bool direct = kind == READ_HASH_DIRECT || kind == READ_PINNED_DIRECT;
+                const int fd = open(path_of(f).c_str(), O_RDONLY | (direct ? O_DIRECT : 0));
                 if (fd < 0) exit(5);
                 if (kind == ZERO_COPY) {  // map + pin this unit, DMA it, release the one before
                     void* m = mmap(nullptr, UNIT, PROT_READ, MAP_SHARED, fd, (off_t)base);
@@ -247,6 +263,7 @@ Res run(const std::vector<int>& kinds, const std::vector<int>& dma, std::vector<
                     switch (kind) {
                         case READ_PINNED:
                         case READ_PINNED_WC:
+                        case READ_PINNED_DIRECT:
                             if (pread_all(fd, win + o, MiB, base + o) != (int64_t)MiB) exit(6);
                             o += MiB;
                             break;
@@ -255,7 +272,8 @@ Res run(const std::vector<int>& kinds, const std::vector<int>& dma, std::vector<
                             nt_copy(win + o, B.hot, HOT);
                             o += HOT;
                             break;
-                        case READ_HASH: {
+                        case READ_HASH:
+                        case READ_HASH_DIRECT: {
                             if (pread_all(fd, B.hot, MiB, base + o) != (int64_t)MiB) exit(6);
                             const uint64_t off = 0, len = MiB;
                             sd_cpu_checksums(B.hot, &off, &len, 1, hash, 1);
@@ -334,6 +352,34 @@ int main(int argc, char** argv) {
     // page cache warm (the files were just written) -- one untimed pass anyway
     run(std::vector<int>(TMAX, READ_HOT), std::vector<int>(TMAX, 0), bufs);
     const bool bound = argc > 4 && strcmp(argv[4], "bound") == 0;
+    if (argc > 4 && strcmp(argv[4], "cold") == 0) {
+        // (round 5) every leg from cold files (evicted before it runs, SD_CK_DIR on a real
+        // filesystem): buffered preads (today's routes) against O_DIRECT ones -- into the
+        // cache-resident buffer for the CPU path's hashing, straight into the pinned window
+        // (the DMA source: no host copy at all) for the GPU route
+        auto leg = [&](const char* name, int T, int g, std::vector<int> kinds, std::vector<int> dma) {
+            evict_all();
+            report(name, T, g, run(kinds, dma, bufs));
+        };
+        for (int rep = 0; rep < 3; rep++) {
+            leg("read_hash", TMAX, 0, std::vector<int>(TMAX, READ_HASH), std::vector<int>(TMAX, 0));
+            leg("read_hash_direct", TMAX, 0, std::vector<int>(TMAX, READ_HASH_DIRECT), std::vector<int>(TMAX, 0));
+            leg("read_hot", TMAX, 0, std::vector<int>(TMAX, READ_HOT), std::vector<int>(TMAX, 0));
+            for (int g : {4, 8}) {
+                leg("read_hot_nt_dma", g, g, std::vector<int>(g, READ_HOT_NT), std::vector<int>(g, 1));
+                leg("read_pinned_direct_dma", g, g, std::vector<int>(g, READ_PINNED_DIRECT), std::vector<int>(g, 1));
+            }
+            for (int g : {6}) {
+                std::vector<int> k1(TMAX, READ_HASH), d1(TMAX, 0), k2(TMAX, READ_HASH_DIRECT), d2(TMAX, 0);
+                for (int t = 0; t < g; t++) k1[t] = READ_HOT_NT, d1[t] = 1, k2[t] = READ_PINNED_DIRECT, d2[t] = 1;
+                leg("hybrid_hot_nt", TMAX, g, k1, d1);
+                leg("hybrid_direct", TMAX, g, k2, d2);
+            }
+        }
+        for (int f = 0; f < NF; f++) unlink(path_of(f).c_str());
+        rmdir(DIR.c_str());
+        return 0;
+    }
     if (argc > 4 && strcmp(argv[4], "wc") == 0) {
         // (round 5) preads straight into write-combined pinned windows: one pass, no
         // read-for-ownership of the destination, against read_pinned (write-back windows)
