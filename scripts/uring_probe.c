@@ -15,7 +15,8 @@
 // Every result byte is compared between the modes.
 //
 // Build: gcc -O2 -o scripts/uring_probe scripts/uring_probe.c -lpthread
-// Run:   scripts/uring_probe [nfiles=200000] [threads=16] [batch=32]
+// Run:   scripts/uring_probe [nfiles=200000] [threads=16] [batch=32] [rd]
+//        (rd, round 5: the reads only through io_uring, opens and closes plain syscalls)
 #define _GNU_SOURCE
 #include <errno.h>
 #include <fcntl.h>
@@ -305,6 +306,99 @@ static void* worker_uring(void* arg) {
     return NULL;
 }
 
+// ---------------------------------------------------------------- io_uring for the reads only
+// (round 5) the opens and closes stay plain syscalls on the thread's private fd table (round
+// 4's OPENAT went to io-wq workers); a batch of B files' reads is one io_uring_enter, each
+// read on a plain descriptor, completed inline when the pages are cached
+static volatile int cursor_c;
+static int urd_failed;
+static uint64_t* dig_c;
+static void* worker_uring_rd(void* arg) {
+    (void)arg;
+    unshare(CLONE_FILES);
+    struct ring r;
+    const int rc = ring_init(&r, 1024);
+    if (rc < 0) {
+        fprintf(stderr, "io_uring setup: %s\n", strerror(-rc));
+        urd_failed = 1;
+        return NULL;
+    }
+    uint8_t* dst = aligned_alloc(4096, (size_t)SLOT * B);
+    int64_t res[64][6];
+    int fds[64];
+    for (;;) {
+        const int i0 = __atomic_fetch_add(&cursor_c, B, __ATOMIC_RELAXED);
+        if (i0 >= NF) break;
+        const int nb = i0 + B <= NF ? B : NF - i0;
+        int nsqe = 0;
+        for (int q = 0; q < nb; q++) {
+            const int i = i0 + q;
+            char p[256];
+            path_of(i, p);
+            fds[q] = open(p, O_RDONLY | O_CLOEXEC);
+            for (int k = 0; k < 6; k++) res[q][k] = INT64_MIN;
+            res[q][0] = fds[q] < 0 ? -errno : 0;
+            if (fds[q] < 0) continue;
+            uint64_t off[5], len[5];
+            const int n = plan(i, off, len);
+            uint64_t pos = 0;
+            for (int k = 0; k < n; k++) {
+                struct io_uring_sqe* sq = sqe_get(&r);
+                sq->opcode = IORING_OP_READ;
+                sq->fd = fds[q];
+                sq->addr = (uint64_t)(uintptr_t)(dst + (size_t)q * SLOT + pos);
+                sq->len = (uint32_t)len[k];
+                sq->off = off[k];
+                sq->user_data = ((uint64_t)q << 8) | (uint64_t)(k + 1);
+                pos += len[k];
+            }
+            nsqe += n;
+        }
+        int done = 0;
+        while (done < nsqe) {
+            const int sub = done == 0 ? nsqe : 0;
+            if (syscall(__NR_io_uring_enter, r.fd, sub, nsqe - done, IORING_ENTER_GETEVENTS, NULL, 0) < 0 &&
+                errno != EINTR) {
+                fprintf(stderr, "io_uring_enter: %s\n", strerror(errno));
+                urd_failed = 1;
+                return NULL;
+            }
+            unsigned head = *r.cq_head;
+            const unsigned tail = __atomic_load_n(r.cq_tail, __ATOMIC_ACQUIRE);
+            for (; head != tail; head++) {
+                const struct io_uring_cqe* c = &r.cqes[head & *r.cq_mask];
+                res[c->user_data >> 8][c->user_data & 0xFF] = c->res;
+                done++;
+            }
+            __atomic_store_n(r.cq_head, head, __ATOMIC_RELEASE);
+        }
+        for (int q = 0; q < nb; q++) {
+            const int i = i0 + q;
+            if (fds[q] >= 0) close(fds[q]);
+            uint64_t off[5], len[5];
+            const int n = plan(i, off, len);
+            int64_t st = res[q][0];
+            uint64_t got = 0, pos = 0;
+            // the pread mode reads each window right after the last, stopping at an error;
+            // its digest covers the bytes up to the first error, in order
+            for (int k = 0; k < n && res[q][0] >= 0; k++) {
+                if (res[q][k + 1] < 0) {
+                    st = res[q][k + 1];
+                    break;
+                }
+                st = st * 131 + res[q][k + 1];
+                if (pos != got) memmove(dst + (size_t)q * SLOT + got, dst + (size_t)q * SLOT + pos, (size_t)res[q][k + 1]);
+                got += (uint64_t)res[q][k + 1];
+                pos += len[k];
+            }
+            dig_c[i] = digest(dst + (size_t)q * SLOT, got, st);
+        }
+    }
+    free(dst);
+    close(r.fd);
+    return NULL;
+}
+
 static double run(void* (*fn)(void*), double* us_per_file) {
     pthread_t th[256];
     const double c0 = cpu_s(), t0 = now();
@@ -323,7 +417,32 @@ int main(int argc, char** argv) {
     make_files();
     dig_a = calloc(NF, 8);
     dig_b = calloc(NF, 8);
+    dig_c = calloc(NF, 8);
     double us;
+    if (argc > 4 && strcmp(argv[4], "rd") == 0) {  // pread vs io_uring for the reads only
+        for (int rnd = 0; rnd < 3; rnd++) {
+            cursor_a = 0;
+            const double ra = run(worker_pread, &us);
+            printf("{\"mode\": \"pread\", \"round\": %d, \"threads\": %d, \"files_per_s\": %.0f, "
+                   "\"cpu_us_per_file\": %.2f}\n", rnd, T, ra, us);
+            cursor_c = 0;
+            const double rc = run(worker_uring_rd, &us);
+            int same = 1;
+            for (int i = 0; i < NF; i++) same &= dig_a[i] == dig_c[i];
+            printf("{\"mode\": \"uring_reads\", \"round\": %d, \"threads\": %d, \"batch\": %d, \"files_per_s\": %.0f, "
+                   "\"cpu_us_per_file\": %.2f, \"same_bytes\": %s, \"failed\": %d}\n",
+                   rnd, T, B, rc, us, same ? "true" : "false", urd_failed);
+            fflush(stdout);
+            if (urd_failed) break;
+        }
+        char p[256];
+        for (int i = 0; i < NF; i++) {
+            path_of(i, p);
+            unlink(p);
+        }
+        rmdir(DIR);
+        return 0;
+    }
     for (int rnd = 0; rnd < 3; rnd++) {
         cursor_a = 0;
         const double ra = run(worker_pread, &us);
