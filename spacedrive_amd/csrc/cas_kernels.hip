@@ -9,9 +9,10 @@
 //                   cost-sorted partial / short pairs), then two level-wise merge passes of
 //                   <= 8 pair nodes per lane.
 //   k_ck_leaf       file_checksum (hash.rs:10-24), and whole-file cas messages longer than
-//   k_ck_reduce     the work-list path takes: one 256-lane workgroup per 1 MiB of a
-//                   message, 4 consecutive chunks per lane merged in-lane, 256 lane CVs
-//                   merged in LDS; then 256-way LDS reductions over the block CVs.
+//   k_ck_reduce     the work-list path takes: 256 lanes per 1 MiB block of a message, two
+//                   blocks per workgroup, 4 consecutive chunks per lane merged in-lane, each
+//                   block's 256 lane CVs merged in LDS (both trees packed into the lowest
+//                   lanes); then 256-way LDS reductions over the block CVs.
 //
 // Tree shape: every merge is the level-wise pairwise merge with the odd node carried up
 // unchanged, over power-of-two aligned groups.  It is the BLAKE3 tree (left subtree =
@@ -363,72 +364,124 @@ __global__ __launch_bounds__(256) void k_scatter_hash(const uint32_t* __restrict
 }
 
 // ------------------------------------------------------------------------ checksums
-// Leaf: workgroup (256 lanes) = 1 MiB block = 1024 chunks of one message; lane l hashes
-// chunks [4l, 4l+4) and merges them in-lane; then the lane CVs merge in LDS.  Block
-// number = wg_map[blockIdx.x].y + blk_base; `shift` is subtracted from the message's
-// byte offset (a streamed window holds message bytes [shift, shift + window)).
-constexpr uint32_t CK_LANE_CHUNKS = 4;
+// Leaf: 1 MiB blocks = 1024 chunks of one message, CK_WG_BLOCKS (2) blocks per workgroup of
+// 256 lanes each.  Lane l of a block hashes its chunks [4l, 4l+4) one after the other
+// (line-pair loads) and merges them in-lane with the CV stack; then the lane CVs of each
+// block merge level-wise in LDS with the blocks' trees packed together: at tree level L the
+// parents of both blocks sit in the lowest lanes, so the workgroup's waves run partly masked
+// only at the top levels, once per two blocks (round 5: with one block per workgroup its
+// 8-level tree left 321 lane-compressions of every 17 728 masked, 1.8 %; two blocks leave
+// 129 per block -- 0.3-1.2 % faster, profiles/r5/r5zk_ck_leaf_ab/; 16- or 8-chunk lanes
+// with 4 or 2 blocks per 256-lane workgroup lost it again to 4x / 2x longer workgroups, and
+// 4 blocks of 256 lanes per workgroup to occupancy, r5zk1 and r5zk).  Block number =
+// wg_map[i].y + blk_base for entry i = CK_WG_BLOCKS x workgroup + (lane / 256); `shift` is
+// subtracted from the message's byte offset (a streamed window holds message bytes
+// [shift, shift + window)).
+#ifndef SD_CK_LANE_CHUNKS
+#define SD_CK_LANE_CHUNKS 4
+#endif
+#ifndef SD_CK_WG_BLOCKS
+#define SD_CK_WG_BLOCKS 2
+#endif
 constexpr uint32_t CK_BLOCK_CHUNKS = 1024;
+constexpr uint32_t CK_LANE_CHUNKS = SD_CK_LANE_CHUNKS;
+constexpr uint32_t CK_BLOCK_LANES = CK_BLOCK_CHUNKS / CK_LANE_CHUNKS;
+constexpr uint32_t CK_WG_BLOCKS = SD_CK_WG_BLOCKS;
+constexpr uint32_t CK_WG_THREADS = CK_BLOCK_LANES * CK_WG_BLOCKS;
+constexpr uint32_t CK_TREE_LEVELS = ilog2(CK_BLOCK_LANES);
+static_assert((CK_LANE_CHUNKS & (CK_LANE_CHUNKS - 1)) == 0 && CK_LANE_CHUNKS >= 2 && CK_LANE_CHUNKS <= 16, "lane chunks");
+static_assert(CK_WG_THREADS >= 64 && CK_WG_THREADS <= 1024 && CK_WG_THREADS % 64 == 0, "workgroup size");
 
-__global__ __launch_bounds__(256) void k_ck_leaf(const uint8_t* __restrict__ data, uint64_t shift, uint32_t blk_base,
-                                                 const ck_file* __restrict__ files, const uint2* __restrict__ wg_map,
-                                                 uint32_t* __restrict__ cvbuf, uint32_t* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[256][8];
-    const uint2 wm = wg_map[blockIdx.x];  // (file, block)
-    const uint32_t blk = wm.y + blk_base;
-    const ck_file fi = files[wm.x];
-    const uint64_t nchunks = fi.len == 0 ? 1 : (fi.len + CHUNK_LEN - 1) / CHUNK_LEN;
-    const uint64_t blk0 = (uint64_t)blk * CK_BLOCK_CHUNKS;
-    const uint64_t blk_chunks64 = nchunks - blk0 < CK_BLOCK_CHUNKS ? nchunks - blk0 : CK_BLOCK_CHUNKS;
-    const uint32_t blk_chunks = (uint32_t)blk_chunks64;
-    const uint32_t t = threadIdx.x;
-    const uint32_t c0 = t * CK_LANE_CHUNKS;
-    const bool file_is_lane = nchunks <= CK_LANE_CHUNKS;  // whole message inside lane 0
-    if (c0 < blk_chunks) {
-        const uint32_t nch = blk_chunks - c0 < CK_LANE_CHUNKS ? blk_chunks - c0 : CK_LANE_CHUNKS;
-        const uint8_t* p = data + (fi.offset - shift);
-        uint32_t acc[8], cv[8], tmp[8];
-        for (uint32_t j = 0; j < nch; j++) {
-            const uint64_t ci = blk0 + c0 + j;
-            const uint64_t rem = fi.len - ci * CHUNK_LEN;
-            const uint32_t len = fi.len == 0 ? 0u : (rem < CHUNK_LEN ? (uint32_t)rem : CHUNK_LEN);
-            if (len == CHUNK_LEN && !(file_is_lane && nchunks == 1)) full_chunk_cv_lp(cv, p + ci * CHUNK_LEN, ci);
-            else chunk_cv(cv, p + ci * CHUNK_LEN, len, ci, nchunks == 1);
-            // level-wise in-lane merge of up to 4 chunks: ((0,1),(2,3)) or ((0,1),2)
-            if (j == 0) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) acc[i] = cv[i];
-            } else if (j == 1) {
-                const bool root = file_is_lane && nch == 2;
-                parent(tmp, acc, cv, root ? ROOT : 0u);
-#pragma unroll
-                for (int i = 0; i < 8; i++) acc[i] = tmp[i];
-            } else if (j == 2) {
-                if (nch == 3) {
-                    parent(tmp, acc, cv, file_is_lane ? ROOT : 0u);
-#pragma unroll
-                    for (int i = 0; i < 8; i++) acc[i] = tmp[i];
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 8; i++) tmp[i] = cv[i];  // hold chunk 2
+__global__ __launch_bounds__(CK_WG_THREADS) void k_ck_leaf(
+    const uint8_t* __restrict__ data, uint64_t shift, uint32_t blk_base, const ck_file* __restrict__ files,
+    const uint2* __restrict__ wg_map, uint32_t n_blocks, uint32_t* __restrict__ cvbuf, uint32_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[CK_WG_THREADS][8];
+    __shared__ uint32_t s_lanes[CK_WG_BLOCKS], s_root[CK_WG_BLOCKS];
+    __shared__ uint64_t s_dst[CK_WG_BLOCKS];  // output row: file (root) or CV slot, | 1 << 63 for out
+    const uint32_t t = threadIdx.x, wv = t / CK_BLOCK_LANES, lane = t % CK_BLOCK_LANES;
+    const uint32_t bi = blockIdx.x * CK_WG_BLOCKS + wv;  // this lane's block entry
+    uint32_t lanes_b = 0, root_b = 0;
+    uint64_t dst_b = 0;
+    if (bi < n_blocks) {
+        const uint2 wm = wg_map[bi];  // (file, block)
+        const uint32_t blk = wm.y + blk_base;
+        const ck_file fi = files[wm.x];
+        const uint64_t nchunks = fi.len == 0 ? 1 : (fi.len + CHUNK_LEN - 1) / CHUNK_LEN;
+        const uint64_t blk0 = (uint64_t)blk * CK_BLOCK_CHUNKS;
+        const uint32_t blk_chunks = (uint32_t)(nchunks - blk0 < CK_BLOCK_CHUNKS ? nchunks - blk0 : CK_BLOCK_CHUNKS);
+        const bool file_is_block = nchunks <= CK_BLOCK_CHUNKS;
+        const bool file_is_lane = nchunks <= CK_LANE_CHUNKS;  // the whole message inside lane 0
+        lanes_b = (blk_chunks + CK_LANE_CHUNKS - 1) / CK_LANE_CHUNKS;
+        root_b = file_is_block && !file_is_lane;
+        dst_b = file_is_block ? ((uint64_t)wm.x | (1ull << 63)) : fi.cv_base + blk;
+        const uint32_t c0 = lane * CK_LANE_CHUNKS;
+        if (c0 < blk_chunks) {
+            const uint32_t nch = blk_chunks - c0 < CK_LANE_CHUNKS ? blk_chunks - c0 : CK_LANE_CHUNKS;
+            const uint8_t* p = data + (fi.offset - shift);
+            CvStack<ilog2(CK_LANE_CHUNKS)> st;  // after chunk j it holds popcount(j + 1) subtrees
+            uint32_t cv[8];
+#pragma unroll 1
+            for (uint32_t j = 0; j < nch; j++) {
+                const uint64_t ci = blk0 + c0 + j;
+                const uint64_t rem = fi.len - ci * CHUNK_LEN;
+                const uint32_t len = fi.len == 0 ? 0u : (rem < CHUNK_LEN ? (uint32_t)rem : CHUNK_LEN);
+                if (len == CHUNK_LEN && nchunks > 1) full_chunk_cv_lp(cv, p + ci * CHUNK_LEN, ci);
+                else chunk_cv(cv, p + ci * CHUNK_LEN, len, ci, nchunks == 1);
+                if (j + 1 < nch) {  // an aligned group that ends here merges, then waits on the stack
+#pragma unroll 1
+                    for (uint32_t g = j + 1; (g & 1u) == 0; g >>= 1) st.merge_top(cv, 0u);
+                    st.push(cv);
+                } else {  // the lane's last chunk: its aligned merges and the fold, one run of
+                          // popcount(nch - 1) merges; ROOT on the last when the file is this lane
+                    const uint32_t ops = (uint32_t)__builtin_popcount(nch - 1);
+#pragma unroll 1
+                    for (uint32_t k = ops; k > 0; k--) st.merge_top(cv, (file_is_lane && k == 1) ? ROOT : 0u);
                 }
-            } else {
-                uint32_t p23[8];
-                parent(p23, tmp, cv, 0u);
-                parent(tmp, acc, p23, file_is_lane ? ROOT : 0u);
-#pragma unroll
-                for (int i = 0; i < 8; i++) acc[i] = tmp[i];
             }
+            store_cv(lds[t], cv);
         }
-        store_cv(lds[t], acc);
+    }
+    if (lane == 0) {
+        s_lanes[wv] = lanes_b;
+        s_root[wv] = root_b;
+        s_dst[wv] = dst_b;
     }
     __syncthreads();
-    const uint32_t lanes = (blk_chunks + CK_LANE_CHUNKS - 1) / CK_LANE_CHUNKS;
-    const bool file_is_block = nchunks <= CK_BLOCK_CHUNKS;
-    lds_reduce(lds, lanes, file_is_block && !file_is_lane);
-    if (t < 8) {
-        if (file_is_block) out[(size_t)wm.x * 8 + t] = lds[0][t];
-        else cvbuf[(fi.cv_base + blk) * 8 + t] = lds[0][t];
+    // the blocks' trees, level-wise with the odd node carried up (CK_BLOCK_LANES -> 1); block
+    // b's level-L nodes at lds[CK_BLOCK_LANES b .. + n_b(L))
+#pragma unroll 1
+    for (uint32_t L = 0; L < CK_TREE_LEVELS; L++) {
+        const uint32_t P = (CK_BLOCK_LANES / 2) >> L;  // parent slots per block at this level
+        uint32_t res[8];
+        bool have = false;
+        uint32_t to = 0;
+        if (t < CK_WG_BLOCKS * P) {
+            const uint32_t b = t / P, j = t - b * P;
+            uint32_t nb = s_lanes[b];
+            for (uint32_t l = 0; l < L; l++) nb = (nb + 1) >> 1;
+            if (2 * j + 1 < nb) {
+                uint32_t l8[8], r8[8];
+                load_cv(l8, lds[CK_BLOCK_LANES * b + 2 * j]);
+                load_cv(r8, lds[CK_BLOCK_LANES * b + 2 * j + 1]);
+                parent(res, l8, r8, (s_root[b] && nb == 2) ? ROOT : 0u);
+                have = true;
+            } else if (2 * j + 1 == nb) {  // the odd last node
+                load_cv(res, lds[CK_BLOCK_LANES * b + 2 * j]);
+                have = true;
+            }
+            to = CK_BLOCK_LANES * b + j;
+        }
+        __syncthreads();
+        if (have) store_cv(lds[to], res);
+        __syncthreads();
+    }
+    if (t < 8 * CK_WG_BLOCKS) {
+        const uint32_t b = t >> 3, w = t & 7u;
+        if (s_lanes[b]) {
+            const uint64_t d = s_dst[b];
+            if (d >> 63) out[(d & ~(1ull << 63)) * 8 + w] = lds[CK_BLOCK_LANES * b][w];
+            else cvbuf[d * 8 + w] = lds[CK_BLOCK_LANES * b][w];
+        }
     }
 }
 
@@ -505,7 +558,8 @@ hipError_t launch_scatter_hash(const uint32_t* src, const uint32_t* idx, uint32_
 hipError_t launch_ck_leaf(const uint8_t* data, uint64_t shift, uint32_t blk_base, const ck_file* files,
                           const uint2* wg_map, uint32_t n_wg, uint32_t* cvbuf, uint32_t* out, hipStream_t s) {
     if (n_wg == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ck_leaf, dim3(n_wg), dim3(256), 0, s, data, shift, blk_base, files, wg_map, cvbuf, out);
+    hipLaunchKernelGGL(k_ck_leaf, dim3((n_wg + CK_WG_BLOCKS - 1) / CK_WG_BLOCKS), dim3(CK_WG_THREADS), 0, s, data, shift,
+                       blk_base, files, wg_map, n_wg, cvbuf, out);
     return hipGetLastError();
 }
 

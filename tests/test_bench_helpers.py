@@ -228,6 +228,6 @@ def test_pmc_lookups_cover_the_default_launch_shapes():
     assert tr is not None and 0.99 < tr["bytes"] / (n_sampled * (57352 + 32)) < 1.02
     r = bench.pmc_issue_rate(bench.SAMPLED_KERNELS[0], grids[0])
     assert r is not None and 0.95 < r["frac"] <= 1.02, r
-    ck = bench.pmc_issue_rate("k_ck_leaf", 16 * 4096 * 256)
+    ck = bench.pmc_issue_rate("k_ck_leaf", bench.ck_leaf_grid(16 * 4096))
     assert ck is not None and 0.95 < ck["frac"] <= 1.02, ck
     assert bench.pmc_issue_rate("k_cas_sampled_lanes", 12345) is None

@@ -74,11 +74,12 @@ def _level_shape_range(a, b):
 
 def test_tree_shapes_equal():
     # SURVEY.md §7 "hard parts": level-wise merge with odd carry == spec tree, 1..600 chunks;
-    # and the kernels' blocked form (4-chunk lanes, 1024-chunk workgroups, 256-way groups)
+    # and the kernels' blocked form (4- or 16-chunk lanes, 1024-chunk blocks, 256-way groups)
     for n in range(1, 601):
         s = _stack_shape(n)
         assert _level_shape(n) == s, n
         assert _blocked_shape(n, 4) == s, n
+        assert _blocked_shape(n, 16) == s, n
         assert _blocked_shape(n, 64) == s, n
     for n in (1023, 1024, 1025, 4097, 70000):
         assert _blocked_shape(n, 1024) == _level_shape(n), n
