@@ -1152,13 +1152,18 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
         runs = {k: [] for k in legs}
         routes0 = sd.file_checksums_stats()
         split_bytes = {"gpu": 0, "cpu_in_split": 0}
+        per_call = []  # policy_default: the route each call took ("checksum_split_adapt") and its GB/s
         for rnd in range(4):  # round 0 warms the windows, the pools and the page cache
             for k, f in legs.items():
-                b0 = sd.file_checksums_bytes()
+                b0, r0 = sd.file_checksums_bytes(), sd.file_checksums_stats()
                 t0 = time.perf_counter()
                 got = f()
                 dt = time.perf_counter() - t0
                 assert got == want, k
+                if k == "policy_default":
+                    r1 = sd.file_checksums_stats()
+                    per_call.append({"round": rnd, "route": "split" if r1["hybrid"] > r0["hybrid"] else
+                                     ("cpu" if r1["cpu"] > r0["cpu"] else "gpu"), "GBps": total / dt / 1e9})
                 if rnd:
                     runs[k].append(dt)
                     if k == "policy_default":
@@ -1171,12 +1176,17 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
                       "seconds_median": float(np.median(runs[k])), "rounds": len(runs[k])}
         res["library_cpu_path"]["threads"] = 16
         res["policy_default"]["route"] = {k: routes1[k] - routes0[k] for k in routes1}
+        res["policy_default"]["per_call"] = per_call
+        res["policy_default"]["split_adapt"] = sd.get_tuning("checksum_split_adapt")
         res["policy_default"]["hybrid_threads"] = sd.get_tuning("checksum_hybrid_threads")
         tot = split_bytes["gpu"] + split_bytes["cpu_in_split"]
         res["policy_default"]["gpu_share"] = split_bytes["gpu"] / tot if tot else None
         res["policy_default_over_cpu_path"] = res["policy_default"]["GBps"] / res["library_cpu_path"]["GBps"]
         res["note"] = ("medians of 3 interleaved rounds after a warm one; policy_default splits this call between "
-                       "the GPU route (hybrid_threads readers) and the CPU path (DESIGN.md §4.1)")
+                       "the GPU route (hybrid_threads GPU slots) and the CPU path, or runs the CPU path alone where "
+                       "this context measured it faster (split_adapt: each route once -- the warm call and the "
+                       "first round --, then the faster, the other every split_adapt-th call; per_call; DESIGN.md "
+                       "§4.1)")
         from oracle import native
         bad = sum(native.checksum_synth_mt(flen, 30_000 + i, 0, nthreads=oracle_threads()).hex() != want[i]
                   for i in range(nf))

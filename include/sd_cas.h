@@ -251,7 +251,11 @@ int sd_checksums_stats(sd_cas_ctx* ctx, uint64_t out[2]);
  * to 32 blocks of a file into it (fewer slots under a smaller host budget); otherwise it
  * hashes the small files, then single blocks, on the CPU path; each file's root is merged
  * from both sides' block CVs -- from the page cache 1.13-1.43x the CPU path alone
- * (round 4's whole-file claims, "checksum_split_blocks" 0: 0.9-1.24x).  Any other call of at most "checksum_cpu_max" files is
+ * (round 4's whole-file claims, "checksum_split_blocks" 0: 0.9-1.24x).  On a
+ * host whose threads hash fast the split can lose to them (0.93x on one box), so by default
+ * ("checksum_split_adapt" 8) such a call takes the split or the CPU path alone by the context's
+ * recent GB/s of each: each route once, then the faster, the other every 8th call (the
+ * routes give identical results).  Any other call of at most "checksum_cpu_max" files is
  * hashed by sd_cpu_file_checksums on "read_threads" threads -- by default every such call,
  * because from the page cache the host's threads hash faster than PCIe can carry the bytes
  * to the GPU; "checksum_cpu_max" 0 = the GPU route alone for every call. */
@@ -473,6 +477,9 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * "checksum_split_blocks" (1): sd_file_checksums' split claims work by 1 MiB blocks (the
  * GPU's "checksum_hybrid_threads" slots take runs of blocks while free, the host threads
  * single blocks); 0 = by whole files (round 4);
+ * "checksum_split_adapt" (8): a call the split applies to takes the split or the CPU path
+ * alone, learned per context from the GB/s of its past calls -- each once, then the faster,
+ * the other every k-th call to keep its rate current; 0 = always the split;
  * "host_cohash_threads" (15): host threads hashing beside the GPU in sd_cas_ids calls of
  * >= 8192 files and sd_checksums calls of >= 1 GiB (0 = the GPU alone; never more than the
  * host budget less one in sd_cas_ids, less three in sd_checksums -- 13 of 16 measured best

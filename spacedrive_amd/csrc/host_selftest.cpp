@@ -897,6 +897,34 @@ void test_shared_range_pick() {
     CHECK(shared_range_pick(two.data(), 2, MIN, 10, 55.0, 5.5) == 0);
 }
 
+// sd_file_checksums' learned route (sd_host.h): each route once, then the faster, the other
+// every k-th call; a route that slows down loses its place
+void test_split_routes() {
+    SplitRoutes s;
+    std::vector<int> seen;
+    auto call = [&](double split_gbps, double cpu_gbps, uint32_t k) {
+        const int r = split_route_choose(s, k);
+        split_route_record(s, r, r == 0 ? split_gbps : cpu_gbps);
+        seen.push_back(r);
+        return r;
+    };
+    CHECK(call(120, 100, 8) == 0);  // first: the split
+    CHECK(call(120, 100, 8) == 1);  // then the CPU path once
+    int split_calls = 0, cpu_calls = 0;
+    for (int i = 0; i < 30; i++) (call(120, 100, 8) == 0 ? split_calls : cpu_calls)++;
+    CHECK(split_calls >= 26 && cpu_calls >= 3);  // the faster, and the other every 8th call
+    // the host slows the split down (96 against 103): the CPU path takes over
+    for (int i = 0; i < 6; i++) call(96, 103, 8);
+    int cpu_after = 0;
+    for (int i = 0; i < 16; i++) cpu_after += call(96, 103, 8);
+    CHECK(cpu_after >= 13);
+    // k = 0: no exploring once both are known
+    SplitRoutes t;
+    split_route_record(t, 0, 50);
+    split_route_record(t, 1, 60);
+    for (int i = 0; i < 20; i++) CHECK(split_route_choose(t, 0) == 1);
+}
+
 int main() {
     char tmpl[] = "/tmp/sd_selftest_XXXXXX";
     if (!mkdtemp(tmpl)) return 2;
@@ -914,6 +942,7 @@ int main() {
     test_coalescer();
     test_exchange_plan();
     test_shared_range_pick();
+    test_split_routes();
     test_comm_group();
     test_private_fd_tables();
     test_numa_placement();  // last: it moves the pools' threads

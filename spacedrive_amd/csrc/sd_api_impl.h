@@ -227,6 +227,8 @@ struct sd_cas_ctx {
     std::atomic<uint64_t> checksum_bytes_gpu{0}, checksum_bytes_cpu_split{0};
     std::atomic<uint64_t> cas_ids_gpu_files{0}, cas_ids_host_files{0};  // sd_cas_ids: who hashed
     std::atomic<uint64_t> checksums_gpu_bytes{0}, checksums_host_bytes{0};  // sd_checksums: who hashed
+    std::mutex split_mu;
+    SplitRoutes split_routes;  // sd_file_checksums: the split or the CPU path, learned (sd_host.h)
     std::mutex pool_mu;
     // Reader threads.  stage_pool: tasks that open and close their own files (the cas
     // stager, checksum packs), on private fd tables (stage_pool.h); io_pool: parallel preads

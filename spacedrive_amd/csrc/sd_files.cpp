@@ -980,6 +980,10 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
 //     With "checksum_split_blocks" 0, round 4's split: the GPU route on g reader threads and
 //     the CPU path on the rest on a second host thread, whole large files to whichever is
 //     free next (one shared cursor, largest first; 0.9-1.24x, the last whole file the tail).
+//     The split's gain depends on the host: 0.93-1.34x the CPU path alone on round 5's four
+//     boxes.  So ("checksum_split_adapt" k, default 8) each such call takes the split or the
+//     CPU path alone, by the GB/s this context measured for each: each once, then the
+//     faster, the other every k-th call (split_route_choose, sd_host.h).
 //   * Otherwise calls of at most "checksum_cpu_max" files (default: all) take the CPU path:
 //     from the page cache the host's threads hash faster than PCIe carries the bytes.
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65, int32_t* status) {
@@ -1007,10 +1011,35 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
             }
         }
         if (big.size() >= 2 && big_bytes >= BIG_TOTAL) {
+            // the split, or the CPU path alone where this host has hashed faster by itself
+            // ("checksum_split_adapt" k > 0: each route once, then the faster by its recent
+            // GB/s, the other every k-th call; sd_host.h split_route_choose)
+            const int adapt = std::max(0, tuning_get(SD_TUNE_CHECKSUM_SPLIT_ADAPT));
+            int route = 0;
+            if (adapt) {
+                std::lock_guard<std::mutex> g(ctx->split_mu);
+                route = split_route_choose(ctx->split_routes, (uint32_t)adapt);
+            }
+            uint64_t call_bytes = 0;
+            for (size_t q = 0; q < n; q++) call_bytes += hint[q];
+            const auto t0 = std::chrono::steady_clock::now();
+            auto learn = [&](int r) {
+                if (!adapt) return;
+                const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                std::lock_guard<std::mutex> g(ctx->split_mu);
+                split_route_record(ctx->split_routes, r, (double)call_bytes / std::max(s, 1e-9) / 1e9);
+            };
+            if (route == 1) {
+                ctx->checksum_calls_cpu.fetch_add(1, std::memory_order_relaxed);
+                const int rc = sd_cpu_file_checksums(paths, n, out_hex65, status, threads);
+                if (rc == SD_OK) learn(1);
+                return rc;
+            }
             ctx->checksum_calls_hybrid.fetch_add(1, std::memory_order_relaxed);
             std::stable_sort(big.begin(), big.end(), [&](size_t a, size_t b) { return hint[a] > hint[b]; });
             if (tuning_get(SD_TUNE_CHECKSUM_SPLIT_BLOCKS) != 0) {
                 split_checksums_blocks(ctx, paths, out_hex65, status, threads, hyb, big, rest, hint);
+                learn(0);
                 return SD_OK;
             }
             std::atomic<size_t> cursor{0};
@@ -1097,6 +1126,7 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
             }
             cpu.join();
             if (cpu_rc != SD_OK) throw sd_failure(cpu_rc, cpu_err);
+            learn(0);
             return SD_OK;
         }
     }

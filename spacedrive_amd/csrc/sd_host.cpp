@@ -44,14 +44,15 @@ thread_local std::string g_err;
 // the writer left it, profiles/r4/r4h_numa_lib_probe.json); 15 host threads hashing beside the GPU in
 // large sd_cas_ids calls (profiles/r3/r3ad_cohash_probe.json: 300 000 files from pinned memory,
 // GPU alone 1.89-1.94 M files/s, CPU path alone 2.24-2.36 M, both at once 3.87-4.08 M)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {6}, {15}, {0}, {1}, {0}, {256}, {1}};
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {6}, {15}, {0}, {1}, {0}, {256}, {1}, {8}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
                                                "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",
                                                "files_ring",         "checksum_cpu_max", "files_stage_hot",
                                                "checksum_hybrid_threads", "host_cohash_threads",
                                                "host_cpu_budget",    "checksum_stage_hot", "numa_pin",
-                                               "cpu_read_piece_kib", "checksum_split_blocks"};
+                                               "cpu_read_piece_kib", "checksum_split_blocks",
+                                               "checksum_split_adapt"};
 
 bool read_small(const std::string& path, char* buf, size_t cap) {
     FILE* f = fopen(path.c_str(), "re");
@@ -298,6 +299,21 @@ void sd_set_err(const char* fmt, ...) {
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
     g_err = buf;
+}
+
+int split_route_choose(const SplitRoutes& s, uint32_t explore_every) {
+    if (s.n[0] == 0) return 0;  // each route once
+    if (s.n[1] == 0) return 1;
+    const int better = s.rate[0] >= s.rate[1] ? 0 : 1;
+    if (explore_every && s.calls % explore_every == explore_every - 1) return 1 - better;  // keep the loser's rate current
+    return better;
+}
+
+void split_route_record(SplitRoutes& s, int route, double gbps) {
+    const int r = route ? 1 : 0;
+    s.rate[r] = s.n[r] ? 0.5 * s.rate[r] + 0.5 * gbps : gbps;
+    s.n[r]++;
+    s.calls++;
 }
 
 int tuning_get(int key) { return (key >= 0 && key < SD_TUNE_NKEYS) ? g_tune[key].load(std::memory_order_relaxed) : 0; }

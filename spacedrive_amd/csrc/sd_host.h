@@ -68,7 +68,8 @@ enum sd_tune_key {
     SD_TUNE_NUMA_PIN = 16,                 // library threads on the GPU's NUMA node (0 = float)
     SD_TUNE_CPU_READ_PIECE_KIB = 17,       // CPU path: a 1 MiB block read and hashed in pieces of this size
     SD_TUNE_CHECKSUM_SPLIT_BLOCKS = 18,    // sd_file_checksums' split: 1 = claims by blocks, 0 = by files
-    SD_TUNE_NKEYS = 19
+    SD_TUNE_CHECKSUM_SPLIT_ADAPT = 19,     // split-eligible calls: 0 = always split, k = learn the faster route
+    SD_TUNE_NKEYS = 20
 };
 int tuning_get(int key);
 
@@ -417,4 +418,17 @@ int32_t cpu_checksum_file(const char* path, char out_hex65[65]);
 // the (non-root) chaining value of 1 MiB block `block` of a regular file of file_len >= 2
 // blocks, read from fd at its offset ("cpu_read_piece_kib" pieces); false on a short read
 bool cpu_block_cv_fd(int fd, uint64_t file_len, uint64_t block, uint8_t cv[32]);
+
+// sd_file_checksums' route for a call the split applies to, learned per context (round 5:
+// the split lost 7 % to the CPU path alone on a host whose CPU path read and hashed 103 GB/s
+// from files, and won 34 % on one at 78).  rate[r] is the EWMA of GB/s of
+// route r's past calls (0 = the split, 1 = the CPU path alone), n[r] how many; each route
+// runs once, then the faster one, and every explore_every-th call the other (0 = never).
+struct SplitRoutes {
+    double rate[2] = {0.0, 0.0};
+    uint32_t n[2] = {0, 0};
+    uint64_t calls = 0;
+};
+int split_route_choose(const SplitRoutes& s, uint32_t explore_every);
+void split_route_record(SplitRoutes& s, int route, double gbps);
 void hex_lower(const uint8_t* h, int nbytes, char* out);

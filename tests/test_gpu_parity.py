@@ -533,8 +533,9 @@ def test_file_checksums_hybrid_split(ctx, tmp_path, mode, budget):
     want = dict(zip([p for p in paths if p != fifo], zip(want_h, want_st)))
     from spacedrive_amd._native import check, lib
     keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads", "checksum_split_blocks",
-                                          "host_cpu_budget")}
+                                          "host_cpu_budget", "checksum_split_adapt")}
     sd.set_tuning("checksum_cpu_max", 2147483647)  # the library default (the module sets 0)
+    sd.set_tuning("checksum_split_adapt", 0)  # always the split (the learned route has its own test)
     sd.set_tuning("checksum_hybrid_threads", 4)  # the library default
     sd.set_tuning("checksum_split_blocks", 1 if mode == "blocks" else 0)
     sd.set_tuning("host_cpu_budget", budget)
@@ -600,8 +601,10 @@ def test_file_checksums_split_block_edges(ctx, tmp_path, oracle_native, slots):
             f.truncate(24 * MiB)
         os.chmod(locked, 0)
         paths.insert(4, str(locked))
-    keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads", "checksum_split_blocks")}
+    keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads", "checksum_split_blocks",
+                                          "checksum_split_adapt")}
     sd.set_tuning("checksum_cpu_max", 2147483647)  # the library default (the module sets 0)
+    sd.set_tuning("checksum_split_adapt", 0)  # always the split
     sd.set_tuning("checksum_hybrid_threads", slots)
     sd.set_tuning("checksum_split_blocks", 1)
     try:
@@ -615,6 +618,41 @@ def test_file_checksums_split_block_edges(ctx, tmp_path, oracle_native, slots):
     finally:
         for k, v in keep.items():
             sd.set_tuning(k, v)
+
+
+def test_file_checksums_learned_route(ctx, tmp_path, oracle_native):
+    """"checksum_split_adapt" k (round 5, default 8): a call the split applies to takes the
+    split or the CPU path alone by this context's recent GB/s of each -- each once, then the
+    faster, the other every k-th call.  With k = 2 over six calls both routes run, each
+    result equals the oracle's, and every call is counted on the route it took."""
+    import spacedrive_amd as sd
+    MiB = 1 << 20
+    sizes = [64 * MiB + 5 * i for i in range(9)]
+    paths = []
+    for i, L in enumerate(sizes):
+        p = tmp_path / f"r{i}"
+        with open(p, "wb") as f:
+            pos = 0
+            while pos < L:
+                k = min(32 * MiB, L - pos)
+                f.write(oracle_native.synth_bytes(9500 + i, 0, pos, k))
+                pos += k
+        paths.append(str(p))
+    want = [w.tobytes().hex() for w in oracle_native.file_checksums(paths, nthreads=NT)[0]]
+    keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_split_adapt")}
+    sd.set_tuning("checksum_cpu_max", 2147483647)  # the library default (the module sets 0)
+    sd.set_tuning("checksum_split_adapt", 2)
+    try:
+        before = sd.file_checksums_stats()
+        for _ in range(6):
+            assert sd.file_checksums(paths) == want
+        after = sd.file_checksums_stats()
+    finally:
+        for k, v in keep.items():
+            sd.set_tuning(k, v)
+    took_split, took_cpu = after["hybrid"] - before["hybrid"], after["cpu"] - before["cpu"]
+    assert took_split + took_cpu == 6 and after["gpu"] == before["gpu"]
+    assert took_split >= 2 and took_cpu >= 2, (took_split, took_cpu)  # k = 2: the loser every 2nd call
 
 
 def test_concurrent_callers_share_a_context(ctx, tmp_path):
@@ -672,8 +710,9 @@ def test_concurrent_split_checksum_calls(ctx, tmp_path, oracle_native):
             ps.append(str(p))
         paths.append(ps)
     want = [[w.tobytes().hex() for w in oracle_native.file_checksums(ps, nthreads=NT)[0]] for ps in paths]
-    keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads")}
+    keep = {k: sd.get_tuning(k) for k in ("checksum_cpu_max", "checksum_hybrid_threads", "checksum_split_adapt")}
     sd.set_tuning("checksum_cpu_max", 2147483647)  # the library default (the module sets 0)
+    sd.set_tuning("checksum_split_adapt", 0)  # always the split
     sd.set_tuning("checksum_hybrid_threads", 6)
     errors = []
     before = sd.file_checksums_stats()["hybrid"]
