@@ -1153,6 +1153,15 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
         routes0 = sd.file_checksums_stats()
         split_bytes = {"gpu": 0, "cpu_in_split": 0}
         per_call = []  # policy_default: the route each call took ("checksum_split_adapt") and its GB/s
+        # the policy's learning calls first: each route's uncounted warm-up call and one counted
+        # call (sd_host.h split_route_choose), so the timed rounds see the route it settled on
+        for _ in range(4):
+            r0 = sd.file_checksums_stats()
+            t0 = time.perf_counter()
+            assert legs["policy_default"]() == want
+            r1 = sd.file_checksums_stats()
+            per_call.append({"round": "learn", "route": "split" if r1["hybrid"] > r0["hybrid"] else
+                             ("cpu" if r1["cpu"] > r0["cpu"] else "gpu"), "GBps": total / (time.perf_counter() - t0) / 1e9})
         for rnd in range(4):  # round 0 warms the windows, the pools and the page cache
             for k, f in legs.items():
                 b0, r0 = sd.file_checksums_bytes(), sd.file_checksums_stats()
@@ -1184,9 +1193,9 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
         res["policy_default_over_cpu_path"] = res["policy_default"]["GBps"] / res["library_cpu_path"]["GBps"]
         res["note"] = ("medians of 3 interleaved rounds after a warm one; policy_default splits this call between "
                        "the GPU route (hybrid_threads GPU slots) and the CPU path, or runs the CPU path alone where "
-                       "this context measured it faster (split_adapt: each route once -- the warm call and the "
-                       "first round --, then the faster, the other every split_adapt-th call; per_call; DESIGN.md "
-                       "§4.1)")
+                       "this context measured it faster (split_adapt: after 4 learning calls -- each route's "
+                       "uncounted warm-up and one counted call --, the faster, the other every split_adapt-th "
+                       "call; per_call; DESIGN.md §4.1)")
         from oracle import native
         bad = sum(native.checksum_synth_mt(flen, 30_000 + i, 0, nthreads=oracle_threads()).hex() != want[i]
                   for i in range(nf))

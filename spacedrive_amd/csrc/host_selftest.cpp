@@ -908,8 +908,10 @@ void test_split_routes() {
         seen.push_back(r);
         return r;
     };
-    CHECK(call(120, 100, 8) == 0);  // first: the split
-    CHECK(call(120, 100, 8) == 1);  // then the CPU path once
+    CHECK(call(30, 100, 8) == 0);   // first: the split, a warm-up that is not counted
+    CHECK(call(120, 100, 8) == 0);  // the split again, counted
+    CHECK(call(10, 100, 8) == 1);   // then the CPU path, warm-up
+    CHECK(call(120, 100, 8) == 1);  // and counted: now both are known
     int split_calls = 0, cpu_calls = 0;
     for (int i = 0; i < 30; i++) (call(120, 100, 8) == 0 ? split_calls : cpu_calls)++;
     CHECK(split_calls >= 26 && cpu_calls >= 3);  // the faster, and the other every 8th call
@@ -920,8 +922,7 @@ void test_split_routes() {
     CHECK(cpu_after >= 13);
     // k = 0: no exploring once both are known
     SplitRoutes t;
-    split_route_record(t, 0, 50);
-    split_route_record(t, 1, 60);
+    for (int r : {0, 0, 1, 1}) split_route_record(t, r, r ? 60 : 50);  // each: a warm-up, then counted
     for (int i = 0; i < 20; i++) CHECK(split_route_choose(t, 0) == 1);
 }
 

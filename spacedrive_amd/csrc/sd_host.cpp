@@ -311,6 +311,7 @@ int split_route_choose(const SplitRoutes& s, uint32_t explore_every) {
 
 void split_route_record(SplitRoutes& s, int route, double gbps) {
     const int r = route ? 1 : 0;
+    if (s.seen[r]++ == 0) return;  // the route's first call: a warm-up, not counted
     s.rate[r] = s.n[r] ? 0.5 * s.rate[r] + 0.5 * gbps : gbps;
     s.n[r]++;
     s.calls++;

@@ -422,12 +422,15 @@ bool cpu_block_cv_fd(int fd, uint64_t file_len, uint64_t block, uint8_t cv[32]);
 // sd_file_checksums' route for a call the split applies to, learned per context (round 5:
 // the split lost 7 % to the CPU path alone on a host whose CPU path read and hashed 103 GB/s
 // from files, and won 34 % on one at 78).  rate[r] is the EWMA of GB/s of
-// route r's past calls (0 = the split, 1 = the CPU path alone), n[r] how many; each route
-// runs once, then the faster one, and every explore_every-th call the other (0 = never).
+// route r's past calls (0 = the split, 1 = the CPU path alone), n[r] how many were counted
+// -- a route's first call in the context is not (it pays for its pinned windows and pools:
+// a split's first call ran at 82 GB/s against 100+ after) -- and each route runs until one
+// call is counted, then the faster one, and every explore_every-th call the other (0 = never).
 struct SplitRoutes {
     double rate[2] = {0.0, 0.0};
     uint32_t n[2] = {0, 0};
-    uint64_t calls = 0;
+    uint32_t seen[2] = {0, 0};  // calls recorded per route, the uncounted first included
+    uint64_t calls = 0;         // counted calls
 };
 int split_route_choose(const SplitRoutes& s, uint32_t explore_every);
 void split_route_record(SplitRoutes& s, int route, double gbps);
