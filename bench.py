@@ -1187,6 +1187,7 @@ def file_checksums_leg(ctx, mib: int, with_cpu: bool, dev):
         res["policy_default"]["route"] = {k: routes1[k] - routes0[k] for k in routes1}
         res["policy_default"]["per_call"] = per_call
         res["policy_default"]["split_adapt"] = sd.get_tuning("checksum_split_adapt")
+        res["policy_default"]["learned"] = sd.file_checksums_learned()
         res["policy_default"]["hybrid_threads"] = sd.get_tuning("checksum_hybrid_threads")
         tot = split_bytes["gpu"] + split_bytes["cpu_in_split"]
         res["policy_default"]["gpu_share"] = split_bytes["gpu"] / tot if tot else None

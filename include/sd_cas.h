@@ -264,6 +264,10 @@ int sd_file_checksums_routes(sd_cas_ctx* ctx, uint64_t out[3]); /* [0] CPU path,
 /* bytes (stat lengths) of the files [0] the GPU route hashed (GPU-only and split calls) and
  * [1] the CPU path hashed inside split calls: the split's share on this host */
 int sd_file_checksums_bytes(sd_cas_ctx* ctx, uint64_t out[2]);
+/* what the context learned for the calls the split applies to ("checksum_split_adapt"):
+ * [0] the split's GB/s, [1] the CPU path's (EWMAs of counted calls), [2] / [3] how many
+ * calls each was counted for (each route's first call is a warm-up and not counted) */
+int sd_file_checksums_learned(sd_cas_ctx* ctx, double out[4]);
 int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char* out_hex65,
                       int32_t* status);
 

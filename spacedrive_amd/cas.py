@@ -167,6 +167,14 @@ def file_checksums_bytes(device: Optional[int] = None) -> dict:
     return {"gpu": int(v[0]), "cpu_in_split": int(v[1])}
 
 
+def file_checksums_learned(device: Optional[int] = None) -> dict:
+    """sd_file_checksums_learned: the GB/s the context learned for the split and for the CPU
+    path alone ("checksum_split_adapt"), and how many calls each was counted for."""
+    v = np.zeros(4, np.float64)
+    check(lib().sd_file_checksums_learned(default_context(device).handle, _ptr(v)))
+    return {"split_GBps": float(v[0]), "cpu_GBps": float(v[1]), "split_calls": int(v[2]), "cpu_calls": int(v[3])}
+
+
 def set_tuning(key: str, value: int) -> None:
     """sd_cas_set_tuning (process-wide knobs, include/sd_cas.h)."""
     check(lib().sd_cas_set_tuning(key.encode(), int(value)))

@@ -653,6 +653,9 @@ def test_file_checksums_learned_route(ctx, tmp_path, oracle_native):
     took_split, took_cpu = after["hybrid"] - before["hybrid"], after["cpu"] - before["cpu"]
     assert took_split + took_cpu == 6 and after["gpu"] == before["gpu"]
     assert took_split >= 2 and took_cpu >= 2, (took_split, took_cpu)  # k = 2: the loser every 2nd call
+    learned = sd.file_checksums_learned()  # each route counted once its warm-up call is past
+    assert learned["split_calls"] >= 1 and learned["cpu_calls"] >= 1, learned
+    assert learned["split_GBps"] > 0 and learned["cpu_GBps"] > 0, learned
 
 
 def test_concurrent_callers_share_a_context(ctx, tmp_path):
