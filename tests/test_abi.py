@@ -102,6 +102,9 @@ def test_stage_file_errors(tmp_path):
 def test_invalid_arguments_do_not_cross_boundary():
     rc = lib().sd_cas_stage_plan(None, 3, None, None)
     assert rc == -1 and b"null" in lib().sd_cas_last_error()
+    out = (ctypes.c_double * 4)()
+    rc = lib().sd_file_checksums_learned(None, out)  # no context: refused before any HIP call
+    assert rc == -1 and b"null" in lib().sd_cas_last_error()
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="GPU present")
