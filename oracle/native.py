@@ -176,12 +176,30 @@ def checksums_synth(sizes, cids, twins=None, nthreads: int = 1) -> np.ndarray:
     return out
 
 
-def stage_synth(sizes, cids, twins, offsets, total: int) -> np.ndarray:
-    """Host buffer holding the exact cas messages of synthetic files at `offsets`."""
+def stage_synth(sizes, cids, twins, offsets, total: int, nthreads: int = 1) -> np.ndarray:
+    """Host buffer holding the exact cas messages of synthetic files at `offsets`; with
+    nthreads > 1 the files are split into contiguous ranges written by that many threads
+    (each message lands at its own absolute offset, so the ranges never overlap)."""
     sizes = np.ascontiguousarray(sizes, np.uint64)
     cids = np.ascontiguousarray(cids, np.uint64)
     tw = None if twins is None else np.ascontiguousarray(twins, np.uint32)
     offsets = np.ascontiguousarray(offsets, np.uint64)
     buf = np.zeros(total + 64, np.uint8)
-    lib().sdo_stage_synth(_p(sizes), _p(cids), _p(tw), _p(offsets), len(sizes), _p(buf))
+    n = len(sizes)
+    nthreads = max(1, min(int(nthreads), n // 1024 or 1))
+    if nthreads == 1:
+        lib().sdo_stage_synth(_p(sizes), _p(cids), _p(tw), _p(offsets), n, _p(buf))
+        return buf
+    import threading
+    cuts = np.linspace(0, n, nthreads + 1).astype(np.int64)
+
+    def run(a, b):
+        lib().sdo_stage_synth(_p(sizes[a:b]), _p(cids[a:b]), None if tw is None else _p(tw[a:b]),
+                              _p(offsets[a:b]), b - a, _p(buf))
+
+    th = [threading.Thread(target=run, args=(int(cuts[i]), int(cuts[i + 1]))) for i in range(nthreads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
     return buf

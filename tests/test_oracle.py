@@ -357,3 +357,19 @@ def test_checksum_mt_over_memory_equals_simd(oracle_native):
         d = rng.integers(0, 256, n + 64, dtype=np.uint8)
         want = oracle_native.checksums_simd(d, [0], [n], nthreads=1)[0].tobytes()
         assert oracle_native.checksum_mt(d, n, nthreads=3) == want, n
+
+
+def test_stage_synth_threaded_equals_serial(oracle_native):
+    # the CPU baseline stages its shard with several threads: the bytes (and the prefix the
+    # legs hash) are the same as one thread's
+    from spacedrive_amd import synth
+    from spacedrive_amd.device import stage_plan
+    sizes, cids, twins = synth.library(3, 6000, 6000)
+    ext, total = stage_plan(sizes)
+    one = oracle_native.stage_synth(sizes, cids, twins, ext["msg_offset"], total)
+    many = oracle_native.stage_synth(sizes, cids, twins, ext["msg_offset"], total, nthreads=5)
+    assert np.array_equal(one, many)
+    e2, t2 = stage_plan(sizes[:2500])
+    assert np.array_equal(e2, ext[:2500])
+    part = oracle_native.stage_synth(sizes[:2500], cids[:2500], twins[:2500], e2["msg_offset"], t2)
+    assert np.array_equal(part[:t2], one[:t2])
