@@ -495,7 +495,8 @@ int sd_cas_get_tuning(const char* key, int* value);
 /* Read-only probe over d_buf[0, bytes) (bytes a multiple of 4096) for calibrating the
  * PMC byte counters on this kernel family's access patterns: pattern 0 = coalesced
  * 16 B/lane streaming, pattern 1 = one lane per 1 KiB chunk reading 4 x 16 B per 64-byte
- * block (the hashing kernels' pattern), pattern 2 = pattern 1 with 2 chunks per lane. */
+ * block (the hashing kernels' pattern), pattern 2 = pattern 1 with 2 chunks per lane,
+ * pattern 3 = pattern 0 with its loads marked non-temporal. */
 int sd_read_probe(sd_cas_ctx* ctx, const uint8_t* d_buf, uint64_t bytes, int pattern, void* stream);
 /* VALU ceiling of the kernels' BLAKE3 G instruction mix (asm, registers only, 8 waves per SIMD):
  * measured lane-ops/s on this device. */

@@ -7,7 +7,8 @@ are read before and after each workload loops for a few seconds, and the GPU met
 (per-XCD gfx clocks, socket power, hotspot / memory / VR temperatures, throttle status) is
 sampled every 50 ms while it runs.
 
-  idle, valu_peak (k_valu_peak), hbm_read (a coalesced 16 GiB read), sampled (CasBatch.run over
+  idle, valu_peak (k_valu_peak), hbm_read (a coalesced 16 GiB read; _nt: its loads marked
+  non-temporal, to compare the energy per byte), sampled (CasBatch.run over
   250 000 sampled files), checksum (ChecksumBatch.run over 4 x 1 GiB)
 
 python scripts/clock_limit_probe.py [seconds per mode=4] -> one JSON line"""
@@ -150,6 +151,7 @@ def main():
         "idle": lambda: time.sleep(0.005),
         "valu_peak": lambda: ctx.valu_peak(),
         "hbm_read": lambda: check(L.sd_read_probe(ctx.handle, d_rd.data_ptr(), d_rd.numel(), 0, s)),
+        "hbm_read_nt": lambda: check(L.sd_read_probe(ctx.handle, d_rd.data_ptr(), d_rd.numel(), 3, s)),
         "sampled": lambda: cas.run(d_st, d_hash),
         "checksum": lambda: ck.run(d_ck, d_ckh),
     }
@@ -184,7 +186,9 @@ def main():
                 xs = [y for y in flat_nums(x) if isinstance(y, (int, float))]
                 if xs:
                     frac[k] = round(max(xs) / n_acc, 4)
+        moved = {"hbm_read": d_rd.numel(), "hbm_read_nt": d_rd.numel(), "sampled": total, "checksum": 4 * GiB}.get(name)
         res["modes"][name] = {"launches": launches, "s_per_launch": dt / launches, "metrics": summarize(rows),
+                              "TBps": moved / (dt / launches) / 1e12 if moved else None,
                               "violation_delta": d, "violation_frac_of_samples": frac}
         print(name, json.dumps(res["modes"][name]["metrics"]), json.dumps(frac), file=sys.stderr, flush=True)
     amdsmi.amdsmi_shut_down()

@@ -151,6 +151,12 @@ __global__ __launch_bounds__(256) void k_read_probe(const uint8_t* __restrict__ 
             const uint4 v = b[i];
             acc ^= v.x ^ v.y ^ v.z ^ v.w;
         }
+    } else if (pattern == 3) {  // the same coalesced read, loads marked non-temporal (power per byte)
+        for (uint64_t i = tid; i < bytes / 16; i += nthreads) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b) + i);
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
     } else {
         const uint32_t per = pattern == 2 ? 2048u : 1024u;  // bytes per lane
         for (uint64_t lane = tid; lane < bytes / per; lane += nthreads) {
