@@ -539,6 +539,12 @@ void test_cpu_budget() {
     CHECK(cpu_budget_resolve(16, 256, 64.0, 8).budget == 8);   // the shared quota still splits
     CHECK(cpu_budget_resolve(256, 256, 0.0, 8).budget == 32);  // unbound, no quota: the node's CPUs split
     CHECK(cpu_budget_resolve(16, 8, 0.0, 1).online == 16);     // online never below the mask
+    // a container pinned to a 16-CPU cpuset with no quota (docker --cpuset-cpus, k8s without
+    // limits) on a 256-CPU host: the scope passed is the cpuset, so 8 ranks split it
+    CHECK(cpu_budget_resolve(16, 16, 0.0, 8).budget == 2);
+    CHECK(cpu_budget_resolve(2, 16, 0.0, 8).budget == 2);      // ranks bound inside the cpuset
+    CHECK(cpulist_count("0-15\n") == 16 && cpulist_count("0-3,8,10-11") == 7 && cpulist_count("5") == 1);
+    CHECK(cpulist_count("") == 0 && cpulist_count("3-1") == 0 && cpulist_count("a") == 0);
     // the cgroup readers, on fake cgroup trees
     const std::string v2 = g_dir + "/cg2", v1 = g_dir + "/cg1", v1c = v1 + "/cpu", none = g_dir + "/cg0";
     CHECK(mkdir(v2.c_str(), 0700) == 0 && mkdir(v1.c_str(), 0700) == 0 && mkdir(v1c.c_str(), 0700) == 0 &&
@@ -587,6 +593,24 @@ void test_cpu_budget() {
     put(pc, "12:memory:/slice\n");  // no cpu controller line: the root only (unlimited)
     CHECK(cgroup_cpu_quota_self(v1.c_str(), pc.c_str()) == 0.0);
     CHECK(cgroup_cpu_quota_self(none.c_str(), (g_dir + "/no_such_file").c_str()) == 0.0);
+    // cpusets: v2 the process's own cgroup, else the mount root; v1 the cpuset hierarchy
+    put(v2 + "/cpuset.cpus.effective", "0-255\n");
+    put(abc + "/cpuset.cpus.effective", "16-31\n");
+    put(pc, "0::/a/b/c\n");
+    CHECK(cgroup_cpuset_count(v2.c_str(), pc.c_str()) == 16);
+    put(pc, "0::/\n");
+    CHECK(cgroup_cpuset_count(v2.c_str(), pc.c_str()) == 256);
+    const std::string v1s = v1 + "/cpuset", v1sd = v1s + "/pod";
+    CHECK(mkdir(v1s.c_str(), 0700) == 0 && mkdir(v1sd.c_str(), 0700) == 0);
+    put(v1sd + "/cpuset.cpus", "0-7,64-71\n");
+    put(pc, "7:cpuset:/pod\n12:cpuacct,cpu:/slice\n");
+    CHECK(cgroup_cpuset_count(v1.c_str(), pc.c_str()) == 16);
+    CHECK(cgroup_cpuset_count(none.c_str(), (g_dir + "/no_such_file").c_str()) == 0);
+    unlink((v1sd + "/cpuset.cpus").c_str());
+    rmdir(v1sd.c_str());
+    rmdir(v1s.c_str());
+    unlink((v2 + "/cpuset.cpus.effective").c_str());
+    unlink((abc + "/cpuset.cpus.effective").c_str());
     for (const std::string& d : {abc, ab, a}) {
         unlink((d + "/cpu.max").c_str());
         rmdir(d.c_str());
@@ -784,6 +808,52 @@ void test_private_fd_tables() {
     close(p[0]);
 }
 
+// The HIP-thread rule, enforced: a submission step guarded the way
+// HIP_CHECK guards every HIP call (sd_api_impl.h) fails with SD_ERR_INTERNAL and a message
+// on a private-fd-table worker, and passes on a shared-table pool's workers and the caller.
+namespace {
+int submit_window_probe() {
+    SD_GUARD_BEGIN
+    hip_thread_check("hipMemcpyAsync(window)");
+    return SD_OK;
+    SD_GUARD_END
+}
+}  // namespace
+
+void test_hip_thread_rule() {
+    CHECK(!on_private_fd_table() && submit_window_probe() == SD_OK);
+    for (bool priv : {true, false}) {
+        StagePool pool(4, priv);
+        std::atomic<int> refused{0}, ok{0}, worker_tasks{0};
+        std::mutex mu;
+        std::string msg;
+        const std::thread::id caller = std::this_thread::get_id();
+        pool.run(64, [&](size_t) {
+            std::this_thread::sleep_for(std::chrono::microseconds(200));  // every worker gets tasks
+            if (std::this_thread::get_id() == caller) {  // the caller keeps its shared table
+                if (submit_window_probe() == SD_OK) ok++;
+                return;
+            }
+            worker_tasks++;
+            const int rc = submit_window_probe();
+            if (rc == SD_ERR_INTERNAL) {
+                refused++;
+                std::lock_guard<std::mutex> g(mu);
+                msg = sd_cas_last_error();
+            } else if (rc == SD_OK) {
+                ok++;
+            }
+        });
+        if (priv) {
+            CHECK(refused.load() == worker_tasks.load() && refused.load() > 0);
+            CHECK(msg.find("private-fd-table") != std::string::npos && msg.find("hipMemcpyAsync") != std::string::npos);
+        } else {
+            CHECK(refused.load() == 0 && ok.load() == 64);
+        }
+    }
+    CHECK(!on_private_fd_table() && submit_window_probe() == SD_OK);
+}
+
 // ------------------------------------------------------------------ in-process communicator
 // sd_comm_group's barrier and slots, as sd_cas_dedup_mgpu uses them: publish, barrier,
 // read every peer's slot, barrier -- each rank must see exactly this round's values; and a
@@ -924,6 +994,27 @@ void test_split_routes() {
     SplitRoutes t;
     for (int r : {0, 0, 1, 1}) split_route_record(t, r, r ? 60 : 50);  // each: a warm-up, then counted
     for (int i = 0; i < 20; i++) CHECK(split_route_choose(t, 0) == 1);
+    // seeded with the split slower than the CPU path, after the warm-ups: every call but the
+    // explore ones (calls % k == k - 1) takes the CPU path, and those take the split
+    SplitRoutes u;
+    for (int r : {0, 0, 1, 1}) split_route_record(u, r, r ? 110 : 80);
+    for (int i = 0; i < 40; i++) {
+        const bool explore = u.calls % 8 == 7;
+        const int r = split_route_choose(u, 8);
+        CHECK(r == (explore ? 0 : 1));
+        split_route_record(u, r, r ? 110 : 80);
+    }
+    // a change of a key the rates depend on moves the generation; an unchanged value does not
+    int keep = 0;
+    CHECK(sd_cas_get_tuning("checksum_hybrid_threads", &keep) == SD_OK);
+    const uint64_t g0 = split_route_tuning_gen();
+    CHECK(sd_cas_set_tuning("checksum_hybrid_threads", keep) == SD_OK && split_route_tuning_gen() == g0);
+    CHECK(sd_cas_set_tuning("checksum_hybrid_threads", keep + 1) == SD_OK && split_route_tuning_gen() == g0 + 1);
+    CHECK(sd_cas_set_tuning("coalesce_window_us", 200) == SD_OK && split_route_tuning_gen() == g0 + 1);
+    CHECK(sd_cas_set_tuning("checksum_hybrid_threads", keep) == SD_OK && split_route_tuning_gen() == g0 + 2);
+    // the co-hash cap scales with the budget
+    CHECK(checksum_cohash_cap(16) == 13 && checksum_cohash_cap(8) == 6 && checksum_cohash_cap(4) == 3);
+    CHECK(checksum_cohash_cap(2) == 1 && checksum_cohash_cap(1) == 0 && checksum_cohash_cap(32) == 26);
 }
 
 int main() {
@@ -946,6 +1037,7 @@ int main() {
     test_split_routes();
     test_comm_group();
     test_private_fd_tables();
+    test_hip_thread_rule();
     test_numa_placement();  // last: it moves the pools' threads
     // clean up the scratch directory
     if (DIR* d = opendir(g_dir.c_str())) {

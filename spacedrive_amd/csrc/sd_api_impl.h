@@ -17,6 +17,7 @@
 
 #define HIP_CHECK(expr)                                                                              \
     do {                                                                                             \
+        hip_thread_check(#expr); /* never on a private-fd-table thread (sd_host.h) */                \
         hipError_t e_ = (expr);                                                                      \
         if (e_ != hipSuccess)                                                                        \
             throw sd_failure(e_ == hipErrorOutOfMemory ? SD_ERR_NOMEM : SD_ERR_DEVICE,              \
@@ -191,6 +192,7 @@ struct Slot {
     hipStream_t stream = nullptr;
     DevBuf staged, hashes;
     PinnedBuf host_hashes, window;
+    Tables aux;  // a call's own tables (the split checksum's block map), grown with the slot
     sd_cas_batch cas;
     sd_checksum_batch ck;
     hipEvent_t drained = nullptr;  // sync()'s blocking-sync event
@@ -229,6 +231,7 @@ struct sd_cas_ctx {
     std::atomic<uint64_t> checksums_gpu_bytes{0}, checksums_host_bytes{0};  // sd_checksums: who hashed
     std::mutex split_mu;
     SplitRoutes split_routes;  // sd_file_checksums: the split or the CPU path, learned (sd_host.h)
+    uint64_t split_routes_gen = 0;  // split_route_tuning_gen() the rates were learned under
     std::mutex pool_mu;
     // Reader threads.  stage_pool: tasks that open and close their own files (the cas
     // stager, checksum packs), on private fd tables (stage_pool.h); io_pool: parallel preads

@@ -767,15 +767,6 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
     std::vector<sd_u32x2> map(nb_total);
     for (size_t q = 0; q < nf; q++)
         for (uint64_t b = fb[q]; b < fb[q + 1]; b++) map[b] = sd_u32x2{(uint32_t)q, (uint32_t)(b - fb[q])};
-    Tables tab;
-    tab.begin();
-    const size_t o_files = tab.add(files), o_map = tab.add(map);
-    tab.upload(nullptr);
-    DevBuf d_cv;
-    d_cv.ensure(nb_total * 32);
-    PinnedBuf h_cv;  // every block's CV, from either side
-    h_cv.ensure(nb_total * 32);
-
     struct GpuSlot {
         std::unique_ptr<Slot> s;
         hipEvent_t copied = nullptr;
@@ -801,6 +792,17 @@ void split_checksums_blocks(sd_cas_ctx* ctx, const char* const* paths, char* out
         }
     } sl{ctx, std::vector<GpuSlot>(std::max(1, gpu_slots)), nullptr};
     sl.cp = ctx->acquire();
+    // the call's tables and CV tables live on its copy slot, grow-only in the context's slot
+    // pool: no per-call hipMalloc/hipHostMalloc, and no hipFree/hipHostFree (each of which
+    // synchronises the device and stalled concurrent calls)
+    Tables& tab = sl.cp->aux;
+    tab.begin();
+    const size_t o_files = tab.add(files), o_map = tab.add(map);
+    tab.upload(nullptr);
+    DevBuf& d_cv = sl.cp->hashes;
+    d_cv.ensure(nb_total * 32);
+    PinnedBuf& h_cv = sl.cp->host_hashes;  // every block's CV, from either side
+    h_cv.ensure(nb_total * 32);
     for (auto& x : sl.g) {
         x.s = ctx->acquire();
         x.s->window.ensure(GPU_RUN * SD_CK_BLOCK + 128);
@@ -997,6 +999,9 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
     const int hyb = threads >= 16 ? hyb_knob : std::min(hyb_knob, std::max(1, hyb_knob * threads / 16));
     std::vector<uint64_t> hint;
     std::vector<uint8_t> regular;
+    // the learned route compares whole calls: from here, so the split's stat pass counts
+    // against it as the CPU path's own stat pass does against that route
+    const auto t0 = std::chrono::steady_clock::now();
     if (cpu_max != 0 && hyb > 0 && hyb < threads && n >= 2) {
         constexpr uint64_t BIG_FILE = 8ull << 20, BIG_TOTAL = 512ull << 20;
         stat_files(*ctx->stage_pool(threads), paths, n, hint, regular, threads);
@@ -1018,11 +1023,16 @@ int sd_file_checksums(sd_cas_ctx* ctx, const char* const* paths, size_t n, char*
             int route = 0;
             if (adapt) {
                 std::lock_guard<std::mutex> g(ctx->split_mu);
+                // what either route's rate depends on: a change of it starts the learning again
+                const uint64_t gen = split_route_tuning_gen();
+                if (ctx->split_routes_gen != gen) {
+                    ctx->split_routes = SplitRoutes{};
+                    ctx->split_routes_gen = gen;
+                }
                 route = split_route_choose(ctx->split_routes, (uint32_t)adapt);
             }
             uint64_t call_bytes = 0;
             for (size_t q = 0; q < n; q++) call_bytes += hint[q];
-            const auto t0 = std::chrono::steady_clock::now();
             auto learn = [&](int r) {
                 if (!adapt) return;
                 const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -1223,14 +1233,17 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     // there the GPU loop claims its 1 MiB blocks a window at a time from the front, the
     // host thread 64 blocks at a time from the back into a host CV table; when none is
     // left, the GPU loop uploads the host's CVs next to its own and runs the reduce passes.
-    // Never more host threads than the process's host budget less three: this thread, and
-    // two CPUs of headroom.  Measured on the box (16-CPU quota, 4 x 1 GiB, interleaved
+    // Never more host threads than the process's host budget less 3/16 of it (at least one:
+    // this thread), i.e. 13 of 16.  Measured on the box (16-CPU quota, 4 x 1 GiB, interleaved
     // rounds; scripts/cohash_checksum_probe.py, profiles/r5/r5g_cohash_checksum.json and
     // r5h_cohash_ck.json): 13 co-hashing threads 138-151 GB/s, 14: 136-148, 15: 123-129 --
     // at 15 the process burns 16.5 CPUs of time per call for fewer bytes (no throttled
-    // periods: the contention is the cores', not the quota's).  sd_cas_ids keeps budget - 1:
-    // there 15 measured best (4.86 vs 4.51 M files/s at 13, r5h_cohash_cas.json).
-    const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS), host_cpu_budget() - 3}));
+    // periods: the contention is the cores', not the quota's).  The headroom scales with the
+    // budget (an absolute 3 left one thread of a 4-CPU budget): 8 -> 6, 4 -> 3,
+    // 2 -> 1 (cohash_headroom, sd_host.h).  sd_cas_ids keeps budget - 1: there 15 measured
+    // best (4.86 vs 4.51 M files/s at 13, r5h_cohash_cas.json).
+    const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS),
+                                             checksum_cohash_cap(host_cpu_budget())}));
     uint64_t all_bytes = 0;
     for (size_t q = 0; q < n; q++) all_bytes += lens[q];
     std::mutex claim_mu;

@@ -172,13 +172,75 @@ double cgroup_cpu_quota_self(const char* root, const char* proc_cgroup) {
     return q;
 }
 
+int cpulist_count(const char* list) {
+    int n = 0;
+    const char* p = list;
+    while (*p && *p != '\n') {
+        char* e = nullptr;
+        const long a = strtol(p, &e, 10);
+        if (e == p || a < 0) return 0;
+        long b = a;
+        p = e;
+        if (*p == '-') {
+            b = strtol(p + 1, &e, 10);
+            if (e == p + 1 || b < a) return 0;
+            p = e;
+        }
+        n += (int)(b - a + 1);
+        if (*p == ',') p++;
+        else if (*p && *p != '\n') return 0;
+    }
+    return n;
+}
+
+int cgroup_cpuset_count(const char* root, const char* proc_cgroup) {
+    const std::string mnt = root ? root : "/sys/fs/cgroup";
+    std::string v2path, v1path;
+    bool have_v2 = false, have_v1 = false;
+    if (FILE* f = fopen(proc_cgroup ? proc_cgroup : "/proc/self/cgroup", "re")) {
+        char line[4096];
+        while (fgets(line, sizeof line, f)) {
+            line[strcspn(line, "\n")] = 0;
+            char* c1 = strchr(line, ':');
+            char* c2 = c1 ? strchr(c1 + 1, ':') : nullptr;
+            if (!c2) continue;
+            const std::string ctrl(c1 + 1, c2);
+            if (strncmp(line, "0:", 2) == 0 && ctrl.empty()) {
+                v2path = c2 + 1;
+                have_v2 = true;
+            } else if (("," + ctrl + ",").find(",cpuset,") != std::string::npos) {
+                v1path = c2 + 1;
+                have_v1 = true;
+            }
+        }
+        fclose(f);
+    }
+    char buf[4096];
+    auto count = [&](const std::string& file) { return read_small(file, buf, sizeof buf) ? cpulist_count(buf) : 0; };
+    if (have_v1) {
+        const std::string d = mnt + "/cpuset" + (v1path == "/" ? std::string() : v1path);
+        int n = count(d + "/cpuset.effective_cpus");
+        if (!n) n = count(d + "/cpuset.cpus");
+        if (n) return n;
+    }
+    if (have_v2 && v2path != "/") {
+        const int n = count(mnt + v2path + "/cpuset.cpus.effective");
+        if (n) return n;
+    }
+    return count(mnt + "/cpuset.cpus.effective");
+}
+
 CpuBudget host_cpu_budget_detail() {
     static const CpuBudget resolved = [] {
         int affinity = 1;
         cpu_set_t set;
         CPU_ZERO(&set);
         if (sched_getaffinity(0, sizeof set, &set) == 0) affinity = CPU_COUNT(&set);
-        const long online = sysconf(_SC_NPROCESSORS_ONLN);
+        long online = sysconf(_SC_NPROCESSORS_ONLN);
+        // a container's cpuset narrower than the machine is the scope the mask is compared
+        // with: a mask of all of it is the node's shared set, split over the ranks
+        const int cpuset = cgroup_cpuset_count(nullptr, nullptr);
+        if (cpuset > 0 && (online <= 0 || cpuset < online)) online = cpuset;
         int world = 1;
         if (const char* w = getenv("LOCAL_WORLD_SIZE")) world = std::max(1, atoi(w));
         return cpu_budget_resolve(affinity, online > 0 ? (int)online : affinity, cgroup_cpu_quota_self(nullptr, nullptr),
@@ -300,6 +362,12 @@ void sd_set_err(const char* fmt, ...) {
     va_end(ap);
     g_err = buf;
 }
+
+namespace {
+std::atomic<uint64_t> g_split_gen{1};
+}  // namespace
+
+uint64_t split_route_tuning_gen() { return g_split_gen.load(std::memory_order_relaxed); }
 
 int split_route_choose(const SplitRoutes& s, uint32_t explore_every) {
     if (s.n[0] == 0) return 0;  // each route once
@@ -425,8 +493,16 @@ int sd_cas_set_tuning(const char* key, int value) {
     if (!key) throw sd_failure(SD_ERR_INVALID, "null key");
     for (int k = 0; k < SD_TUNE_NKEYS; k++)
         if (strcmp(key, TUNE_NAMES[k]) == 0) {
-            g_tune[k].store(value, std::memory_order_relaxed);
+            const int was = g_tune[k].exchange(value, std::memory_order_relaxed);
             if (k == SD_TUNE_NUMA_PIN) g_numa_gen.fetch_add(1);  // threads re-place at their next run
+            switch (k) {  // keys the split / CPU-path rates depend on (split_route_tuning_gen)
+                case SD_TUNE_READ_THREADS: case SD_TUNE_CHECKSUM_HYBRID_THREADS: case SD_TUNE_HOST_CPU_BUDGET:
+                case SD_TUNE_CHECKSUM_SPLIT_BLOCKS: case SD_TUNE_CPU_READ_PIECE_KIB:
+                case SD_TUNE_CHECKSUM_STAGE_HOT: case SD_TUNE_NUMA_PIN:
+                    if (was != value) g_split_gen.fetch_add(1, std::memory_order_relaxed);
+                    break;
+                default: break;
+            }
             return SD_OK;
         }
     throw sd_failure(SD_ERR_INVALID, std::string("unknown tuning key ") + key);
@@ -623,7 +699,22 @@ void plan_checksum(CkPlan& p, const uint64_t* offsets, const uint64_t* lens, siz
 }
 
 // ------------------------------------------------------------------ file reading
+namespace {
+// set when this thread took (or, where unshare is refused or under TSan, was meant to take)
+// a private fd table: the rule is about the thread's role, so it holds in every build
+thread_local bool t_private_fds = false;
+}  // namespace
+
+bool on_private_fd_table() { return t_private_fds; }
+
+void hip_thread_check(const char* what) {
+    if (t_private_fds)
+        throw sd_failure(SD_ERR_INTERNAL, std::string("HIP call on a private-fd-table worker thread (its device "
+                                                      "descriptors are closed): ") + what);
+}
+
 void private_fd_table() {
+    t_private_fds = true;
 #if defined(__SANITIZE_THREAD__)
     // ThreadSanitizer tracks descriptors by number across threads: fd 3 of two private
     // tables would read as one descriptor raced on.  The TSan build keeps the shared table.

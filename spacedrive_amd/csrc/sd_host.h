@@ -7,6 +7,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <memory>
@@ -24,6 +25,13 @@ struct sd_failure : std::runtime_error {
     sd_failure(int r, const std::string& m) : std::runtime_error(m), rc(r) {}
 };
 void sd_set_err(const char* fmt, ...);
+
+// The HIP-thread rule: a thread that ran private_fd_table() has closed its
+// copies of the HIP runtime's device descriptors, so a HIP call from it faults the process
+// (round 5's first block split did exactly that).  Every HIP_CHECK (sd_api_impl.h) asks
+// this first and throws SD_ERR_INTERNAL with `what` named instead of calling HIP there.
+bool on_private_fd_table();
+void hip_thread_check(const char* what);
 
 // every extern "C" entry point: no C++ exception crosses the ABI (the reference FFI fences
 // panics with catch_unwind, apps/mobile/modules/sd-core/ios/crate/src/lib.rs:41,60)
@@ -89,7 +97,7 @@ int tuning_get(int key);
 struct CpuBudget {
     int budget = 1;       // the cap
     int affinity = 1;     // CPUs in sched_getaffinity
-    int online = 1;       // CPUs online on the machine
+    int online = 1;       // CPUs the process's container may use: online, or its cpuset when smaller
     int quota_milli = 0;  // cgroup CPU quota in milli-CPUs (0 = no limit)
     int local_world = 1;  // ranks per node sharing the host
     int overridden = 0;   // 1 when "host_cpu_budget" set the cap
@@ -103,6 +111,13 @@ double cgroup_cpu_quota(const char* root);
 // (read from `proc_cgroup`, default /proc/self/cgroup) up to it; `root` defaults to
 // /sys/fs/cgroup.  0 when none is set
 double cgroup_cpu_quota_self(const char* root, const char* proc_cgroup);
+// CPUs in the process's cgroup cpuset (v2 cpuset.cpus.effective of its own cgroup, else the
+// mount root's; v1 cpuset/<path>/cpuset.effective_cpus or cpuset.cpus), 0 when unreadable:
+// a container pinned with --cpuset-cpus and no quota shows the host's CPUs online, and an
+// affinity mask of the whole cpuset is then shared by the node's ranks, not one rank's binding
+int cgroup_cpuset_count(const char* root, const char* proc_cgroup);
+// CPUs in a cpuset list ("0-15,32,40-47"); 0 when malformed
+int cpulist_count(const char* list);
 CpuBudget host_cpu_budget_detail();  // resolved once per process, then the override applied
 int host_cpu_budget();
 inline int cap_host_threads(int n) {
@@ -434,4 +449,12 @@ struct SplitRoutes {
 };
 int split_route_choose(const SplitRoutes& s, uint32_t explore_every);
 void split_route_record(SplitRoutes& s, int route, double gbps);
+// bumped by sd_cas_set_tuning when a key either route's rate depends on changes value
+// (read_threads, checksum_hybrid_threads, host_cpu_budget, checksum_split_blocks,
+// cpu_read_piece_kib, checksum_stage_hot, numa_pin): a context's learned rates from before
+// are dropped at its next split-eligible call
+uint64_t split_route_tuning_gen();
+// co-hashing threads of a sd_checksums call under a host budget of b: b less 3/16 of it, at
+// least one less (16 -> 13, 8 -> 6, 4 -> 3, 2 -> 1, 1 -> 0)
+inline int checksum_cohash_cap(int b) { return b <= 1 ? 0 : b - std::max(1, (3 * b + 8) / 16); }
 void hex_lower(const uint8_t* h, int nbytes, char* out);

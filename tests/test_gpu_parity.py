@@ -550,7 +550,7 @@ def test_file_checksums_packing_and_streaming(ctx, tmp_path):
 
 @pytest.mark.parametrize("mode,budget", [("blocks", 0), ("blocks", 3), ("files", 0)])
 def test_file_checksums_hybrid_split(ctx, tmp_path, mode, budget):
-    """sd_file_checksums' split policy ("checksum_hybrid_threads", default 4): a call whose regular
+    """sd_file_checksums' split policy ("checksum_hybrid_threads", default 6): a call whose regular
     files of >= 8 MiB total >= 512 MiB runs the GPU route and the CPU path at once -- by
     blocks (round 5's default: the GPU's slots take runs of 1 MiB blocks while free, the host
     threads single blocks, roots merged from both sides' CVs) or by whole files (round 4,
@@ -590,7 +590,7 @@ def test_file_checksums_hybrid_split(ctx, tmp_path, mode, budget):
                                           "host_cpu_budget", "checksum_split_adapt")}
     sd.set_tuning("checksum_cpu_max", 2147483647)  # the library default (the module sets 0)
     sd.set_tuning("checksum_split_adapt", 0)  # always the split (the learned route has its own test)
-    sd.set_tuning("checksum_hybrid_threads", 4)  # the library default
+    sd.set_tuning("checksum_hybrid_threads", 6)  # the library default
     sd.set_tuning("checksum_split_blocks", 1 if mode == "blocks" else 0)
     sd.set_tuning("host_cpu_budget", budget)
     by0 = np.zeros(2, np.uint64)
