@@ -75,6 +75,7 @@ namespace {
 
 #define HIP_OK(expr)                                                                                    \
     do {                                                                                                \
+        hip_thread_check(#expr); /* the HIP-thread rule (sd_host.h) */                                  \
         hipError_t e_ = (expr);                                                                         \
         if (e_ != hipSuccess)                                                                           \
             throw sd_failure(e_ == hipErrorOutOfMemory ? SD_ERR_NOMEM : SD_ERR_DEVICE,                 \
@@ -83,6 +84,7 @@ namespace {
 
 #define NCCL_OK(expr)                                                                                   \
     do {                                                                                                \
+        hip_thread_check(#expr);                                                                        \
         ncclResult_t r_ = (expr);                                                                       \
         if (r_ != ncclSuccess) throw sd_failure(SD_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
     } while (0)
