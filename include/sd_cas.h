@@ -65,7 +65,8 @@ typedef enum sd_rc {
     SD_ERR_INVALID = -1,  /* bad argument (null pointer, misaligned extent, ...) */
     SD_ERR_DEVICE = -2,   /* HIP / device error, or no gfx950 device */
     SD_ERR_NOMEM = -3,    /* device or pinned-host allocation failed */
-    SD_ERR_INTERNAL = -4, /* unexpected exception caught at the boundary */
+    SD_ERR_INTERNAL = -4, /* unexpected exception caught at the boundary, or a HIP call
+                             attempted on a private-fd-table worker thread */
     SD_ERR_COMM = -5,     /* collective (RCCL) failure */
     SD_ERR_CAPACITY = -6  /* sd_cas_dedup_mgpu: some rank's output capacity is too small (every
                              rank returns it, before the exchange; *m_out = own requirement) */
@@ -106,7 +107,8 @@ int sd_cas_abi_version(void);
  * process starts -- readers, CPU-path workers and co-hashing threads alike.  Resolved once
  * as min(affinity share, quota share), at least 1: the CPUs in the affinity mask, divided by
  * LOCAL_WORLD_SIZE (the ranks sharing the node's host; 1 when unset) only when the mask holds
- * every online CPU (a narrower mask is a per-rank binding); and the tightest cgroup CPU quota
+ * every CPU of its scope -- the online CPUs, or the cgroup cpuset when that is smaller (a
+ * narrower mask is a per-rank binding); and the tightest cgroup CPU quota
  * from the process's cgroup up, rounded up, divided by LOCAL_WORLD_SIZE.  The tuning key
  * "host_cpu_budget" > 0 replaces it.  out[5]: [0] the budget, [1] affinity CPUs, [2] cgroup
  * quota in milli-CPUs (0 = none), [3] LOCAL_WORLD_SIZE, [4] 1 if the tuning key set it. */
@@ -486,8 +488,8 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * the other every k-th call to keep its rate current; 0 = always the split;
  * "host_cohash_threads" (15): host threads hashing beside the GPU in sd_cas_ids calls of
  * >= 8192 files and sd_checksums calls of >= 1 GiB (0 = the GPU alone; never more than the
- * host budget less one in sd_cas_ids, less three in sd_checksums -- 13 of 16 measured best
- * there); "host_cpu_budget" (0 = resolved, see sd_host_cpu_budget): the cap
+ * host budget less one in sd_cas_ids, less 3/16 of it (at least one) in sd_checksums -- 13
+ * of 16 measured best there); "host_cpu_budget" (0 = resolved, see sd_host_cpu_budget): the cap
  * on every call's host threads -- thread counts callers pass (nthreads) and the knobs above
  * are clamped to it.  Unknown keys fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);
