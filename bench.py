@@ -445,7 +445,7 @@ def cpu_baseline(sizes, cids, twins, seconds: float):
     nN, dtN, bN = rate(nA, 100000)
     simd = {0: "scalar", 1: "AVX2 8-way", 2: "AVX-512 16-way"}[level]
     return {
-        "value": nT / dtT, "unit": "files/s", "cores": threads, "kind": "port",
+        "value": nT / dtT, "unit": "files/s", "cores": threads, "kind": "port", "sample_files": nT,
         "sample": f"first {nT} files of this shard (same mixture), messages pre-staged in host RAM, hash only; "
                   f"C restatement of cas.rs + blake3 with {simd} multi-chunk hash_many (oracle/sd_oracle_simd.c) "
                   f"on {threads} threads; {bT / dtT / 1e9:.2f} GB/s of message bytes",
@@ -1553,7 +1553,8 @@ def compact_line(out: dict, full_path: str = None) -> dict:
                              "ratio": v.get("ratio"), "host_share": v.get("host_share", v.get("host_share_of_hashing"))})
         c["cpu_baseline"] = _prune({
             "value": cb.get("value"), "unit": cb.get("unit"), "cores": cb.get("cores"), "kind": cb.get("kind"),
-            "sample": "first 1.25M files of the shard, messages in host RAM, hash only",
+            "sample": (f"first {cb['sample_files']} files of the shard" if cb.get("sample_files") else
+                       "a prefix of the shard") + ", messages in host RAM, hash only (oracle AVX-512 hash_many)",
             "single_thread": _g(cb, "single_thread", "value"), "all_cores": _g(cb, "all_cores", "value"),
             "all_cores_threads": _g(cb, "all_cores", "cores"), "simd": cb.get("simd"),
             "host_cpu": _g(cb, "host_cpu", "model"), "cgroup_cpu_quota": _g(cb, "host_cpu", "cgroup_cpu_quota"),
