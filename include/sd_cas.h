@@ -375,7 +375,12 @@ int sd_comm_create_local(sd_cas_ctx* ctx, sd_comm_group* group, int rank, sd_com
  * SD_ERR_CAPACITY before the record exchange, with *m_out = its own requirement (and
  * SD_ERR_INTERNAL together if any rank's partition counts disagree with its valid records:
  * the gathered rows carry both, so no rank is left waiting in the exchange).  Runs on
- * `stream`; returns after the group counts are known (host sync).  Overlapping it with the
+ * `stream`; returns after the group counts are known (host sync).  Over RCCL, each wait for
+ * the peers is bounded by the tuning key "comm_timeout_ms" (300 000; 0 = unbounded): a peer
+ * that died or hung, or an RCCL asynchronous error, makes the call return SD_ERR_COMM naming
+ * the step, and the communicator is broken from then on -- later calls on it return
+ * SD_ERR_COMM, and sd_comm_destroy releases nothing of it (work may still be queued against
+ * it; the host is expected to exit).  Overlapping it with the
  * next batch's hashing (a second stream) pays only with the hashing stream at the higher
  * priority (107.5 vs 103.9-104.3 M files/s with equal priorities). */
 int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, const uint8_t* d_valid, uint64_t n,
@@ -491,7 +496,8 @@ int sd_checksum_batch_time(sd_cas_ctx* ctx, const sd_checksum_batch* batch, cons
  * host budget less one in sd_cas_ids, less 3/16 of it (at least one) in sd_checksums -- 13
  * of 16 measured best there); "host_cpu_budget" (0 = resolved, see sd_host_cpu_budget): the cap
  * on every call's host threads -- thread counts callers pass (nthreads) and the knobs above
- * are clamped to it.  Unknown keys fail with SD_ERR_INVALID. */
+ * are clamped to it; "comm_timeout_ms" (300000): the longest sd_cas_dedup_mgpu waits for its
+ * RCCL peers (0 = no bound).  Unknown keys fail with SD_ERR_INVALID. */
 int sd_cas_set_tuning(const char* key, int value);
 int sd_cas_get_tuning(const char* key, int* value);
 /* Read-only probe over d_buf[0, bytes) (bytes a multiple of 4096) for calibrating the

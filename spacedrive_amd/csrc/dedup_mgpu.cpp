@@ -34,9 +34,11 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sd_internal.h"
@@ -56,7 +58,20 @@ struct sd_comm {
     bool timing = false;
     bool timed = false;  // the last call recorded all of ev[]
     hipEvent_t ev[SD_DEDUP_PHASES + 1] = {};
+    // A wait for the peers outlasted "comm_timeout_ms" (wait_peers): work may still be queued
+    // or spinning on the stream against these buffers and this RCCL communicator, so every
+    // later call fails and destruction releases nothing (the host is expected to exit; its
+    // process teardown frees the device state).
+    bool broken = false;
+    std::string broken_why;
     ~sd_comm() {
+        if (broken) {
+            if (group) {
+                std::lock_guard<std::mutex> lk(group->mu);
+                group->joined[rank] = 0;
+            }
+            return;
+        }
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
         if (d_part_scratch) (void)hipFree(d_part_scratch);
@@ -103,6 +118,46 @@ void mark(sd_comm* c, int k, hipStream_t s) {
     if (!c->timing) return;
     if (!c->ev[k]) HIP_OK(hipEventCreate(&c->ev[k]));
     HIP_OK(hipEventRecord(c->ev[k], s));
+}
+
+// Waits for the work queued on `s` -- this call's collectives among it -- for at most
+// "comm_timeout_ms" (0 = no bound).  An RCCL kernel waits for its peers without limit, so a
+// peer rank that died or hung would otherwise keep this rank's host thread, and its GPU,
+// waiting forever.  On RCCL's asynchronous error or the deadline this rank reports
+// SD_ERR_COMM naming the step, and the communicator is marked broken (see sd_comm).  It is
+// not aborted: ncclCommAbort frees resources that kernels still queued behind the wait
+// would use.  The in-process transport has its own bounded barrier.
+void wait_peers(sd_comm* c, hipStream_t s, const char* step) {
+    const int ms = tuning_get(SD_TUNE_COMM_TIMEOUT_MS);
+    if (c->group || ms <= 0) {
+        HIP_OK(hipStreamSynchronize(s));
+        return;
+    }
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (int spin = 0;; spin++) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) HIP_OK(e);
+        ncclResult_t r = ncclSuccess;
+        NCCL_OK(ncclCommGetAsyncError(c->comm, &r));
+        const bool late = clk::now() - t0 > std::chrono::milliseconds(ms);
+        if ((r != ncclSuccess && r != ncclInProgress) || late) {
+            c->broken = true;
+            c->broken_why = std::string(step) + ": " +
+                            (late ? "the peers did not complete within comm_timeout_ms = " + std::to_string(ms)
+                                  : std::string("RCCL reported ") + ncclGetErrorString(r));
+            throw sd_failure(SD_ERR_COMM, "sd_cas_dedup_mgpu: " + c->broken_why +
+                                              " (the communicator is unusable from now on)");
+        }
+        // a short exchange finishes within microseconds: poll first, then sleep between polls
+        if (spin < 256) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+void check_usable(const sd_comm* c) {
+    if (c->broken) throw sd_failure(SD_ERR_COMM, "communicator broken by an earlier call (" + c->broken_why + ")");
 }
 
 // In-process all-gather of `bytes` per rank: rank p's block at `src` lands at dst + p * bytes
@@ -211,6 +266,7 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
         (capacity && (!d_records_out || !d_rep_out || !d_owner_out)))
         throw sd_failure(SD_ERR_INVALID, "null argument");
     if (chunk_size == 0) throw sd_failure(SD_ERR_INVALID, "chunk_size must be positive");
+    check_usable(comm);
     HIP_OK(hipSetDevice(comm->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int R = comm->nranks, me = comm->rank;
@@ -250,7 +306,7 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
         HIP_OK(hipMemcpyAsync(all, d_all, sizeof(uint64_t) * row * R, hipMemcpyDeviceToHost, s));
         mark(comm, 2, s);
     }
-    HIP_OK(hipStreamSynchronize(s));  // the one sync before the exchange: every rank's row
+    wait_peers(comm, s, "all-gather of the count rows");  // the sync before the exchange: every rank's row
     const ExchangePlan plan = exchange_plan(all, R, me);
     *m_out = plan.recv_total;
     *n_groups_out = 0;
@@ -288,6 +344,8 @@ int sd_cas_dedup_mgpu(sd_cas_ctx* ctx, sd_comm* comm, const uint8_t* d_hash32, c
         NCCL_OK(ncclGroupEnd());
     }
     mark(comm, 4, s);
+    // bounded, before the grouping's own (unbounded) sync for the group count
+    if (!comm->group) wait_peers(comm, s, "send/receive of the records");
     // 4. group by cas_id and assign Objects (chunk-of-100 rule) on the received records
     uint64_t ng = 0;
     dedup_group_owners(ctx, d_records_out, *m_out, plan.ascending ? SD_DEDUP_INDEX_SORTED : 0, d_rep_out, chunk_size,
@@ -344,6 +402,7 @@ int sd_split_checksum_mgpu(sd_cas_ctx* ctx, sd_comm* comm, sd_split_checksum* sp
     const SplitPlan& p = sd_split_plan_of(split);
     if (p.nranks != comm->nranks || p.rank != comm->rank)
         throw sd_failure(SD_ERR_INVALID, "the split's nranks / rank differ from the communicator's");
+    check_usable(comm);
     HIP_OK(hipSetDevice(comm->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     check_rc(sd_split_checksum_leaves(ctx, split, d_slice, d_cvs, stream));

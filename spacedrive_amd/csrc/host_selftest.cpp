@@ -1012,6 +1012,9 @@ void test_split_routes() {
     CHECK(sd_cas_set_tuning("checksum_hybrid_threads", keep + 1) == SD_OK && split_route_tuning_gen() == g0 + 1);
     CHECK(sd_cas_set_tuning("coalesce_window_us", 200) == SD_OK && split_route_tuning_gen() == g0 + 1);
     CHECK(sd_cas_set_tuning("checksum_hybrid_threads", keep) == SD_OK && split_route_tuning_gen() == g0 + 2);
+    // the RCCL exchange's bound on waiting for its peers: 5 minutes by default
+    int tmo = 0;
+    CHECK(sd_cas_get_tuning("comm_timeout_ms", &tmo) == SD_OK && tmo == 300000);
     // the co-hash cap scales with the budget
     CHECK(checksum_cohash_cap(16) == 13 && checksum_cohash_cap(8) == 6 && checksum_cohash_cap(4) == 3);
     CHECK(checksum_cohash_cap(2) == 1 && checksum_cohash_cap(1) == 0 && checksum_cohash_cap(32) == 26);

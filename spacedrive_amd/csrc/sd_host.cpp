@@ -43,8 +43,10 @@ thread_local std::string g_err;
 // ("numa_pin" 0: placing them on the GPU's node measured neutral with the page cache where
 // the writer left it, profiles/r4/r4h_numa_lib_probe.json); 15 host threads hashing beside the GPU in
 // large sd_cas_ids calls (profiles/r3/r3ad_cohash_probe.json: 300 000 files from pinned memory,
-// GPU alone 1.89-1.94 M files/s, CPU path alone 2.24-2.36 M, both at once 3.87-4.08 M)
-std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {6}, {15}, {0}, {1}, {0}, {256}, {1}, {8}};
+// GPU alone 1.89-1.94 M files/s, CPU path alone 2.24-2.36 M, both at once 3.87-4.08 M); a
+// 5-minute bound on every wait of the RCCL exchange for its peers (torch's own NCCL watchdog
+// waits 10)
+std::atomic<int> g_tune[SD_TUNE_NKEYS] = {{200}, {4096}, {32}, {1}, {16}, {16}, {6144}, {512}, {4096}, {4}, {2147483647}, {1}, {6}, {15}, {0}, {1}, {0}, {256}, {1}, {8}, {300000}};
 const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_max",    "files_window_mb",
                                                "dedup_variant",      "latency_cpu_max", "read_threads",
                                                "sampled_wave_max",   "whole_wave_max",  "batch_cpu_max",
@@ -52,7 +54,7 @@ const char* const TUNE_NAMES[SD_TUNE_NKEYS] = {"coalesce_window_us", "coalesce_m
                                                "checksum_hybrid_threads", "host_cohash_threads",
                                                "host_cpu_budget",    "checksum_stage_hot", "numa_pin",
                                                "cpu_read_piece_kib", "checksum_split_blocks",
-                                               "checksum_split_adapt"};
+                                               "checksum_split_adapt", "comm_timeout_ms"};
 
 bool read_small(const std::string& path, char* buf, size_t cap) {
     FILE* f = fopen(path.c_str(), "re");

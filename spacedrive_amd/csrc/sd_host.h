@@ -77,7 +77,8 @@ enum sd_tune_key {
     SD_TUNE_CPU_READ_PIECE_KIB = 17,       // CPU path: a 1 MiB block read and hashed in pieces of this size
     SD_TUNE_CHECKSUM_SPLIT_BLOCKS = 18,    // sd_file_checksums' split: 1 = claims by blocks, 0 = by files
     SD_TUNE_CHECKSUM_SPLIT_ADAPT = 19,     // split-eligible calls: 0 = always split, k = learn the faster route
-    SD_TUNE_NKEYS = 20
+    SD_TUNE_COMM_TIMEOUT_MS = 20,          // sd_cas_dedup_mgpu over RCCL: longest wait for the peers (0 = none)
+    SD_TUNE_NKEYS = 21
 };
 int tuning_get(int key);
 

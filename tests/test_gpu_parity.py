@@ -3,6 +3,7 @@
 Bit-exact on every byte: the full 32-byte BLAKE3 of every staged message, the 16-hex
 cas_id, the 64-hex checksum, and the dedup grouping.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -1239,6 +1240,53 @@ def test_dedup_mgpu_through_rccl_single_rank(ctx, rccl_comm):
     # the torch.distributed exchange path gives the same outputs
     r2, rep2, ng2, own2 = dedup.dedup_shard(ctx, d_hash, d_valid, n, base)
     assert ng2 == gng and np.array_equal(r2.cpu().numpy(), gr) and np.array_equal(own2.cpu().numpy(), want_owner)
+
+
+def test_dedup_mgpu_bounded_wait_breaks_the_comm(ctx):
+    """"comm_timeout_ms" (round 6): over RCCL every wait of sd_cas_dedup_mgpu for its peers
+    is bounded.  A host function that holds the call's stream stands in for a peer that never
+    arrives (no spinning kernel, no abort -- safe on a shared box): the call returns
+    SD_ERR_COMM naming the step within the bound, the communicator refuses every later call,
+    and once the stream is released its queued work drains and sd_comm_destroy returns."""
+    import threading
+    import time
+    import spacedrive_amd as sd
+    from spacedrive_amd import dedup
+    from spacedrive_amd._native import SdCasError
+    comm = dedup.make_comm(ctx)  # its own: the fixture's communicator stays usable
+    n = 5000
+    sizes, cids, twins = synth.library(0, n, n, dup_frac=0.3)
+    d_hash = torch.from_numpy(gpu_cas(ctx, sizes, cids, twins).copy()).cuda()
+    d_valid = torch.from_numpy((sizes != 0).astype(np.uint8)).cuda()
+    recs = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    rep = torch.empty(n, dtype=torch.int64, device="cuda")
+    own = torch.empty(n, dtype=torch.int64, device="cuda")
+    s = torch.cuda.Stream()
+    m, ng = ctx.dedup_mgpu(comm, d_hash, d_valid, n, 0, recs, rep, own, n, stream=s)  # a normal call
+    assert m == int((sizes != 0).sum()) and ng > 0
+    s.synchronize()
+    gate = threading.Event()
+    hold = ctypes.CFUNCTYPE(None, ctypes.c_void_p)(lambda _: gate.wait(60))
+    hip = ctypes.CDLL("libamdhip64.so")
+    keep = sd.get_tuning("comm_timeout_ms")
+    sd.set_tuning("comm_timeout_ms", 300)
+    try:
+        assert hip.hipLaunchHostFunc(ctypes.c_void_p(s.cuda_stream), hold, None) == 0
+        t0 = time.monotonic()
+        with pytest.raises(SdCasError) as e:
+            ctx.dedup_mgpu(comm, d_hash, d_valid, n, 0, recs, rep, own, n, stream=s)
+        waited = time.monotonic() - t0
+        assert e.value.rc == -5 and "all-gather of the count rows" in str(e.value), str(e.value)
+        assert "comm_timeout_ms = 300" in str(e.value) and 0.25 < waited < 20, waited
+    finally:
+        gate.set()
+        sd.set_tuning("comm_timeout_ms", keep)
+    s.synchronize()  # the call's queued partition and all-gather drain (one rank: RCCL to self)
+    with pytest.raises(SdCasError) as e2:
+        ctx.dedup_mgpu(comm, d_hash, d_valid, n, 0, recs, rep, own, n, stream=s)
+    assert e2.value.rc == -5 and "broken" in str(e2.value)
+    comm.close()  # a broken communicator releases nothing, and does not wait
+    assert keep == 300000
 
 
 def test_dedup_of_one_batch_beside_the_next_batchs_hashing(ctx, rccl_comm):
