@@ -688,6 +688,11 @@ def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1, lib_=None):
     return res
 
 
+def cohash_cap(budget: int) -> int:
+    """sd_checksums' co-hash thread cap under a host budget (sd_host.h checksum_cohash_cap)"""
+    return 0 if budget <= 1 else budget - max(1, (3 * budget + 8) // 16)
+
+
 def checksum_host(ctx, gib: int, dev, stream):
     """with-H2D checksums: `gib` GiB of pinned host memory (files of 1 GiB) through the
     drop-in sd_checksums, beside the raw H2D copy and the device-resident kernels."""
@@ -723,6 +728,10 @@ def checksum_host(ctx, gib: int, dev, stream):
         try:
             runs = []
             if mode == "default":
+                # the library's learned route (co-hashed or the CPU path alone, "checksum_split_adapt"):
+                # its four learning calls -- each route's warm-up and first counted call -- first
+                for _ in range(4):
+                    check(lib().sd_checksums(ctx.handle, host.data_ptr(), offs.ctypes.data, lens.ctypes.data, nf, out))
                 check(lib().sd_checksums_stats(ctx.handle, st0.ctypes.data))
             for _ in range(3):  # the first call allocates the context's windows
                 ctypes.memset(out, 0, 65 * nf)
@@ -739,6 +748,10 @@ def checksum_host(ctx, gib: int, dev, stream):
         e2e[mode] = min(runs)
     d_gpu, d_host = (int(x) for x in (st1 - st0))
     host_share = d_host / (d_gpu + d_host) if d_gpu + d_host else None
+    lv = np.zeros(4, np.float64)  # what this context learned (sd_checksums_learned)
+    check(lib().sd_checksums_learned(ctx.handle, lv.ctypes.data))
+    learned = {"cohash_GBps": float(lv[0]), "cpu_GBps": float(lv[1]), "cohash_calls": int(lv[2]),
+               "cpu_calls": int(lv[3])}
     e2e_s = e2e["default"]
     from oracle import native
     bad = sum(native.checksum_synth_mt(flen, 20_000 + i, 0, nthreads=oracle_threads()).hex() != got[i]
@@ -774,8 +787,8 @@ def checksum_host(ctx, gib: int, dev, stream):
     return {"files": nf, "bytes": total, "h2d_ms": h2d_ms, "h2d_GBps": total / (h2d_ms * 1e-3) / 1e9, "parity": par,
             "kernel_ms": kernel_ms, "kernel_GBps": total / (kernel_ms * 1e-3) / 1e9,
             "end_to_end_ms": e2e_s * 1e3, "end_to_end_GBps": total / e2e_s / 1e9,
-            "host_cohash_threads": max(0, min(keep, _native.host_cpu_budget()["budget"] - 3)),
-            "host_share": host_share,
+            "host_cohash_threads": max(0, min(keep, cohash_cap(_native.host_cpu_budget()["budget"]))),
+            "host_share": host_share, "learned": learned,
             "gpu_only": {"end_to_end_ms": e2e["gpu_only"] * 1e3, "end_to_end_GBps": total / e2e["gpu_only"] / 1e9},
             "library_cpu_path": {"threads": cpu_t, "GBps": total / min(cpu_runs) / 1e9,
                                  "parity": parity(nf, cpu_bad, "sd_cpu_checksums of each range vs sd_checksums' "

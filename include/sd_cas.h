@@ -233,12 +233,20 @@ int sd_checksum_batch_stats(const sd_checksum_batch* batch, uint64_t out[4]);
  * >= 1 GiB, "host_cohash_threads" host threads (default 15; 0 = GPU only) hash ranges from
  * the end on the CPU path meanwhile (ranges of >= 8 MiB block-parallel), the GPU taking
  * them from the front until the two meet; one range of >= 256 MiB, the one nearest the
- * predicted meeting point, is shared 1 MiB block by block. */
+ * predicted meeting point, is shared 1 MiB block by block.  Such a call
+ * ("checksum_split_adapt" k > 0, default 8) runs co-hashed or on the CPU path alone
+ * (sd_cpu_checksums on the host budget's threads), whichever this context has measured
+ * faster: each once (a warm-up call, then a counted one), then the faster by an EWMA of
+ * its GB/s, the other every k-th call; results are identical either way (round 6). */
 int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint64_t* lens, size_t n,
                  char* out_hex65);
-/* bytes sd_checksums hashed so far on this context: [0] by the GPU, [1] by the co-hashing
- * host threads (their share of a call: the host_share of the bench's with-H2D rows) */
+/* bytes sd_checksums hashed so far on this context: [0] by the GPU, [1] by host threads --
+ * the co-hashing threads, and every byte of a call the learned route sent to the CPU path
+ * (their share of a call: the host_share of the bench's with-H2D rows) */
 int sd_checksums_stats(sd_cas_ctx* ctx, uint64_t out[2]);
+/* what the context learned for sd_checksums' co-hash-eligible calls: [0] the co-hashed
+ * call's GB/s, [1] the CPU path's, [2] / [3] how many calls each was counted for */
+int sd_checksums_learned(sd_cas_ctx* ctx, double out[4]);
 /* Drop-in: checksums of n files on disk -> 65-byte lowercase hex each (hash.rs:21-23);
  * status[n] required.  Each file is read as hash.rs reads it: 1 MiB read calls until a
  * short one -- for a regular file its bytes up to EOF, read with parallel preads

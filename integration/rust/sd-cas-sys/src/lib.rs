@@ -85,6 +85,8 @@ extern "C" {
     pub fn sd_file_checksums_bytes(ctx: *mut sd_cas_ctx, out: *mut u64) -> c_int;
     // what the context learned for the split vs the CPU path ("checksum_split_adapt")
     pub fn sd_file_checksums_learned(ctx: *mut sd_cas_ctx, out: *mut f64) -> c_int;
+    // what the context learned for sd_checksums' co-hashed calls vs the CPU path alone
+    pub fn sd_checksums_learned(ctx: *mut sd_cas_ctx, out: *mut f64) -> c_int;
     // the CPU path (no device)
     pub fn sd_cpu_simd_lanes() -> c_int;
     pub fn sd_cpu_cas_ids_files(paths: *const *const c_char, sizes: *const u64, n: usize, out_hex17: *mut c_char,

@@ -124,6 +124,7 @@ SIGNATURES = [
     ("sd_file_checksums_routes", I32, [P, P]),
     ("sd_file_checksums_bytes", I32, [P, P]),
     ("sd_file_checksums_learned", I32, [P, P]),
+    ("sd_checksums_learned", I32, [P, P]),
     ("sd_cas_ids_stats", I32, [P, P]),
     ("sd_checksums_stats", I32, [P, P]),
     ("sd_read_probe", I32, [P, P, U64, I32, P]),

@@ -175,6 +175,14 @@ def file_checksums_learned(device: Optional[int] = None) -> dict:
     return {"split_GBps": float(v[0]), "cpu_GBps": float(v[1]), "split_calls": int(v[2]), "cpu_calls": int(v[3])}
 
 
+def checksums_learned(device: Optional[int] = None) -> dict:
+    """sd_checksums_learned: the GB/s the context learned for sd_checksums' co-hashed calls
+    and for the CPU path alone ("checksum_split_adapt"), and how many calls each was counted for."""
+    v = np.zeros(4, np.float64)
+    check(lib().sd_checksums_learned(default_context(device).handle, _ptr(v)))
+    return {"cohash_GBps": float(v[0]), "cpu_GBps": float(v[1]), "cohash_calls": int(v[2]), "cpu_calls": int(v[3])}
+
+
 def set_tuning(key: str, value: int) -> None:
     """sd_cas_set_tuning (process-wide knobs, include/sd_cas.h)."""
     check(lib().sd_cas_set_tuning(key.encode(), int(value)))

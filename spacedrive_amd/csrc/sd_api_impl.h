@@ -232,6 +232,10 @@ struct sd_cas_ctx {
     std::mutex split_mu;
     SplitRoutes split_routes;  // sd_file_checksums: the split or the CPU path, learned (sd_host.h)
     uint64_t split_routes_gen = 0;  // split_route_tuning_gen() the rates were learned under
+    // sd_checksums' co-hashed calls: the GPU + host threads, or the CPU path alone, learned
+    // the same way (route 0 = co-hash, 1 = CPU path; under split_mu)
+    SplitRoutes cohash_routes;
+    uint64_t cohash_routes_gen = 0;
     std::mutex pool_mu;
     // Reader threads.  stage_pool: tasks that open and close their own files (the cas
     // stager, checksum packs), on private fd tables (stage_pool.h); io_pool: parallel preads

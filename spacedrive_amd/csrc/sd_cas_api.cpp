@@ -604,6 +604,19 @@ int sd_file_checksums_learned(sd_cas_ctx* ctx, double out[4]) {
     SD_GUARD_END
 }
 
+int sd_checksums_learned(sd_cas_ctx* ctx, double out[4]) {
+    SD_GUARD_BEGIN
+    if (!ctx || !out) throw sd_failure(SD_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(ctx->split_mu);
+    const SplitRoutes& r = ctx->cohash_routes;
+    out[0] = r.rate[0];
+    out[1] = r.rate[1];
+    out[2] = (double)r.n[0];
+    out[3] = (double)r.n[1];
+    return SD_OK;
+    SD_GUARD_END
+}
+
 // ---------------------------------------------------------------------- checksums
 int sd_checksum_batch_create(sd_cas_ctx* ctx, const uint64_t* offsets, const uint64_t* lens, size_t n,
                              sd_checksum_batch** out) {

@@ -1167,6 +1167,43 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     for (size_t i = 0; i < n; i++)
         if (offsets[i] % 16) throw sd_failure(SD_ERR_INVALID, "range " + std::to_string(i) + " not 16-byte aligned");
     ctx->bind();
+    // Co-hashed calls (below) or the CPU path alone, learned per context as sd_file_checksums
+    // learns its split ("checksum_split_adapt" k, split_route_choose): the co-hashed call
+    // reaches 98 % of its two halves' sum on one host (13 threads + PCIe) and lost to 16
+    // threads alone on a host whose CPU path read 127 GB/s (0.95x, profiles/r6/r6f_*), so no
+    // fixed choice is right everywhere.  Calls are timed from here, either route.
+    const int cohash_cap = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS),
+                                                 checksum_cohash_cap(host_cpu_budget())}));
+    uint64_t call_bytes = 0;
+    for (size_t q = 0; q < n; q++) call_bytes += lens[q];
+    const int adapt = std::max(0, tuning_get(SD_TUNE_CHECKSUM_SPLIT_ADAPT));
+    const bool learn_route = adapt > 0 && cohash_cap > 0 && n && call_bytes >= (1ull << 30);
+    const auto t_call = std::chrono::steady_clock::now();
+    auto learn = [&](int route) {
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_call).count();
+        std::lock_guard<std::mutex> g(ctx->split_mu);
+        split_route_record(ctx->cohash_routes, route, (double)call_bytes / std::max(sec, 1e-9) / 1e9);
+    };
+    if (learn_route) {
+        int route;
+        {
+            std::lock_guard<std::mutex> g(ctx->split_mu);
+            const uint64_t gen = split_route_tuning_gen();
+            if (ctx->cohash_routes_gen != gen) {
+                ctx->cohash_routes = SplitRoutes{};
+                ctx->cohash_routes_gen = gen;
+            }
+            route = split_route_choose(ctx->cohash_routes, (uint32_t)adapt);
+        }
+        if (route == 1) {  // the CPU path alone, on the host budget's threads
+            std::vector<uint8_t> h32(32 * n);
+            check_rc(sd_cpu_checksums(data, offsets, lens, n, h32.data(), host_cpu_budget()));
+            for (size_t q = 0; q < n; q++) to_hex(h32.data() + 32 * q, 32, out_hex65 + 65 * q);
+            ctx->checksums_host_bytes.fetch_add(call_bytes, std::memory_order_relaxed);
+            learn(1);
+            return SD_OK;
+        }
+    }
     constexpr uint64_t W = Streamer::W;
     SlotPair slots(ctx);
     Streamer::prepare(slots);
@@ -1240,12 +1277,10 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     // at 15 the process burns 16.5 CPUs of time per call for fewer bytes (no throttled
     // periods: the contention is the cores', not the quota's).  The headroom scales with the
     // budget (an absolute 3 left one thread of a 4-CPU budget): 8 -> 6, 4 -> 3,
-    // 2 -> 1 (cohash_headroom, sd_host.h).  sd_cas_ids keeps budget - 1: there 15 measured
-    // best (4.86 vs 4.51 M files/s at 13, r5h_cohash_cas.json).
-    const int cohash = std::max(0, std::min({64, tuning_get(SD_TUNE_HOST_COHASH_THREADS),
-                                             checksum_cohash_cap(host_cpu_budget())}));
-    uint64_t all_bytes = 0;
-    for (size_t q = 0; q < n; q++) all_bytes += lens[q];
+    // 2 -> 1 (checksum_cohash_cap, sd_host.h).  sd_cas_ids keeps budget - 1: there 15
+    // measured best (4.86 vs 4.51 M files/s at 13, r5h_cohash_cas.json).
+    const int cohash = cohash_cap;
+    const uint64_t all_bytes = call_bytes;
     std::mutex claim_mu;
     size_t back = n, front = 0;  // [back, n) claimed by the host, [0, front) by the GPU loop
     constexpr uint64_t SHARED_MIN = 256ull << 20, HOST_UNIT = 64;  // bytes; blocks per host claim
@@ -1517,6 +1552,7 @@ int sd_checksums(sd_cas_ctx* ctx, const uint8_t* data, const uint64_t* offsets, 
     if (host_rc != SD_OK) throw sd_failure(host_rc, host_err);
     ctx->checksums_host_bytes.fetch_add(host_bytes.load(), std::memory_order_relaxed);
     ctx->checksums_gpu_bytes.fetch_add(all_bytes - std::min(all_bytes, host_bytes.load()), std::memory_order_relaxed);
+    if (learn_route) learn(0);
     return SD_OK;
     SD_GUARD_END
 }

@@ -500,7 +500,7 @@ int sd_cas_set_tuning(const char* key, int value) {
             switch (k) {  // keys the split / CPU-path rates depend on (split_route_tuning_gen)
                 case SD_TUNE_READ_THREADS: case SD_TUNE_CHECKSUM_HYBRID_THREADS: case SD_TUNE_HOST_CPU_BUDGET:
                 case SD_TUNE_CHECKSUM_SPLIT_BLOCKS: case SD_TUNE_CPU_READ_PIECE_KIB:
-                case SD_TUNE_CHECKSUM_STAGE_HOT: case SD_TUNE_NUMA_PIN:
+                case SD_TUNE_CHECKSUM_STAGE_HOT: case SD_TUNE_NUMA_PIN: case SD_TUNE_HOST_COHASH_THREADS:
                     if (was != value) g_split_gen.fetch_add(1, std::memory_order_relaxed);
                     break;
                 default: break;

@@ -452,8 +452,8 @@ int split_route_choose(const SplitRoutes& s, uint32_t explore_every);
 void split_route_record(SplitRoutes& s, int route, double gbps);
 // bumped by sd_cas_set_tuning when a key either route's rate depends on changes value
 // (read_threads, checksum_hybrid_threads, host_cpu_budget, checksum_split_blocks,
-// cpu_read_piece_kib, checksum_stage_hot, numa_pin): a context's learned rates from before
-// are dropped at its next split-eligible call
+// cpu_read_piece_kib, checksum_stage_hot, numa_pin, host_cohash_threads): a context's
+// learned rates from before are dropped at its next eligible call
 uint64_t split_route_tuning_gen();
 // co-hashing threads of a sd_checksums call under a host budget of b: b less 3/16 of it, at
 // least one less (16 -> 13, 8 -> 6, 4 -> 3, 2 -> 1, 1 -> 0)

@@ -105,6 +105,8 @@ def test_invalid_arguments_do_not_cross_boundary():
     out = (ctypes.c_double * 4)()
     rc = lib().sd_file_checksums_learned(None, out)  # no context: refused before any HIP call
     assert rc == -1 and b"null" in lib().sd_cas_last_error()
+    rc = lib().sd_checksums_learned(None, out)
+    assert rc == -1 and b"null" in lib().sd_cas_last_error()
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="GPU present")

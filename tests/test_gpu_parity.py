@@ -33,13 +33,17 @@ def ctx():
 @pytest.fixture(scope="module", autouse=True)
 def _gpu_route_for_batches():
     """sd_cas_ids_files hashes calls of up to "batch_cpu_max" files on the CPU path, and
-    sd_file_checksums calls of up to "checksum_cpu_max" (by default all); the parity tests
-    below exercise the GPU routes, so the module turns both policies off (the policies have
+    sd_file_checksums calls of up to "checksum_cpu_max" (by default all), and the learned
+    routes ("checksum_split_adapt") may send large calls to the CPU path; the parity tests
+    below exercise the GPU routes, so the module turns these policies off (the policies have
     their own tests) and restores the library defaults after."""
     import spacedrive_amd as sd
-    keep = {k: sd.get_tuning(k) for k in ("batch_cpu_max", "checksum_cpu_max")}
+    keep = {k: sd.get_tuning(k) for k in ("batch_cpu_max", "checksum_cpu_max", "checksum_split_adapt")}
     sd.set_tuning("batch_cpu_max", 0)
     sd.set_tuning("checksum_cpu_max", 0)  # sd_file_checksums: its GPU route (the default is the CPU path)
+    # sd_checksums' co-hashed calls and sd_file_checksums' split always take the GPU side
+    # (the learned routes have their own tests)
+    sd.set_tuning("checksum_split_adapt", 0)
     yield
     for k, v in keep.items():
         sd.set_tuning(k, v)
@@ -1410,6 +1414,55 @@ def test_checksums_from_host_memory_cohashed(ctx, oracle_native, cohash):
     d_gpu, d_host = (int(x) for x in (st1 - st0))
     assert d_gpu + d_host == sum(lens)
     assert (d_host > 0 and d_gpu > 0) if cohash else d_host == 0
+
+
+def test_checksums_learned_route(ctx, oracle_native):
+    """"checksum_split_adapt" k for sd_checksums (round 6): a co-hash-eligible call (>= 1 GiB)
+    runs co-hashed (the GPU + host threads) or on the CPU path alone, each once as a warm-up
+    and once counted, then the faster by its learned GB/s and the other every k-th call.
+    Every call's hashes equal the oracle's, whichever route ran; a CPU-route call hashes
+    every byte on the host (sd_checksums_stats), a co-hashed one gives the GPU a share."""
+    import spacedrive_amd as sd
+    from spacedrive_amd._native import check, lib
+    lens = [(300 << 20) + 5, 77, (400 << 20) + 1, 3 << 20, (360 << 20) + 3]
+    offs, off = [], 0
+    for L in lens:
+        offs.append(off)
+        off = (off + L + 128 + 127) // 128 * 128
+    assert sum(lens) >= 1 << 30
+    d = torch.randint(0, 256, (off + 64,), dtype=torch.uint8, device="cuda")
+    host = torch.empty(off + 64, dtype=torch.uint8, pin_memory=True)
+    host.copy_(d)
+    del d
+    arr_o, arr_l = np.array(offs, np.uint64), np.array(lens, np.uint64)
+    want = [w.tobytes().hex() for w in oracle_native.checksums_simd(host.numpy(), arr_o, arr_l, nthreads=NT)]
+    out = ctypes.create_string_buffer(65 * len(lens))
+    keep = {k: sd.get_tuning(k) for k in ("checksum_split_adapt", "host_cohash_threads")}
+    sd.set_tuning("host_cohash_threads", 14)  # a change of a key the rates depend on:
+    sd.set_tuning("host_cohash_threads", 15)  # the context learns afresh
+    sd.set_tuning("checksum_split_adapt", 2)
+    routes = []
+    try:
+        for _ in range(8):
+            st0, st1 = np.zeros(2, np.uint64), np.zeros(2, np.uint64)
+            check(lib().sd_checksums_stats(ctx.handle, st0.ctypes.data))
+            ctypes.memset(out, 0, 65 * len(lens))
+            check(lib().sd_checksums(ctx.handle, host.data_ptr(), arr_o.ctypes.data, arr_l.ctypes.data, len(lens),
+                                     out))
+            check(lib().sd_checksums_stats(ctx.handle, st1.ctypes.data))
+            raw = out.raw
+            assert [raw[65 * i:65 * i + 64].decode() for i in range(len(lens))] == want
+            d_gpu, d_host = (int(x) for x in (st1 - st0))
+            assert d_gpu + d_host == sum(lens)
+            routes.append("cpu" if d_gpu == 0 else "cohash")
+        learned = sd.checksums_learned()
+    finally:
+        for k, v in keep.items():
+            sd.set_tuning(k, v)
+    assert routes[:2] == ["cohash", "cohash"] and routes[2:4] == ["cpu", "cpu"], routes
+    assert learned["cohash_calls"] >= 1 and learned["cpu_calls"] >= 1 and learned["cohash_GBps"] > 0, learned
+    faster = "cohash" if learned["cohash_GBps"] >= learned["cpu_GBps"] else "cpu"
+    assert faster in routes[4:] and len(set(routes[4:])) == 2, routes  # k = 2: the other every 2nd call
 
 
 @pytest.mark.parametrize("cohash", [0, 15])
