@@ -583,6 +583,11 @@ def ev_ms(fn, stream, reps=1):
     return e0.elapsed_time(e1) / reps
 
 
+def _native_budget() -> int:
+    from spacedrive_amd._native import host_cpu_budget
+    return int(host_cpu_budget()["budget"])
+
+
 def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1, lib_=None):
     """with-H2D cas_ids: the first k files' staged messages in pinned host memory through
     the drop-in sd_cas_ids (host plan + H2D + kernels + D2H + hex, windows pipelined on two
@@ -625,7 +630,9 @@ def host_staged(ctx, ext, d_staged, k, dev, stream, world: int = 1, lib_=None):
             t0 = time.perf_counter()
             for _ in range(reps):
                 call()
-            e2e[mode] = ((time.perf_counter() - t0) / reps, h)
+            # the threads the library runs for h: at most the host budget less one (sd_cas_ids)
+            e2e[mode] = ((time.perf_counter() - t0) / reps,
+                         max(0, min(h, _native_budget() - 1)))
             check(lib().sd_cas_ids_stats(ctx.handle, s1.ctypes.data))
             e2e[mode] += (float((s1 - s0)[1]) / (reps * k),)
             if DIST:
@@ -1601,6 +1608,9 @@ def compact_line(out: dict, full_path: str = None) -> dict:
             "unit": "files/s" if "end_to_end_files_per_s" in v else "GB/s",
             "gpu_only": _g(v, "gpu_only", "end_to_end_files_per_s") or _g(v, "gpu_only", "end_to_end_GBps"),
             "h2d_GBps": v.get("h2d_GBps"), "kernel_ms": v.get("kernel_ms"), "host_share": v.get("host_share"),
+            "host_threads": v.get("host_cohash_threads"),
+            # N > 1: every rank at once, all ranks' files over the slowest rank's time
+            "aggregate_files_per_s": _g(v, "aggregate", "files_per_s"), "aggregate_GBps": _g(v, "aggregate", "GBps"),
             "parity": _par(v.get("parity"))})
     fb = out.get("file_backed")
     if fb:

@@ -87,6 +87,8 @@ def test_n8_line_keeps_balance_and_rccl():
     assert d["distributed"]["rccl_libs"]["one_rccl"] is True
     assert len(d["dedup"]["records_per_rank"]) == 8
     assert d["parity"]["full"] == [2_400_000, 0] and d["parity"]["ranks"] == 8
+    # the with-H2D leg runs on every rank at once: the line keeps the aggregate
+    assert d["legs"]["with_h2d_cas"]["aggregate_files_per_s"] > d["legs"]["with_h2d_cas"]["end_to_end"]
 
 
 def test_overlong_line_fails_loudly():
