@@ -321,6 +321,20 @@ def test_cas_sampled_batch_shapes(ctx, oracle_native, wave_max):
         lib().sd_cas_set_tuning(b"sampled_wave_max", 6144)
 
 
+def test_cas_huge_sampled_sizes(ctx, oracle_native):
+    """Sampled files far past 4 GiB, up to u64's maximum size: the device stager's sample
+    offsets (8192 + k * ((size - 16384) / 4), cas.rs:41-51), its footer at size - 8192 and the
+    le64 header in 64-bit arithmetic, then the sampled kernels -- bit-exact with the C
+    oracle, which tests/test_oracle.py pins to the Python spec at the same sizes."""
+    from tests.test_oracle import HUGE_SAMPLED
+    sizes = np.array(HUGE_SAMPLED * 40, np.uint64)  # 280 files: the throughput kernels' batch shape too
+    cids = np.arange(700, 700 + len(sizes), dtype=np.uint64) % np.uint64(len(HUGE_SAMPLED)) + np.uint64(700)
+    twins = np.zeros(len(sizes), np.uint32)
+    h = gpu_cas(ctx, sizes, cids, twins)
+    want = oracle_native.cas_ids_synth(sizes, cids, twins, nthreads=NT)
+    assert np.array_equal(h[:, :8], want)
+
+
 def test_sample_twins_and_duplicates(ctx):
     sizes = np.array([5 << 20, 5 << 20, 5 << 20, 3000, 3000], np.uint64)
     cids = np.array([1, 1, 1, 2, 2], np.uint64)

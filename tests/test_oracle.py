@@ -198,6 +198,25 @@ def test_synth_generator_c_vs_python(oracle_native, golden):
     assert oracle_native.synth_bytes(3, 5, 18430, 4) == cs.synth_bytes(3, 5, 18430, 4)
 
 
+HUGE_SAMPLED = [(1 << 32) - 1, (1 << 32) + 1, (1 << 33) + 7, (1 << 40) + 12345, (1 << 50) - 1, (1 << 62) + 3,
+                (1 << 64) - 1]
+
+
+def test_c_oracle_huge_sampled_sizes_vs_spec(oracle_native):
+    """Sampled files far past 4 GiB -- a 1 TiB video, sizes up to u64's maximum: the sample
+    offsets 8192 + k * ((size - 16384) / 4) (cas.rs:41-51), the footer at size - 8192
+    (cas.rs:54-57) and the le64 header all need 64-bit arithmetic.  The C oracle's cas
+    messages and cas_ids equal the Python spec's over the same synthetic content."""
+    sizes = np.array(HUGE_SAMPLED, np.uint64)
+    cids = np.arange(700, 700 + len(sizes), dtype=np.uint64)
+    ids = oracle_native.cas_ids_synth(sizes, cids, np.zeros(len(sizes), np.uint32), nthreads=2)
+    for i, size in enumerate(HUGE_SAMPLED):
+        msg = cs.cas_message(cs.synth_reader(int(cids[i])), size)
+        assert len(msg) == 57352 and msg[:8] == size.to_bytes(8, "little")
+        assert oracle_native.cas_message(int(cids[i]), 0, size) == msg, size
+        assert ids[i].tobytes().hex() == cs.generate_cas_id(cs.synth_reader(int(cids[i])), size), size
+
+
 @pytest.mark.parametrize("level", [1, 2])
 def test_c_oracle_simd_multichunk(oracle_native, level):
     # the CPU-baseline hasher (hash_many over chunks and parents) vs the scalar oracle
