@@ -279,3 +279,46 @@ def test_cpu_cas_id_of_a_pipe(tmp_path, oracle_native):
     finally:
         t.join()
     assert got == oracle_native.blake3(bytes(8) + data)[:8].hex()
+
+
+def _sparse_sampled(tmp_path, name, size, cid):
+    """a sparse file of `size` bytes holding the generator's bytes only where
+    generate_cas_id reads (cas.rs:31-58); None where the filesystem refuses the size"""
+    from spacedrive_amd import synth
+    p = str(tmp_path / name)
+    try:
+        with open(p, "wb") as f:
+            f.truncate(size)
+            for off, ln in synth.sample_windows(size):
+                f.seek(off)
+                f.write(cs.synth_bytes(cid, 0, off, ln))
+    except OSError:  # EFBIG: the filesystem's largest file
+        return None
+    return p
+
+
+def test_cpu_cas_ids_files_past_a_tebibyte(tmp_path, oracle_native):
+    """Sampled files of 1 TiB and more on disk (sparse), through the product's file readers
+    (the CPU path and the stager that feeds the GPU route): 64-bit pread offsets up to the
+    footer at size - 8192, equal to the Python spec and to the oracle's read schedule."""
+    sizes = [(1 << 40) + 12345, (1 << 42) + 3, (1 << 43) - 1]
+    made = [(s, _sparse_sampled(tmp_path, f"tb{i}", s, 990 + i)) for i, s in enumerate(sizes)]
+    made = [(s, p, 990 + i) for i, (s, p) in enumerate(made) if p]
+    if not made:
+        pytest.skip("the filesystem refuses files of 1 TiB")
+    paths = [p for _, p, _ in made]
+    szs = [s for s, _, _ in made]
+    want = [cs.generate_cas_id(cs.synth_reader(c), s) for s, _, c in made]
+    assert cpu.generate_cas_ids(paths, szs, nthreads=2) == want
+    got, st = oracle_native.cas_ids_files(paths, np.array(szs, np.uint64), nthreads=2)
+    assert not st.any() and [g.tobytes().hex() for g in got] == want
+    # the stager (sd_cas_stage_files: the GPU route's reader) stages the spec's messages
+    ext, total = stage_plan(np.array(szs, np.uint64))
+    staged = np.zeros(total + 64, np.uint8)
+    status = np.zeros(len(paths), np.int32)
+    arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+    check(lib().sd_cas_stage_files(arr, ext.ctypes.data, len(paths), staged.ctypes.data, status.ctypes.data, 2))
+    assert not status.any()
+    for i, (s, _, c) in enumerate(made):
+        o, L = int(ext["msg_offset"][i]), int(ext["msg_len"][i])
+        assert staged[o:o + L].tobytes() == cs.cas_message(cs.synth_reader(c), s)

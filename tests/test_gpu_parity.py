@@ -976,6 +976,24 @@ def test_file_api_past_4gib_sparse(ctx, tmp_path, oracle_native):
     assert sums[0] == want
 
 
+def test_file_api_past_a_tebibyte_sparse(ctx, tmp_path, oracle_native):
+    """Sampled files of 1-8 TiB (sparse) through the GPU route of sd_cas_ids_files and the
+    latency path: the stager's 64-bit reads up to the footer, then the kernels -- equal to
+    the Python spec (tests/test_cpu_path.py runs the CPU path and sd_cas_stage_files on the
+    same files)."""
+    import spacedrive_amd as sd
+    from tests.test_cpu_path import _sparse_sampled
+    sizes = [(1 << 40) + 12345, (1 << 42) + 3, (1 << 43) - 1]
+    made = [(s, _sparse_sampled(tmp_path, f"tb{i}", s, 990 + i), 990 + i) for i, s in enumerate(sizes)]
+    made = [m for m in made if m[1]]
+    if not made:
+        pytest.skip("the filesystem refuses files of 1 TiB")
+    paths, szs = [p for _, p, _ in made], [s for s, _, _ in made]
+    want = [cs.generate_cas_id(cs.synth_reader(c), s) for s, _, c in made]
+    assert sd.generate_cas_ids(paths, szs) == want  # the module sets batch_cpu_max 0: the GPU route
+    assert sd.generate_cas_id(paths[-1], szs[-1]) == want[-1]
+
+
 def test_dedup_owners_matches_torch_rule(ctx):
     """sd_dedup_owners (one kernel) == identifier.object_owners (the torch statement)."""
     from spacedrive_amd.identifier import object_owners
