@@ -12,6 +12,8 @@ import pytest
 from spacedrive_amd import _native
 from spacedrive_amd._native import SdCasError, check, lib
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def declared_functions():
     src = open(_native.HEADER).read()
@@ -359,3 +361,21 @@ def test_host_numa_without_a_context_places_nothing():
     assert keep == 0  # opt-in
     sd.set_tuning("numa_pin", 1)
     sd.set_tuning("numa_pin", keep)
+
+
+@pytest.mark.parametrize("lang,std", [("c", "-std=c99"), ("c", "-std=c11"), ("c++", "-std=c++11"), ("c++", "-std=c++17")])
+def test_header_compiles_strict(tmp_path, lang, std):
+    """include/sd_cas.h is the boundary a Rust (bindgen / hand-written extern "C"), C or C++
+    host includes: it compiles on its own under strict ISO modes with every warning an
+    error, and links against the in-tree library (every function a host would call
+    resolves)."""
+    src = tmp_path / ("t.c" if lang == "c" else "t.cpp")
+    src.write_text('#include "sd_cas.h"\n'
+                   "int main(void) { return sd_cas_abi_version() > 0 ? 0 : 1; }\n")
+    cc = "gcc" if lang == "c" else "g++"
+    lib_dir = os.path.join(ROOT, "spacedrive_amd")
+    r = subprocess.run([cc, std, "-pedantic", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                        str(src), "-L", lib_dir, "-lsdcas", "-Wl,-rpath," + lib_dir, "-o", str(tmp_path / "t")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert subprocess.run([str(tmp_path / "t")], timeout=60).returncode == 0
