@@ -49,6 +49,7 @@ def host_numa() -> list:
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    sd.set_tuning("checksum_split_adapt", 0)  # cohash_13 is always the co-hashed call (round 6's learned route off)
     ctx = sd.default_context(0)
     nf, flen = 4, 1 << 30
     total = nf * flen
