@@ -1549,7 +1549,6 @@ def compact_line(out: dict, full_path: str = None) -> dict:
     (the field glossary); `basis` codes name the peak's evidence.  Values are the full
     record's, rounded to 4 significant digits (the ones the value and ms_per_step keep)."""
     c = {k: out.get(k) for k in STD_KEYS}
-    c["value"], c["ms_per_step"] = out.get("value"), out.get("ms_per_step")
     r = out.get("roofline") or {}
     clock = r.get("clock") or {}
     c["roofline"] = _prune({
@@ -1657,7 +1656,10 @@ def compact_line(out: dict, full_path: str = None) -> dict:
     c["launch"] = out.get("launch")
     if full_path:
         c["full_record"] = full_path
-    return _sig(c)
+    c = _sig(c)
+    # the contract's numbers keep full precision (the driver's own consistency checks use them)
+    c["value"], c["ms_per_step"] = out.get("value"), out.get("ms_per_step")
+    return c
 
 
 def emit(out: dict, stream, full_path: str = None) -> str:

@@ -56,7 +56,7 @@ def test_line_fits_and_parses(which, tmp_path):
         assert k in d
     assert d["value"] > 0 and d["ms_per_step"] > 0 and d["n_gpus"] == out["n_gpus"]
     assert d["steps"] == out["steps"] and d["warmup"] == out["warmup"]
-    assert abs(d["value"] / out["value"] - 1) < 1e-3
+    assert d["value"] == out["value"] and d["ms_per_step"] == out["ms_per_step"]  # full precision
     assert list(d)[len(bench.STD_KEYS)] == "roofline"
     for k in ("frac", "frac_full_rate", "achieved", "peak", "kernel_ms", "bound", "unit"):
         assert k in d["roofline"], k
